@@ -1,0 +1,357 @@
+// Python bindings + native static-plan executor.
+//
+// The reference runs its static TF graph through TF's C++ executor
+// (MonitoredTrainingSession -> session.run(train_op)).  Here the
+// ResNet training step is likewise static, so it is recorded ONCE into a
+// `Plan`: a vector of launch closures with all pointers/shapes bound.  Running a
+// segment of the plan is a tight native loop of hipLaunchKernel calls on the
+// given stream (no Python per op); the whole step can additionally be captured
+// into a hipGraph (train/engine.py) which removes the host launch cost.
+//
+// Every op is exposed twice from one definition: as an immediate call
+// (`_C.conv_gemm(..., stream)`, used by ops/functional.py and the tests) and as
+// a plan recorder (`plan.conv_gemm(...)`).  Device pointers travel as Python
+// ints (tensor.data_ptr()); no torch headers are needed, which keeps this
+// extension small and fast to build.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "data.h"
+#include "kernels.h"
+#include "optim.h"
+
+namespace py = pybind11;
+using namespace dtr;
+
+typedef uintptr_t ptr_t;
+typedef std::function<void(hipStream_t)> Launch;
+
+template <typename T>
+static inline T* P(ptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+static inline hipStream_t S(ptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static ConvGeom geom_from(const std::vector<int>& v) {
+  if (v.size() != 11) throw std::invalid_argument("geom needs 11 ints: N,H,W,C,Ho,Wo,K,kh,kw,stride,pad");
+  return ConvGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10]};
+}
+
+// ---------------------------------------------------------------- op makers
+static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32, ptr_t residual,
+                           ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
+                           ptr_t stat_part, int accumulate, std::vector<int> geom) {
+  GemmArgs g{};
+  g.a = P<const bf16>(a);
+  g.b = P<const bf16>(b);
+  g.out = P<bf16>(out);
+  g.out_f32 = P<float>(out_f32);
+  g.residual = P<const bf16>(residual);
+  g.pre_scale = P<const float>(pre_scale);
+  g.pre_shift = P<const float>(pre_shift);
+  g.bias = P<const float>(bias);
+  g.nbias = nbias;
+  g.stat_part = P<float>(stat_part);
+  g.accumulate = accumulate;
+  g.g = geom_from(geom);
+  const ConvGeom& c = g.g;
+  const int taps = c.kh * c.kw;
+  if (mode == MODE_FWD) {
+    g.M = c.N * c.Ho * c.Wo;
+    g.Ncol = c.K;
+    g.Kdim = taps * c.C;
+    if (c.C % 8) throw std::invalid_argument("conv fwd: C must be a multiple of 8");
+  } else {
+    g.M = c.N * c.H * c.W;
+    g.Ncol = c.C;
+    g.Kdim = taps * c.K;
+    if (c.K % 8) throw std::invalid_argument("conv dgrad: K must be a multiple of 8");
+  }
+  if (g.Ncol % 16) throw std::invalid_argument("conv: output channels must be a multiple of 16");
+  if ((pre_scale != 0) && mode != MODE_FWD)
+    throw std::invalid_argument("fused BN+ReLU prologue is forward-only");
+  return [g, mode](hipStream_t s) { conv_gemm(g, mode, s); };
+}
+
+static Launch mk_conv_wgrad(ptr_t dy, ptr_t x, ptr_t pre_scale, ptr_t pre_shift, ptr_t part,
+                            std::vector<int> geom, int splits, int px_per_split) {
+  WgradArgs w{};
+  w.dy = P<const bf16>(dy);
+  w.x = P<const bf16>(x);
+  w.pre_scale = P<const float>(pre_scale);
+  w.pre_shift = P<const float>(pre_shift);
+  w.part = P<float>(part);
+  w.g = geom_from(geom);
+  w.splits = splits;
+  w.px_per_split = px_per_split;
+  if (w.g.C % 8 || w.g.K % 16) throw std::invalid_argument("wgrad: C%8 and K%16 required");
+  if (px_per_split % 64) throw std::invalid_argument("wgrad: px_per_split % 64");
+  return [w](hipStream_t s) { conv_wgrad(w, s); };
+}
+
+static Launch mk_wgrad_reduce(ptr_t part, ptr_t grad, int splits, int K, int K_valid, int taps,
+                              int C, int C_valid, float scale, int accumulate) {
+  return [=](hipStream_t s) {
+    wgrad_reduce(P<const float>(part), P<float>(grad), splits, K, K_valid, taps, C, C_valid, scale,
+                 accumulate, s);
+  };
+}
+
+static Launch mk_bn_finalize(ptr_t part, int tiles, int tile_rows, int M, int C, ptr_t gamma,
+                             ptr_t beta, ptr_t mmean, ptr_t mvar, float momentum, float eps,
+                             int update_moving, ptr_t mean, ptr_t rstd, ptr_t scale,
+                             ptr_t shift) {
+  return [=](hipStream_t s) {
+    bn_finalize(P<const float>(part), tiles, tile_rows, M, C, P<const float>(gamma),
+                P<const float>(beta), P<float>(mmean), P<float>(mvar), momentum, eps,
+                update_moving, P<float>(mean), P<float>(rstd), P<float>(scale), P<float>(shift),
+                s);
+  };
+}
+
+static Launch mk_bn_eval(ptr_t gamma, ptr_t beta, ptr_t mm, ptr_t mv, float eps, int C,
+                         ptr_t scale, ptr_t shift) {
+  return [=](hipStream_t s) {
+    bn_scale_shift_eval(P<const float>(gamma), P<const float>(beta), P<const float>(mm),
+                        P<const float>(mv), eps, C, P<float>(scale), P<float>(shift), s);
+  };
+}
+
+static Launch mk_bn_stats(ptr_t x, int M, int C, ptr_t part) {
+  if (C % 8 || C > 2048) throw std::invalid_argument("bn_stats: C%8==0 and C<=2048");
+  return [=](hipStream_t s) { bn_stats(P<const bf16>(x), M, C, P<float>(part), s); };
+}
+
+static Launch mk_bn_bwd_reduce(ptr_t dy, ptr_t x, ptr_t mean, ptr_t rstd, ptr_t scale,
+                               ptr_t shift, int M, int C, ptr_t part) {
+  if (C % 8 || C > 2048) throw std::invalid_argument("bn bwd: C%8==0 and C<=2048");
+  return [=](hipStream_t s) {
+    bn_relu_bwd_reduce(P<const bf16>(dy), P<const bf16>(x), P<const float>(mean),
+                       P<const float>(rstd), P<const float>(scale), P<const float>(shift), M, C,
+                       P<float>(part), nullptr, s);
+  };
+}
+
+static Launch mk_bn_bwd_finalize(ptr_t part, int tiles, int M, int C, ptr_t gamma, ptr_t rstd,
+                                 ptr_t dgamma, ptr_t dbeta, ptr_t coef) {
+  return [=](hipStream_t s) {
+    bn_bwd_finalize(P<const float>(part), tiles, M, C, P<const float>(gamma),
+                    P<const float>(rstd), P<float>(dgamma), P<float>(dbeta), P<float>(coef), s);
+  };
+}
+
+static Launch mk_bn_bwd_apply(ptr_t dy, ptr_t x, ptr_t mean, ptr_t rstd, ptr_t scale,
+                              ptr_t shift, ptr_t coef, ptr_t add, ptr_t dx, int M, int C) {
+  return [=](hipStream_t s) {
+    bn_relu_bwd_apply(P<const bf16>(dy), P<const bf16>(x), P<const float>(mean),
+                      P<const float>(rstd), P<const float>(scale), P<const float>(shift),
+                      P<const float>(coef), P<const bf16>(add), P<bf16>(dx), M, C, s);
+  };
+}
+
+static Launch mk_bn_relu_apply(ptr_t x, ptr_t scale, ptr_t shift, ptr_t y, int M, int C) {
+  return [=](hipStream_t s) {
+    bn_relu_apply(P<const bf16>(x), P<const float>(scale), P<const float>(shift), P<bf16>(y), M,
+                  C, s);
+  };
+}
+
+static Launch mk_bnrelu_avgpool(ptr_t x, ptr_t scale, ptr_t shift, ptr_t pooled, int N, int HW,
+                                int C) {
+  if (C % 8 || C > 2048) throw std::invalid_argument("avgpool: C%8==0 and C<=2048");
+  return [=](hipStream_t s) {
+    bnrelu_avgpool(P<const bf16>(x), P<const float>(scale), P<const float>(shift),
+                   P<bf16>(pooled), N, HW, C, s);
+  };
+}
+
+static Launch mk_avgpool_bwd(ptr_t dp, ptr_t dx, int N, int HW, int C) {
+  return [=](hipStream_t s) { avgpool_bwd(P<const bf16>(dp), P<bf16>(dx), N, HW, C, s); };
+}
+
+static Launch mk_softmax_xent(ptr_t logits, int ld, ptr_t labels, int N, int classes,
+                              ptr_t loss_sum, ptr_t correct, ptr_t dlogits, ptr_t dbias,
+                              float grad_scale, ptr_t probs) {
+  return [=](hipStream_t s) {
+    softmax_xent(P<const float>(logits), ld, P<const int>(labels), N, classes, P<float>(loss_sum),
+                 P<float>(correct), P<bf16>(dlogits), P<float>(dbias), grad_scale,
+                 P<float>(probs), s);
+  };
+}
+
+static Launch mk_maxpool_fwd(ptr_t x, ptr_t y, std::vector<int> geom, int k) {
+  ConvGeom g = geom_from(geom);
+  return [=](hipStream_t s) {
+    maxpool_fwd(P<const bf16>(x), P<bf16>(y), g.N, g.H, g.W, g.C, g.Ho, g.Wo, k, g.stride, g.pad,
+                s);
+  };
+}
+
+static Launch mk_maxpool_bwd(ptr_t x, ptr_t dy, ptr_t dx, std::vector<int> geom, int k) {
+  ConvGeom g = geom_from(geom);
+  return [=](hipStream_t s) {
+    maxpool_bwd(P<const bf16>(x), P<const bf16>(dy), P<bf16>(dx), g.N, g.H, g.W, g.C, g.Ho, g.Wo,
+                k, g.stride, g.pad, s);
+  };
+}
+
+static LrSchedule make_sched(float init, long long warm_steps, float warm_from, float warm_to,
+                             std::vector<long long> bounds, std::vector<float> vals) {
+  LrSchedule sc{};
+  if (bounds.size() > 7 || vals.size() != bounds.size() + 1)
+    throw std::invalid_argument("lr schedule: <=7 bounds and len(vals)==len(bounds)+1");
+  sc.init = init;
+  sc.warm_steps = warm_steps;
+  sc.warm_from = warm_from;
+  sc.warm_to = warm_to;
+  sc.nb = (int)bounds.size();
+  for (size_t i = 0; i < bounds.size(); ++i) sc.bound[i] = bounds[i];
+  for (size_t i = 0; i < vals.size(); ++i) sc.val[i] = vals[i];
+  return sc;
+}
+
+static Launch mk_sgd_update_pack(ptr_t master, ptr_t grad, ptr_t mom, long n, float init,
+                                 long long warm_steps, float warm_from, float warm_to,
+                                 std::vector<long long> bounds, std::vector<float> vals,
+                                 ptr_t gstep, float momentum, float wd, float grad_scale,
+                                 int use_momentum, ptr_t segs, int nseg, ptr_t bf, ptr_t lr_out,
+                                 int update) {
+  const LrSchedule sc = make_sched(init, warm_steps, warm_from, warm_to, bounds, vals);
+  return [=](hipStream_t s) {
+    sgd_update_pack(P<float>(master), P<const float>(grad), P<float>(mom), n, sc,
+                    P<const long long>(gstep), momentum, wd, grad_scale, use_momentum,
+                    P<const ParamSeg>(segs), nseg, P<bf16>(bf), P<float>(lr_out), update, s);
+  };
+}
+
+static Launch mk_step_increment(ptr_t gstep) {
+  return [=](hipStream_t s) { step_increment(P<long long>(gstep), s); };
+}
+
+static Launch mk_l2_half_sum(ptr_t v, long n, ptr_t ws, ptr_t out) {
+  return [=](hipStream_t s) { l2_half_sum(P<const float>(v), n, P<float>(ws), P<float>(out), s); };
+}
+
+static Launch mk_fill(ptr_t p, long n, float a) {
+  return [=](hipStream_t s) { fill_f32(P<float>(p), n, a, s); };
+}
+
+static Launch mk_memset(ptr_t p, long bytes) {
+  return [=](hipStream_t s) {
+    if (hipMemsetAsync(P<void>(p), 0, (size_t)bytes, s) != hipSuccess)
+      fprintf(stderr, "hipMemsetAsync failed\n");
+  };
+}
+
+static Launch mk_cifar_augment(ptr_t img, ptr_t out, int N, int H, int W, int Cpad, int pad,
+                               unsigned long long seed, ptr_t gstep, int train, ptr_t crop_log) {
+  return [=](hipStream_t s) {
+    cifar_augment(P<const uint8_t>(img), P<bf16>(out), N, H, W, Cpad, pad, seed,
+                  P<const long long>(gstep), train, P<int>(crop_log), s);
+  };
+}
+
+static Launch mk_pad_channels(ptr_t x, ptr_t out, long npix, int C, int Cpad) {
+  return [=](hipStream_t s) { nhwc_pad_channels(P<const float>(x), P<bf16>(out), npix, C, Cpad, s); };
+}
+
+static Launch mk_synthetic(ptr_t out, long npix, int C, int Cpad, unsigned long long seed) {
+  return [=](hipStream_t s) { synthetic_images(P<bf16>(out), npix, C, Cpad, seed, s); };
+}
+
+static Launch mk_cast_f2b(ptr_t a, ptr_t b, long n) {
+  return [=](hipStream_t s) { cast_f32_bf16(P<const float>(a), P<bf16>(b), n, s); };
+}
+static Launch mk_cast_b2f(ptr_t a, ptr_t b, long n) {
+  return [=](hipStream_t s) { cast_bf16_f32(P<const bf16>(a), P<float>(b), n, s); };
+}
+
+// ---------------------------------------------------------------- Plan
+struct Plan {
+  std::vector<Launch> ops;
+  std::vector<std::string> names;
+  int add(Launch l, const std::string& name) {
+    ops.push_back(std::move(l));
+    names.push_back(name);
+    return (int)ops.size() - 1;
+  }
+  void run(int begin, int end, ptr_t stream) {
+    if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
+    hipStream_t s = S(stream);
+    py::gil_scoped_release nogil;
+    for (int i = begin; i < end; ++i) ops[i](s);
+  }
+  int size() const { return (int)ops.size(); }
+};
+
+// Register `name` both as an immediate op (trailing stream arg) and as a Plan
+// recorder (returns the op index).
+template <typename R, typename... Args>
+static void def_op(py::module_& m, py::class_<Plan>& plan, const char* name,
+                   R (*maker)(Args...)) {
+  m.def(name, [maker](Args... args, ptr_t stream) { maker(args...)(S(stream)); });
+  plan.def(name, [maker, name](Plan& p, Args... args) { return p.add(maker(args...), name); });
+}
+
+static int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gfx950 (MI355X) native kernels + static-plan executor for ResNet training";
+  py::class_<Plan> plan(m, "Plan");
+  plan.def(py::init<>())
+      .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"))
+      .def("size", &Plan::size)
+      .def("names", [](const Plan& p) { return p.names; });
+
+  def_op(m, plan, "conv_gemm", mk_conv_gemm);
+  def_op(m, plan, "conv_wgrad", mk_conv_wgrad);
+  def_op(m, plan, "wgrad_reduce", mk_wgrad_reduce);
+  def_op(m, plan, "bn_finalize", mk_bn_finalize);
+  def_op(m, plan, "bn_eval", mk_bn_eval);
+  def_op(m, plan, "bn_stats", mk_bn_stats);
+  def_op(m, plan, "bn_bwd_reduce", mk_bn_bwd_reduce);
+  def_op(m, plan, "bn_bwd_finalize", mk_bn_bwd_finalize);
+  def_op(m, plan, "bn_bwd_apply", mk_bn_bwd_apply);
+  def_op(m, plan, "bn_relu_apply", mk_bn_relu_apply);
+  def_op(m, plan, "bnrelu_avgpool", mk_bnrelu_avgpool);
+  def_op(m, plan, "avgpool_bwd", mk_avgpool_bwd);
+  def_op(m, plan, "softmax_xent", mk_softmax_xent);
+  def_op(m, plan, "maxpool_fwd", mk_maxpool_fwd);
+  def_op(m, plan, "maxpool_bwd", mk_maxpool_bwd);
+  def_op(m, plan, "sgd_update_pack", mk_sgd_update_pack);
+  def_op(m, plan, "step_increment", mk_step_increment);
+  def_op(m, plan, "l2_half_sum", mk_l2_half_sum);
+  def_op(m, plan, "fill", mk_fill);
+  def_op(m, plan, "memset", mk_memset);
+  def_op(m, plan, "cifar_augment", mk_cifar_augment);
+  def_op(m, plan, "pad_channels", mk_pad_channels);
+  def_op(m, plan, "synthetic_images", mk_synthetic);
+  def_op(m, plan, "cast_f32_bf16", mk_cast_f2b);
+  def_op(m, plan, "cast_bf16_f32", mk_cast_b2f);
+
+  // host-side helpers that mirror the launchers' internal choices
+  m.def("conv_gemm_bm", &conv_gemm_bm);
+  m.def("bn_bwd_tiles", &bn_bwd_tiles);
+  m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
+  m.def("l2_workspace_floats", &l2_workspace_floats);
+  m.def("wgrad_pick_splits", [](std::vector<int> geom) {
+    int pps = 0;
+    const int sp = wgrad_pick_splits(geom_from(geom), &pps);
+    return py::make_tuple(sp, pps);
+  });
+  m.def("param_seg_bytes", []() { return (int)sizeof(ParamSeg); });
+  m.def("device_count", &hip_device_count);
+  m.def("device_synchronize", []() {
+    py::gil_scoped_release nogil;
+    return (int)hipDeviceSynchronize();
+  });
+}

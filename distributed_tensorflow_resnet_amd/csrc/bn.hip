@@ -1,0 +1,340 @@
+// Training-mode BatchNorm + ReLU for NHWC bf16 activations (replaces TF's
+// FusedBatchNorm / FusedBatchNormGrad / Relu / ReluGrad / AssignSub, SURVEY §2.5;
+// semantics of `batch_norm_relu`, resnet_model_official.py:41-50: decay 0.997,
+// eps 1e-5, moving variance fed with the Bessel-corrected batch variance).
+//
+// Forward statistics come as per-tile Welford partials (mean, M2) -- either from
+// the producing convolution's epilogue (conv_gemm STATS) or from bn_stats below
+// -- and are combined deterministically with Chan's parallel formula.  The
+// normalisation itself is never a separate pass: consumers apply
+// relu(x*scale+shift) while staging their operands.
+//
+// Backward: g = dy * [x*scale+shift > 0];  dbeta = sum g;  dgamma = sum g*xhat;
+//   dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat))   (+ residual gradient).
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+struct Welford {
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Welford wcombine(Welford a, Welford b) {
+  const float n = a.n + b.n;
+  if (n <= 0.f) return a;
+  const float d = b.mean - a.mean;
+  const float fb = b.n / n;
+  Welford r;
+  r.n = n;
+  r.mean = a.mean + d * fb;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * fb;
+  return r;
+}
+
+// One block per channel: thread t folds tiles t, t+256, ... then a fixed-shape
+// LDS tree -- bitwise deterministic.
+__global__ void __launch_bounds__(256)
+bn_finalize_kernel(const float* __restrict__ part, int tiles, int tile_rows, int M, int C,
+                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                   float* moving_mean, float* moving_var, float momentum, float eps,
+                   int update_moving, float* mean_out, float* rstd_out, float* scale_out,
+                   float* shift_out) {
+  __shared__ float sn[256], sm[256], s2[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  Welford w{0.f, 0.f, 0.f};
+  for (int t = tid; t < tiles; t += 256) {
+    Welford b;
+    b.n = (float)min(tile_rows, M - t * tile_rows);
+    b.mean = part[(long)t * 2 * C + c];
+    b.m2 = part[(long)t * 2 * C + C + c];
+    w = wcombine(w, b);
+  }
+  sn[tid] = w.n;
+  sm[tid] = w.mean;
+  s2[tid] = w.m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      Welford a{sn[tid], sm[tid], s2[tid]}, b{sn[tid + o], sm[tid + o], s2[tid + o]};
+      a = wcombine(a, b);
+      sn[tid] = a.n;
+      sm[tid] = a.mean;
+      s2[tid] = a.m2;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float n = sn[0], mean = sm[0], m2 = s2[0];
+    const float var = m2 / n;
+    const float rstd = rsqrtf(var + eps);
+    const float sc = gamma[c] * rstd;
+    mean_out[c] = mean;
+    rstd_out[c] = rstd;
+    scale_out[c] = sc;
+    shift_out[c] = beta[c] - mean * sc;
+    if (update_moving) {
+      const float uvar = n > 1.f ? m2 / (n - 1.f) : m2;
+      moving_mean[c] -= (1.f - momentum) * (moving_mean[c] - mean);
+      moving_var[c] -= (1.f - momentum) * (moving_var[c] - uvar);
+    }
+  }
+}
+
+void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
+                 const float* gamma, const float* beta, float* moving_mean, float* moving_var,
+                 float momentum, float eps, int update_moving, float* mean, float* rstd,
+                 float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, s, stat_part, tiles, tile_rows,
+                     M, C, gamma, beta, moving_mean, moving_var, momentum, eps, update_moving,
+                     mean, rstd, scale, shift);
+  DTR_CHECK_LAUNCH();
+}
+
+__global__ void bn_eval_kernel(const float* gamma, const float* beta, const float* mm,
+                               const float* mv, float eps, int C, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const float sc = gamma[c] * rsqrtf(mv[c] + eps);
+    scale[c] = sc;
+    shift[c] = beta[c] - mm[c] * sc;
+  }
+}
+
+void bn_scale_shift_eval(const float* gamma, const float* beta, const float* moving_mean,
+                         const float* moving_var, float eps, int C, float* scale, float* shift,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, s, gamma, beta,
+                     moving_mean, moving_var, eps, C, scale, shift);
+  DTR_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Row-tiled reductions over [M][C] bf16: each thread owns one 8-channel group
+// (16-B vector loads) of a subset of rows.  Tile = BN_TILE_ROWS rows.
+// ---------------------------------------------------------------------------
+static constexpr int BN_TILE_ROWS = 256;
+
+int bn_bwd_tiles(int M, int C) { return (M + BN_TILE_ROWS - 1) / BN_TILE_ROWS; }
+int bn_stats_tile_rows() { return BN_TILE_ROWS; }
+
+// Standalone forward stats (for BN inputs not produced by a conv, e.g. after
+// max-pool).  Two passes over the tile (the second from L1/L2) -> (mean, M2).
+__global__ void __launch_bounds__(256)
+bn_stats_kernel(const bf16* __restrict__ x, int M, int C, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [256/groups][C]... reused
+  const int G = C / 8;                 // channel groups
+  const int tid = threadIdx.x;
+  const int rows_per_iter = 256 / G;   // C <= 2048 -> G <= 256
+  const int grp = tid % G, rsub = tid / G;
+  const int r0 = blockIdx.x * BN_TILE_ROWS;
+  const int r1 = min(M, r0 + BN_TILE_ROWS);
+  const bool active = rsub < rows_per_iter;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (active)
+    for (int r = r0 + rsub; r < r1; r += rows_per_iter) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)r * C + grp * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+    }
+  // reduce over rsub via LDS: red[rsub][C]
+  float* buf = red;
+  if (active)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) buf[rsub * C + grp * 8 + j] = s[j];
+  __syncthreads();
+  const float n = (float)(r1 - r0);
+  for (int c = tid; c < C; c += 256) {
+    float t = 0.f;
+    for (int k = 0; k < rows_per_iter; ++k) t += buf[k * C + c];
+    buf[rows_per_iter * C + c] = t / n;   // mean stored after the partial rows
+  }
+  __syncthreads();
+  float mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = buf[rows_per_iter * C + grp * 8 + j];
+  float q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (active)
+    for (int r = r0 + rsub; r < r1; r += rows_per_iter) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)r * C + grp * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)v[j] - mu[j];
+        q[j] += d * d;
+      }
+    }
+  __syncthreads();
+  if (active)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) buf[rsub * C + grp * 8 + j] = q[j];
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float t = 0.f;
+    for (int k = 0; k < rows_per_iter; ++k) t += buf[k * C + c];
+    part[(long)blockIdx.x * 2 * C + c] = buf[rows_per_iter * C + c];
+    part[(long)blockIdx.x * 2 * C + C + c] = t;
+  }
+}
+
+void bn_stats(const bf16* x, int M, int C, float* part, hipStream_t s) {
+  const int G = C / 8;
+  const int rpi = 256 / G;
+  const size_t lds = (size_t)(rpi + 1) * C * sizeof(float);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(bn_bwd_tiles(M, C)), dim3(256), lds, s, x, M, C,
+                     part);
+  DTR_CHECK_LAUNCH();
+}
+
+// Backward reduction: per tile sums of g and g*xhat, g = dy*[relu active].
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                     const float* __restrict__ scale, const float* __restrict__ shift, int M,
+                     int C, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int G = C / 8, tid = threadIdx.x;
+  const int rows_per_iter = 256 / G;
+  const int grp = tid % G, rsub = tid / G;
+  const int r0 = blockIdx.x * BN_TILE_ROWS, r1 = min(M, r0 + BN_TILE_ROWS);
+  const bool active = rsub < rows_per_iter;
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], rs[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = grp * 8 + j;
+    mu[j] = active ? mean[c] : 0.f;
+    rs[j] = active ? rstd[c] : 0.f;
+    sc[j] = active ? scale[c] : 0.f;
+    sh[j] = active ? shift[c] : 0.f;
+  }
+  if (active)
+    for (int r = r0 + rsub; r < r1; r += rows_per_iter) {
+      const long o = (long)r * C + grp * 8;
+      const bf16x8 d = *reinterpret_cast<const bf16x8*>(dy + o);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = (float)v[j];
+        const float gg = (xv * sc[j] + sh[j] > 0.f) ? (float)d[j] : 0.f;
+        sg[j] += gg;
+        sgx[j] += gg * (xv - mu[j]) * rs[j];
+      }
+    }
+  if (active)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[rsub * 2 * C + grp * 8 + j] = sg[j];
+      red[rsub * 2 * C + C + grp * 8 + j] = sgx[j];
+    }
+  __syncthreads();
+  for (int c = tid; c < 2 * C; c += 256) {
+    float t = 0.f;
+    for (int k = 0; k < rows_per_iter; ++k) t += red[k * 2 * C + c];
+    part[(long)blockIdx.x * 2 * C + c] = t;
+  }
+}
+
+void bn_relu_bwd_reduce(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                        const float* scale, const float* shift, int M, int C, float* part,
+                        int* tiles_out, hipStream_t s) {
+  const int G = C / 8, rpi = 256 / G;
+  const size_t lds = (size_t)rpi * 2 * C * sizeof(float);
+  const int tiles = bn_bwd_tiles(M, C);
+  if (tiles_out) *tiles_out = tiles;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(tiles), dim3(256), lds, s, dy, x, mean, rstd,
+                     scale, shift, M, C, part);
+  DTR_CHECK_LAUNCH();
+}
+
+// dgamma/dbeta (accumulated into the flat gradient) + apply coefficients.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ rstd, float* dgamma,
+                                       float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sg = 0.f, sgx = 0.f;
+  for (int t = 0; t < tiles; ++t) {
+    sg += part[(long)t * 2 * C + c];
+    sgx += part[(long)t * 2 * C + C + c];
+  }
+  dbeta[c] = sg;
+  dgamma[c] = sgx;
+  const float a = gamma[c] * rstd[c];
+  coef[c] = a;
+  coef[C + c] = a * sg / (float)M;
+  coef[2 * C + c] = a * sgx / (float)M;
+}
+
+void bn_bwd_finalize(const float* part, int tiles, int M, int C, const float* gamma,
+                     const float* rstd, float* dgamma, float* dbeta, float* coef,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, part, tiles,
+                     M, C, gamma, rstd, dgamma, dbeta, coef);
+  DTR_CHECK_LAUNCH();
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                    const float* __restrict__ scale, const float* __restrict__ shift,
+                    const float* __restrict__ coef, const bf16* __restrict__ add,
+                    bf16* __restrict__ dx, long nvec, int C) {
+  const int G = C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % G) * 8;
+    const long o = i * 8;
+    const bf16x8 d = *reinterpret_cast<const bf16x8*>(dy + o);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + o);
+    bf16x8 ad = {};
+    if (add) ad = *reinterpret_cast<const bf16x8*>(add + o);
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xv = (float)v[j];
+      const float gg = (xv * scale[c] + shift[c] > 0.f) ? (float)d[j] : 0.f;
+      const float xh = (xv - mean[c]) * rstd[c];
+      float o2 = coef[c] * gg - coef[C + c] - coef[2 * C + c] * xh;
+      if (add) o2 += (float)ad[j];
+      r[j] = (bf16)o2;
+    }
+    *reinterpret_cast<bf16x8*>(dx + o) = r;
+  }
+}
+
+void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                       const float* scale, const float* shift, const float* coef,
+                       const bf16* add, bf16* dx, int M, int C, hipStream_t s) {
+  const long nvec = (long)M * C / 8;
+  long blocks = (nvec + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dy, x, mean,
+                     rstd, scale, shift, coef, add, dx, nvec, C);
+  DTR_CHECK_LAUNCH();
+}
+
+__global__ void bn_relu_apply_kernel(const bf16* __restrict__ x, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, bf16* __restrict__ y,
+                                     long nvec, int C) {
+  const int G = C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % G) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    *reinterpret_cast<bf16x8*>(y + i * 8) = affine_relu8(v, scale + c0, shift + c0);
+  }
+}
+
+void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M, int C,
+                   hipStream_t s) {
+  const long nvec = (long)M * C / 8;
+  long blocks = (nvec + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, scale,
+                     shift, y, nvec, C);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

@@ -1,0 +1,76 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// Everything here is wave64 / MFMA-first: vector types match the register
+// footprint of `v_mfma_f32_16x16x32_bf16` operands (8 x bf16 = 4 VGPRs) and
+// accumulators (4 x f32).  No CUDA-compat shims: HIP on gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtr {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+static constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32 (RNE, NaN-safe)
+
+__device__ __forceinline__ float bits2f(unsigned short u) {
+  return __uint_as_float(((unsigned)u) << 16);
+}
+
+// D = A(16x32) * B(32x16) + C, bf16 inputs, fp32 accumulate.
+// Lane l holds A[l&15][8*(l>>4)+j] and B[8*(l>>4)+j][l&15], j=0..7;
+// C/D: col = l&15, row = 4*(l>>4)+i.
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// gfx950 transposed LDS read: per 16-lane group, lane 4q+p supplies the address
+// of row q, columns 4p..4p+3 of a 4x16 block of 16-bit values; lane i receives
+// column i of the 4 rows (row q in element q).
+__device__ __forceinline__ s16x4 lds_read_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 8 bf16 <-> 8 float with a per-channel affine + ReLU (pre-activation BN fold).
+__device__ __forceinline__ bf16x8 affine_relu8(bf16x8 v, const float* sc, const float* sh) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float x = (float)v[j] * sc[j] + sh[j];
+    r[j] = (bf16)(x > 0.f ? x : 0.f);
+  }
+  return r;
+}
+
+}  // namespace dtr
+
+#define DTR_CHECK_LAUNCH()                                                      \
+  do {                                                                          \
+    hipError_t e__ = hipGetLastError();                                         \
+    if (e__ != hipSuccess) {                                                    \
+      fprintf(stderr, "HIP launch error %s at %s:%d\n", hipGetErrorString(e__), \
+              __FILE__, __LINE__);                                              \
+    }                                                                           \
+  } while (0)

@@ -1,0 +1,360 @@
+// Implicit-GEMM convolution (forward and data-gradient) for NHWC bf16 tensors on
+// gfx950 matrix cores.
+//
+// Replaces the reference's cuDNN Conv2D / Conv2DBackpropInput (the
+// convs are emitted by `conv2d_fixed_padding`, resnet_model_official.py:80-91).
+//
+//   forward : C[m=(n,ho,wo)][co] = sum_{k=(r,c,ci)} X[n,ho*s-p+r,wo*s-p+c,ci] * W[co][r][c][ci]
+//   dgrad   : C[m=(n,h,w)][ci]   = sum_{k=(r,c,co)} DY[n,(h+p-r)/s,(w+p-c)/s,co] * W[r][c][ci][co]
+//
+// Padding follows TF's conv2d_fixed_padding: pad_beg=(k-1)/2 on top/left, output
+// Ho = (H-1)/s + 1 (identical for the stride-1 SAME and stride-2 fixed-pad cases),
+// folded into index math -- no Pad kernel.
+//
+// Design (CDNA4): 256-thread workgroups = 4 wave64s arranged WM x WN; BK = 64
+// (two k-steps of v_mfma_f32_16x16x32_bf16); A and B tiles are staged
+// global->VGPR->LDS with a one-tile register prefetch and double-buffered LDS
+// (one barrier per K tile), LDS rows XOR-swizzled (16-B chunk ^= row&7) so the
+// 16-lane groups of ds_read_b128 hit 16 distinct bank slots.  Fused extras:
+//   * PRE : apply the previous layer's BatchNorm+ReLU (per-input-channel affine)
+//           while staging A, so BN-ReLU outputs are never materialised in HBM;
+//   * epilogue bias / residual add / accumulate-into-output / fp32 output;
+//   * STATS: per-workgroup per-channel (mean, M2) Welford partials of the bf16
+//           output, finalised by bn_finalize (Chan's parallel combine).
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+template <int BM, int BN, int WM, int WN, int MODE, bool PRE, bool STATS>
+__global__ void __launch_bounds__(256)
+conv_gemm_kernel(GemmArgs args) {
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MR = WTM / 16, NR = WTN / 16;
+  constexpr int A_CHUNKS = BM * 8;                    // 16-byte chunks per A tile
+  constexpr int B_CHUNKS = BN * 8;
+  constexpr int A_PER_T = (A_CHUNKS + 255) / 256;
+  constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(MR >= 1 && NR >= 1, "wave tile >= 16x16");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* As = reinterpret_cast<bf16*>(smem);                 // [2][BM][BK]
+  bf16* Bs = As + 2 * BM * BK;                              // [2][BN][BK]
+  float* pre_s = reinterpret_cast<float*>(Bs + 2 * BN * BK); // [2][Cin] (PRE)
+
+  const ConvGeom& g = args.g;
+  const int M = args.M, NC = args.Ncol, KD = args.Kdim;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+
+  // Input-channel count of the A operand's gather (C for fwd, K for dgrad).
+  const int Acin = (MODE == MODE_FWD) ? g.C : g.K;
+
+  if constexpr (PRE) {
+    for (int i = tid; i < Acin; i += 256) {
+      pre_s[i] = args.pre_scale[i];
+      pre_s[Acin + i] = args.pre_shift[i];
+    }
+  }
+
+  // ---- per-thread loader state (row decomposition is K-invariant) ----
+  const int kg = tid & 7;  // fixed 16-B k-group of every chunk this thread stages
+  int a_base[A_PER_T], a_h[A_PER_T], a_w[A_PER_T];
+#pragma unroll
+  for (int i = 0; i < A_PER_T; ++i) {
+    const int q = tid + i * 256;
+    const int r = q >> 3;
+    const int m = m0 + r;
+    a_h[i] = -(1 << 28);  // invalid row marker
+    a_w[i] = 0;
+    a_base[i] = 0;
+    if (q < A_CHUNKS && m < M) {
+      if constexpr (MODE == MODE_FWD) {
+        const int hw = g.Ho * g.Wo;
+        const int n = m / hw, rem = m - n * hw;
+        const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+        a_base[i] = n * g.H * g.W;
+        a_h[i] = ho * g.stride - g.pad;
+        a_w[i] = wo * g.stride - g.pad;
+      } else {
+        const int hw = g.H * g.W;
+        const int n = m / hw, rem = m - n * hw;
+        const int h = rem / g.W, w = rem - h * g.W;
+        a_base[i] = n * g.Ho * g.Wo;
+        a_h[i] = h + g.pad;
+        a_w[i] = w + g.pad;
+      }
+    }
+  }
+
+  bf16x8 ra[A_PER_T], rb[B_PER_T];
+  const bf16x8 zero8 = {};
+
+  auto load_tile = [&](int t) {
+    const int k = t * BK + kg * 8;
+    const bool kvalid = k < KD;
+    const int tap = kvalid ? k / Acin : 0;
+    const int ci = k - tap * Acin;
+    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      bf16x8 v = zero8;
+      if constexpr (MODE == MODE_FWD) {
+        const int hi = a_h[i] + rr, wi = a_w[i] + cc;
+        if (kvalid && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+          const long off = ((long)(a_base[i] + hi * g.W + wi)) * g.C + ci;
+          v = *reinterpret_cast<const bf16x8*>(args.a + off);
+          if constexpr (PRE) v = affine_relu8(v, pre_s + ci, pre_s + Acin + ci);
+        }
+      } else {
+        int hp = a_h[i] - rr, wp = a_w[i] - cc;
+        bool ok = kvalid && hp >= 0 && wp >= 0;
+        if (g.stride != 1) {
+          ok = ok && (hp % g.stride == 0) && (wp % g.stride == 0);
+          hp /= g.stride;
+          wp /= g.stride;
+        }
+        if (ok && hp < g.Ho && wp < g.Wo) {
+          const long off = ((long)(a_base[i] + hp * g.Wo + wp)) * g.K + ci;
+          v = *reinterpret_cast<const bf16x8*>(args.a + off);
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int nrow = q >> 3;
+      bf16x8 v = zero8;
+      if (q < B_CHUNKS && n0 + nrow < NC && kvalid) {
+        long off;
+        if constexpr (MODE == MODE_FWD) {
+          off = (long)(n0 + nrow) * KD + k;                    // W[co][r][c][ci]
+        } else {
+          off = ((long)tap * g.C + (n0 + nrow)) * g.K + ci;    // W[r][c][ci][co]
+        }
+        v = *reinterpret_cast<const bf16x8*>(args.b + off);
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16* A = As + buf * BM * BK;
+    bf16* B = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (q < A_CHUNKS) {
+        const int r = q >> 3;
+        *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (q < B_CHUNKS) {
+        const int r = q >> 3;
+        *reinterpret_cast<bf16x8*>(B + r * BK + ((kg ^ (r & 7)) << 3)) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (PRE) __syncthreads();
+  const int KT = (KD + BK - 1) / BK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < KT; ++t) {
+    if (t + 1 < KT) load_tile(t + 1);
+    const bf16* A = As + (t & 1) * BM * BK;
+    const bf16* B = Bs + (t & 1) * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + fq;
+      bf16x8 af[MR], bfr[NR];
+#pragma unroll
+      for (int a = 0; a < MR; ++a) {
+        const int r = wm * WTM + a * 16 + fr;
+        af[a] = *reinterpret_cast<const bf16x8*>(A + r * BK + ((ch ^ (r & 7)) << 3));
+      }
+#pragma unroll
+      for (int b = 0; b < NR; ++b) {
+        const int r = wn * WTN + b * 16 + fr;
+        bfr[b] = *reinterpret_cast<const bf16x8*>(B + r * BK + ((ch ^ (r & 7)) << 3));
+      }
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+    }
+    if (t + 1 < KT) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  // Lane owns column n0 + wn*WTN + b*16 + fr, rows m0 + wm*WTM + a*16 + fq*4 + i.
+#pragma unroll
+  for (int b = 0; b < NR; ++b) {
+    const int col = n0 + wn * WTN + b * 16 + fr;
+    const float bias = (args.bias != nullptr && col < args.nbias) ? args.bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * WTM + a * 16 + fq * 4 + i;
+        float v = acc[a][b][i] + bias;
+        if (row < M && col < NC) {
+          const long o = (long)row * NC + col;
+          if (args.residual) v += (float)args.residual[o];
+          if (args.out_f32) {
+            if (args.accumulate) v += args.out_f32[o];
+            args.out_f32[o] = v;
+          } else {
+            if (args.accumulate) v += (float)args.out[o];
+            const bf16 vb = (bf16)v;
+            args.out[o] = vb;
+            v = (float)vb;
+          }
+        } else {
+          v = 0.f;
+        }
+        acc[a][b][i] = v;
+      }
+    }
+  }
+
+  if constexpr (STATS) {
+    // Per-channel Welford partial over this workgroup's valid rows:
+    // pass 1 sums -> tile mean; pass 2 squared deviations from the register copy.
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN]; LDS tiles are dead now
+    const int nvalid = min(BM, M - m0);
+    float mean_c[NR];
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+      float s = 0.f;
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s += acc[a][b][i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fq == 0) red[wm * BN + wn * WTN + b * 16 + fr] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+      const int c = wn * WTN + b * 16 + fr;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
+      mean_c[b] = s / (float)nvalid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+      float s = 0.f;
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * WTM + a * 16 + fq * 4 + i;
+          const float d = acc[a][b][i] - mean_c[b];
+          s += (row < M) ? d * d : 0.f;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fq == 0) red[wm * BN + wn * WTN + b * 16 + fr] = s;
+    }
+    __syncthreads();
+    if (wm == 0 && fq == 0) {
+#pragma unroll
+      for (int b = 0; b < NR; ++b) {
+        const int c = wn * WTN + b * 16 + fr;
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) s += red[w * BN + c];
+        const int col = n0 + c;
+        if (col < NC) {
+          float* p = args.stat_part + (long)blockIdx.x * 2 * NC;
+          p[col] = mean_c[b];
+          p[NC + col] = s;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int MODE, bool PRE, bool STATS>
+static void launch_cfg(const GemmArgs& a, hipStream_t s) {
+  const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
+  size_t lds = (size_t)2 * (BM + BN) * 64 * sizeof(bf16);
+  if (PRE) lds += (size_t)2 * Acin * sizeof(float);
+  lds = (lds + 15) & ~(size_t)15;
+  dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, PRE, STATS>), grid, dim3(256),
+                     lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+template <int BM, int BN, int WM, int WN, int MODE>
+static void launch_flags(const GemmArgs& a, hipStream_t s) {
+  const bool pre = a.pre_scale != nullptr, st = a.stat_part != nullptr;
+  if (pre && st) launch_cfg<BM, BN, WM, WN, MODE, true, true>(a, s);
+  else if (pre) launch_cfg<BM, BN, WM, WN, MODE, true, false>(a, s);
+  else if (st) launch_cfg<BM, BN, WM, WN, MODE, false, true>(a, s);
+  else launch_cfg<BM, BN, WM, WN, MODE, false, false>(a, s);
+}
+
+// Tile selection by output width; BM shrinks for small M so the grid still
+// covers the 256 CUs.  Shared by the launcher and by the host (the BN-stat
+// partial buffer has one row per M tile).
+int conv_gemm_bm(int M, int nc) {
+  const long m = M;
+  if (nc <= 16) return m >= 256L * 512 ? 256 : 64;
+  if (nc <= 32) return m >= 128L * 512 ? 128 : 64;
+  if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
+  return (m >= 128L * 128 && nc % 128 == 0) ? 128 : 64;
+}
+
+template <int MODE>
+static void launch_mode(const GemmArgs& a, hipStream_t s) {
+  const int nc = a.Ncol;
+  const int bm = conv_gemm_bm(a.M, nc);
+  if (nc <= 16) {
+    if (bm == 256) launch_flags<256, 16, 4, 1, MODE>(a, s);
+    else launch_flags<64, 16, 4, 1, MODE>(a, s);
+  } else if (nc <= 32) {
+    if (bm == 128) launch_flags<128, 32, 4, 1, MODE>(a, s);
+    else launch_flags<64, 32, 4, 1, MODE>(a, s);
+  } else if (nc <= 64) {
+    if (bm == 128) launch_flags<128, 64, 4, 1, MODE>(a, s);
+    else launch_flags<64, 64, 4, 1, MODE>(a, s);
+  } else {
+    if (bm == 128) launch_flags<128, 128, 2, 2, MODE>(a, s);
+    else launch_flags<64, 64, 4, 1, MODE>(a, s);
+  }
+}
+
+void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
+  if (mode == MODE_FWD) launch_mode<MODE_FWD>(a, s);
+  else launch_mode<MODE_DGRAD>(a, s);
+}
+
+}  // namespace dtr

@@ -1,0 +1,276 @@
+// Convolution weight gradient (replaces cuDNN Conv2DBackpropFilter).
+//
+//   dW[co][r][c][ci] = sum_{p=(n,ho,wo)} DY[p][co] * X[n, ho*s-pad+r, wo*s-pad+c, ci]
+//
+// GEMM view: M = Cout, N = kh*kw*Cin (tap-major, channel-minor), K = pixels.  In
+// NHWC both operands are pixel-major (channels contiguous), i.e. K-major, which
+// is the wrong way round for MFMA fragments.  Instead of transposing through
+// scattered LDS writes, tiles are staged as they come from HBM ([64 px][ch],
+// 16-byte loads) and the fragments are gathered with gfx950's transposed LDS
+// read `ds_read_b64_tr_b16` (two per 8-element fragment).  Any permutation of
+// the K index is legal as long as A and B use the same one, so each 16-lane
+// group reads four consecutive pixel rows per instruction, which with the 32-B
+// unit XOR swizzle below makes each 32-lane half of the read conflict-free.
+//
+// K (= N*Ho*Wo, up to 1.6M for the ImageNet stem) is split over a grid
+// dimension; every split writes its own fp32 partial slab and wgrad_reduce
+// sums the slabs in fixed order (deterministic; no float atomics), writing the
+// TF HWIO layout of the master gradient.  Optional fused BN+ReLU is applied to
+// X while staging (the pre-activation tensor is never stored).
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+template <int U>
+__device__ __forceinline__ int unit_swz(int row) {
+  if constexpr (U <= 1) return 0;
+  else return (row / (8 / U)) & (U - 1);
+}
+
+template <int BM, int BN, int WM, int WN, bool PRE>
+__global__ void __launch_bounds__(256)
+conv_wgrad_kernel(WgradArgs args) {
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MR = WTM / 16, NR = WTN / 16;
+  constexpr int UA = BM / 16, UB = BN / 16;  // 32-byte units per staged row
+  constexpr int A_CPR = BM / 8, B_CPR = BN / 8;  // 16-byte chunks per row
+  constexpr int A_CH = BK * A_CPR, B_CH = BK * B_CPR;
+  constexpr int A_PER_T = (A_CH + 255) / 256, B_PER_T = (B_CH + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(UA <= 8 && UB <= 8, "row <= 256 B");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* As = reinterpret_cast<bf16*>(smem);        // [2][BK][BM]
+  bf16* Bs = As + 2 * BK * BM;                     // [2][BK][BN]
+  float* pre_s = reinterpret_cast<float*>(Bs + 2 * BK * BN);
+
+  const ConvGeom& g = args.g;
+  const int Cout = g.K, Cin = g.C;
+  const int NT = g.kh * g.kw * Cin;
+  const int P = g.N * g.Ho * g.Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+  const int split = blockIdx.z;
+  const int p_begin = split * args.px_per_split;
+  const int p_end = min(P, p_begin + args.px_per_split);
+
+  if constexpr (PRE) {
+    for (int i = tid; i < Cin; i += 256) {
+      pre_s[i] = args.pre_scale[i];
+      pre_s[Cin + i] = args.pre_shift[i];
+    }
+    __syncthreads();
+  }
+
+  bf16x8 ra[A_PER_T], rb[B_PER_T];
+  const bf16x8 zero8 = {};
+  const int HoWo = g.Ho * g.Wo;
+
+  auto load_tile = [&](int t) {
+    const int pbase = p_begin + t * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int row = q / A_CPR, cc = q % A_CPR;
+      const int p = pbase + row;
+      bf16x8 v = zero8;
+      if (q < A_CH && p < p_end && m0 + cc * 8 < Cout)
+        v = *reinterpret_cast<const bf16x8*>(args.dy + (long)p * Cout + m0 + cc * 8);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int row = q / B_CPR, cc = q % B_CPR;
+      const int p = pbase + row;
+      const int n = n0 + cc * 8;
+      bf16x8 v = zero8;
+      if (q < B_CH && p < p_end && n < NT) {
+        const int tap = n / Cin, ci = n - tap * Cin;
+        const int r = tap / g.kw, c = tap - r * g.kw;
+        const int img = p / HoWo, rem = p - img * HoWo;
+        const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+        const int hi = ho * g.stride - g.pad + r, wi = wo * g.stride - g.pad + c;
+        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+          v = *reinterpret_cast<const bf16x8*>(
+              args.x + ((long)(img * g.H + hi) * g.W + wi) * Cin + ci);
+          if constexpr (PRE) v = affine_relu8(v, pre_s + ci, pre_s + Cin + ci);
+        }
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16* A = As + buf * BK * BM;
+    bf16* B = Bs + buf * BK * BN;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (q < A_CH) {
+        const int row = q / A_CPR, cc = q % A_CPR;
+        const int col = (((cc >> 1) ^ unit_swz<UA>(row)) << 4) + ((cc & 1) << 3);
+        *reinterpret_cast<bf16x8*>(A + row * BM + col) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (q < B_CH) {
+        const int row = q / B_CPR, cc = q % B_CPR;
+        const int col = (((cc >> 1) ^ unit_swz<UB>(row)) << 4) + ((cc & 1) << 3);
+        *reinterpret_cast<bf16x8*>(B + row * BN + col) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = (p_end - p_begin + BK - 1) / BK;
+  if (KT > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  const int gq = lane >> 4;           // 16-lane group
+  const int li = lane & 15;
+  const int qr = li >> 2, pc = li & 3;  // row-in-block, 4-column piece
+
+  for (int t = 0; t < KT; ++t) {
+    if (t + 1 < KT) load_tile(t + 1);
+    const bf16* A = As + (t & 1) * BK * BM;
+    const bf16* B = Bs + (t & 1) * BK * BN;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r1 = ks * 32 + 4 * gq + qr;  // pixel row for elements 0..3
+      const int r2 = r1 + 16;                // pixel row for elements 4..7
+      bf16x8 af[MR], bfr[NR];
+#pragma unroll
+      for (int a = 0; a < MR; ++a) {
+        const int unit = (wm * WTM + a * 16) >> 4;
+        const s16x4 lo = lds_read_tr16(A + r1 * BM + ((unit ^ unit_swz<UA>(r1)) << 4) + 4 * pc);
+        const s16x4 hi = lds_read_tr16(A + r2 * BM + ((unit ^ unit_swz<UA>(r2)) << 4) + 4 * pc);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[a] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int b = 0; b < NR; ++b) {
+        const int unit = (wn * WTN + b * 16) >> 4;
+        const s16x4 lo = lds_read_tr16(B + r1 * BN + ((unit ^ unit_swz<UB>(r1)) << 4) + 4 * pc);
+        const s16x4 hi = lds_read_tr16(B + r2 * BN + ((unit ^ unit_swz<UB>(r2)) << 4) + 4 * pc);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[b] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+    }
+    if (t + 1 < KT) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  float* out = args.part + (long)split * Cout * NT;
+#pragma unroll
+  for (int b = 0; b < NR; ++b) {
+    const int n = n0 + wn * WTN + b * 16 + li;
+#pragma unroll
+    for (int a = 0; a < MR; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * WTM + a * 16 + gq * 4 + i;
+        if (m < Cout && n < NT) out[(long)m * NT + n] = acc[a][b][i];
+      }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void wg_launch(const WgradArgs& a, hipStream_t s) {
+  const int NT = a.g.kh * a.g.kw * a.g.C;
+  size_t lds = (size_t)2 * 64 * (BM + BN) * sizeof(bf16);
+  if (a.pre_scale) lds += (size_t)2 * a.g.C * sizeof(float);
+  dim3 grid((NT + BN - 1) / BN, (a.g.K + BM - 1) / BM, a.splits);
+  if (a.pre_scale)
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+static void wg_tile(const ConvGeom& g, int* bm, int* bn) {
+  const int NT = g.kh * g.kw * g.C;
+  *bm = g.K <= 16 ? 16 : g.K <= 32 ? 32 : g.K <= 64 ? 64 : 128;
+  *bn = NT <= 64 ? 64 : 128;
+  if (*bm == 16) *bn = 64;
+}
+
+int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
+  int bm, bn;
+  wg_tile(g, &bm, &bn);
+  const long NT = (long)g.kh * g.kw * g.C;
+  const long tiles = ((g.K + bm - 1) / bm) * ((NT + bn - 1) / bn);
+  const long P = (long)g.N * g.Ho * g.Wo;
+  long splits = 1024 / tiles;
+  if (splits < 1) splits = 1;
+  long maxs = P / 512;
+  if (maxs < 1) maxs = 1;
+  if (splits > maxs) splits = maxs;
+  long pps = (P + splits - 1) / splits;
+  pps = (pps + 63) / 64 * 64;
+  *px_per_split = (int)pps;
+  return (int)((P + pps - 1) / pps);
+}
+
+void conv_wgrad(const WgradArgs& a, hipStream_t s) {
+  int bm, bn;
+  wg_tile(a.g, &bm, &bn);
+  if (bm == 16) wg_launch<16, 64, 1, 4>(a, s);
+  else if (bm == 32 && bn == 64) wg_launch<32, 64, 2, 2>(a, s);
+  else if (bm == 32) wg_launch<32, 128, 1, 4>(a, s);
+  else if (bm == 64 && bn == 64) wg_launch<64, 64, 2, 2>(a, s);
+  else if (bm == 64) wg_launch<64, 128, 2, 2>(a, s);
+  else if (bn == 64) wg_launch<128, 64, 2, 2>(a, s);
+  else wg_launch<128, 128, 2, 2>(a, s);
+}
+
+// Deterministic split-K reduction + layout change [co][tap][ci] -> HWIO [tap][ci][co],
+// dropping padded output channels (co >= Kv) and padded input channels (ci >= Cv).
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ grad,
+                                    int splits, int K, int Kv, int taps, int C, int Cv,
+                                    float scale, int accumulate) {
+  const long NT = (long)taps * C;
+  const long total = (long)K * NT;
+  const long NTv = (long)taps * Cv;
+  const long outn = (long)Kv * NTv;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < outn;
+       idx += (long)gridDim.x * blockDim.x) {
+    const long co = idx / NTv, nv = idx - co * NTv;
+    const long tap = nv / Cv, ci = nv - tap * Cv;
+    const long src = co * NT + tap * C + ci;
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += part[(long)sp * total + src];
+    const long o = nv * Kv + co;
+    grad[o] = accumulate ? grad[o] + s * scale : s * scale;
+  }
+}
+
+void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_valid, int taps,
+                  int C, int C_valid, float scale, int accumulate, hipStream_t s) {
+  const long total = (long)K_valid * taps * C_valid;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, part, grad_hwio,
+                     splits, K, K_valid, taps, C, C_valid, scale, accumulate);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

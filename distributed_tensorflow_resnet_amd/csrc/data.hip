@@ -1,0 +1,136 @@
+// On-device input pipeline pieces.
+//
+// cifar_augment reproduces the reference CIFAR training preprocessing
+// (resnet_cifar_main.py:201-216: pad to 40x40, random 32x32 crop, random
+// left-right flip, tf.image.per_image_standardization) and the eval path
+// (cifar_input.py:71-76: standardization only) on raw CIFAR-binary uint8 images
+// ([N][3][32][32], the record layout of resnet_cifar_main.py:173-198), writing
+// bf16 NHWC with the channel dim zero-padded to Cpad (the stem conv consumes 8
+// channels so every 16-B fragment is one tap).  Crop/flip randomness comes from
+// a counter-based hash of (seed, global_step, image) read on the device, so the
+// augmentation is part of the captured hipGraph and replays with fresh crops.
+#include "common.h"
+#include "kernels.h"
+#include "data.h"
+
+namespace dtr {
+
+__device__ __forceinline__ unsigned long long splitmix(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void __launch_bounds__(256)
+cifar_augment_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int H, int W,
+                     int Cpad, int pad, unsigned long long seed, const long long* gstep,
+                     int train, int* crop_log) {
+  __shared__ float red[8];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const int HW = H * W, CHW = 3 * HW;
+  const uint8_t* src = img + (long)n * CHW;
+  int oy = pad, ox = pad, flip = 0;
+  if (train) {
+    const unsigned long long step = gstep ? (unsigned long long)*gstep : 0ull;
+    const unsigned long long h = splitmix(seed ^ splitmix(step * 0x100000001B3ull + n));
+    oy = (int)(h % (2 * pad + 1));
+    ox = (int)((h >> 16) % (2 * pad + 1));
+    flip = (int)((h >> 32) & 1);
+  }
+  if (crop_log && tid == 0) {
+    crop_log[n * 3 + 0] = oy;
+    crop_log[n * 3 + 1] = ox;
+    crop_log[n * 3 + 2] = flip;
+  }
+  // pixel (y,x) of the crop = padded-image pixel (y+oy, x'+ox), x' = flip ? W-1-x : x
+  auto val = [&](int p, int c) -> float {
+    const int y = p / W, x = p - y * W;
+    const int xs = flip ? (W - 1 - x) : x;
+    const int py = y + oy - pad, px = xs + ox - pad;
+    if (py < 0 || py >= H || px < 0 || px >= W) return 0.f;
+    return (float)src[c * HW + py * W + px];
+  };
+  float s = 0.f, q = 0.f;
+  for (int i = tid; i < CHW; i += 256) {
+    const float v = val(i / 3, i % 3);
+    s += v;
+    q += v * v;
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = s;
+    red[4 + (tid >> 6)] = q;
+  }
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float totq = red[4] + red[5] + red[6] + red[7];
+  const float nel = (float)CHW;
+  const float mean = tot / nel;
+  const float var = fmaxf(totq / nel - mean * mean, 0.f);
+  const float adj = fmaxf(sqrtf(var), rsqrtf(nel));
+  const float inv = 1.f / adj;
+  bf16* o = out + (long)n * HW * Cpad;
+  for (int i = tid; i < HW * Cpad; i += 256) {
+    const int p = i / Cpad, c = i - p * Cpad;
+    o[i] = (bf16)(c < 3 ? (val(p, c) - mean) * inv : 0.f);
+  }
+}
+
+void cifar_augment(const uint8_t* img, bf16* out, int N, int H, int W, int Cpad, int pad,
+                   unsigned long long seed, const long long* gstep, int train, int* crop_log,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(cifar_augment_kernel, dim3(N), dim3(256), 0, s, img, out, H, W, Cpad, pad,
+                     seed, gstep, train, crop_log);
+  DTR_CHECK_LAUNCH();
+}
+
+__global__ void pad_channels_kernel(const float* __restrict__ x, bf16* __restrict__ out, long npix,
+                                    int C, int Cpad) {
+  const long total = npix * Cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long p = i / Cpad;
+    const int c = (int)(i - p * Cpad);
+    out[i] = (bf16)(c < C ? x[p * C + c] : 0.f);
+  }
+}
+
+void nhwc_pad_channels(const float* x, bf16* out, long npix, int C, int Cpad, hipStream_t s) {
+  long blocks = (npix * Cpad + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pad_channels_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, out, npix,
+                     C, Cpad);
+  DTR_CHECK_LAUNCH();
+}
+
+// Gaussian-ish synthetic activations (sum of 4 uniforms, unit variance) in
+// NHWC with the padded channels kept zero.
+__global__ void synth_kernel(bf16* out, long npix, int C, int Cpad, unsigned long long seed) {
+  const long total = npix * Cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cpad);
+    float v = 0.f;
+    if (c < C) {
+      const unsigned long long h = splitmix(seed + (unsigned long long)i);
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += (float)((h >> (16 * k)) & 0xFFFF) * (1.f / 65535.f);
+      v = (s - 2.f) * 1.7320508f;
+    }
+    out[i] = (bf16)v;
+  }
+}
+
+void synthetic_images(bf16* out, long npix, int C, int Cpad, unsigned long long seed,
+                      hipStream_t s) {
+  long blocks = (npix * Cpad + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, npix, C, Cpad,
+                     seed);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

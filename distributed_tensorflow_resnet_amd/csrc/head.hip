@@ -1,0 +1,270 @@
+// Network head and stem helpers:
+//   * final BN-ReLU fused with the global average pool
+//     (resnet_model_official.py:268-271 / 335-339: batch_norm_relu -> average_pooling2d)
+//   * softmax cross-entropy, mean over the batch, fused with the training
+//     precision (argmax == label, resnet_cifar_main.py:284-286) and the dense
+//     bias gradient (resnet_model.py:77-80)
+//   * 3x3/2 SAME max-pool of the ImageNet stem (resnet_model_official.py:314-316;
+//     TF SAME pads 0 before / 1 after for 112 -> 56), backward by recomputed
+//     first-max argmax (deterministic gather, no atomics).
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+// pooled[n][c] = mean_hw relu(x[n][hw][c]*scale[c] + shift[c]); one block per
+// image, 8 channels per thread-slot, rows strided over the block.
+__global__ void __launch_bounds__(256)
+bnrelu_avgpool_kernel(const bf16* __restrict__ x, const float* __restrict__ scale,
+                      const float* __restrict__ shift, bf16* __restrict__ pooled, int HW,
+                      int C) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const int G = C / 8;
+  const int rpi = max(1, 256 / G);
+  const int grp = tid % G, rsub = tid / G;
+  const bool active = (grp < G) && (rsub < rpi) && tid < G * rpi;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (active) {
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = scale[grp * 8 + j];
+      sh[j] = shift[grp * 8 + j];
+    }
+    for (int p = rsub; p < HW; p += rpi) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((long)n * HW + p) * C + grp * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += fmaxf((float)v[j] * sc[j] + sh[j], 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rsub * C + grp * 8 + j] = s[j];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float t = 0.f;
+    for (int k = 0; k < rpi; ++k) t += red[k * C + c];
+    pooled[(long)n * C + c] = (bf16)(t / (float)HW);
+  }
+}
+
+void bnrelu_avgpool(const bf16* x, const float* scale, const float* shift, bf16* pooled, int N,
+                    int HW, int C, hipStream_t s) {
+  const int G = C / 8;
+  const int rpi = G >= 256 ? 1 : 256 / G;
+  const size_t lds = (size_t)rpi * C * sizeof(float);
+  // C > 2048 would need multiple passes; ResNet heads are 64 / 2048 channels.
+  hipLaunchKernelGGL(bnrelu_avgpool_kernel, dim3(N), dim3(256), lds, s, x, scale, shift, pooled,
+                     HW, C);
+  DTR_CHECK_LAUNCH();
+}
+
+// d_act[n][hw][c] = dpooled[n][c] / HW  (the ReLU mask / BN backward follow in
+// bn_relu_bwd_*).
+__global__ void avgpool_bwd_kernel(const bf16* __restrict__ dp, bf16* __restrict__ dx, int HW,
+                                   int C, long nvec) {
+  const int G = C / 8;
+  const float inv = 1.f / (float)HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const long row = i / G;
+    const int grp = (int)(i - row * G);
+    const long n = row / HW;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(dp + n * C + grp * 8);
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)((float)v[j] * inv);
+    *reinterpret_cast<bf16x8*>(dx + i * 8) = r;
+  }
+}
+
+void avgpool_bwd(const bf16* dpooled, bf16* dx, int N, int HW, int C, hipStream_t s) {
+  const long nvec = (long)N * HW * C / 8;
+  long blocks = (nvec + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dpooled, dx,
+                     HW, C, nvec);
+  DTR_CHECK_LAUNCH();
+}
+
+// Single 1024-thread block (N <= a few thousand rows): one wave per row at a
+// time, fixed reduction order -> deterministic loss / precision / dbias.
+// dlogits = (softmax - onehot) * grad_scale   (grad_scale = 1/global_batch).
+__global__ void __launch_bounds__(1024)
+softmax_xent_kernel(const float* __restrict__ logits, int ld, const int* __restrict__ labels,
+                    int N, int classes, float* loss_sum, float* correct,
+                    bf16* __restrict__ dlogits, float* __restrict__ dbias, float grad_scale,
+                    float* __restrict__ probs) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // [16 waves][ld] dbias partial + misc
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = blockDim.x >> 6;
+  float* db = sh;                    // [nw][ld]
+  float* wl = sh + nw * ld;          // [nw] loss
+  float* wc = wl + nw;               // [nw] correct
+  for (int c = lane; c < ld; c += 64) db[wave * ld + c] = 0.f;
+  float lsum = 0.f, csum = 0.f;
+  for (int row = wave; row < N; row += nw) {
+    const float* z = logits + (long)row * ld;
+    float mx = -INFINITY;
+    int amax = 0;
+    for (int c = lane; c < classes; c += 64) {
+      const float v = z[c];
+      if (v > mx) { mx = v; amax = c; }
+    }
+    // wave argmax (first max on ties, like tf.argmax)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(amax, o, 64);
+      if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+    }
+    float se = 0.f;
+    for (int c = lane; c < classes; c += 64) se += __expf(z[c] - mx);
+    se = wave_sum(se);
+    const float lse = mx + __logf(se);
+    const int y = labels[row];
+    const float zy = (y >= 0 && y < classes) ? z[y] : lse;
+    if (lane == 0) {
+      lsum += lse - zy;
+      csum += (amax == y) ? 1.f : 0.f;
+    }
+    for (int c = lane; c < ld; c += 64) {
+      float g = 0.f;
+      if (c < classes) {
+        const float p = __expf(z[c] - lse);
+        if (probs) probs[(long)row * ld + c] = p;
+        g = (p - (c == y ? 1.f : 0.f)) * grad_scale;
+      }
+      if (dlogits) dlogits[(long)row * ld + c] = (bf16)g;
+      db[wave * ld + c] += g;
+    }
+  }
+  if (lane == 0) {
+    wl[wave] = lsum;
+    wc[wave] = csum;
+  }
+  __syncthreads();
+  for (int c = tid; c < ld; c += blockDim.x) {
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += db[w * ld + c];
+    if (dbias && c < classes) dbias[c] = t;
+  }
+  if (tid == 0) {
+    float l = 0.f, k = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      l += wl[w];
+      k += wc[w];
+    }
+    if (loss_sum) *loss_sum = l;
+    if (correct) *correct = k;
+  }
+}
+
+void softmax_xent(const float* logits, int ld, const int* labels, int N, int classes,
+                  float* loss_sum, float* correct, bf16* dlogits, float* dbias, float grad_scale,
+                  float* probs, hipStream_t s) {
+  const int threads = 1024, nw = threads / 64;
+  const size_t lds = ((size_t)nw * ld + 2 * nw) * sizeof(float);
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(1), dim3(threads), lds, s, logits, ld, labels, N,
+                     classes, loss_sum, correct, dlogits, dbias, grad_scale, probs);
+  DTR_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// max pool (NHWC), window k, stride s, pad_top=pad_left=pad; out-of-range taps
+// are excluded (TF SAME semantics).
+// ---------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H,
+                                   int W, int C, int Ho, int Wo, int k, int st, int pad) {
+  const int G = C / 8;
+  const long total = (long)N * Ho * Wo * G;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int grp = (int)(i % G);
+    long t = i / G;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * st - pad + r;
+      if (hi < 0 || hi >= H) continue;
+      for (int c = 0; c < k; ++c) {
+        const int wi = wo * st - pad + c;
+        if (wi < 0 || wi >= W) continue;
+        const bf16x8 v =
+            *reinterpret_cast<const bf16x8*>(x + (((long)n * H + hi) * W + wi) * C + grp * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+      }
+    }
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)m[j];
+    *reinterpret_cast<bf16x8*>(y + i * 8) = r;
+  }
+}
+
+void maxpool_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
+                 int stride, int pad, hipStream_t s) {
+  const long total = (long)N * Ho * Wo * (C / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, N, H, W,
+                     C, Ho, Wo, k, stride, pad);
+  DTR_CHECK_LAUNCH();
+}
+
+// dx[h][w] = sum over windows containing (h,w) whose first argmax is (h,w).
+__global__ void maxpool_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                   bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                   int Wo, int k, int st, int pad) {
+  const long total = (long)N * H * W * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % C);
+    long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc = 0.f;
+    // outputs whose window covers h: ho*st - pad <= h <= ho*st - pad + k - 1
+    const int ho_lo = max(0, (h + pad - k + st) / st), ho_hi = min(Ho - 1, (h + pad) / st);
+    const int wo_lo = max(0, (w + pad - k + st) / st), wo_hi = min(Wo - 1, (w + pad) / st);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        if (h < ho * st - pad || w < wo * st - pad) continue;
+        // first-max in row-major window order
+        float best = -INFINITY;
+        int bh = -1, bw = -1;
+        for (int r = 0; r < k; ++r) {
+          const int hi = ho * st - pad + r;
+          if (hi < 0 || hi >= H) continue;
+          for (int c = 0; c < k; ++c) {
+            const int wi = wo * st - pad + c;
+            if (wi < 0 || wi >= W) continue;
+            const float v = (float)x[(((long)n * H + hi) * W + wi) * C + ch];
+            if (v > best) { best = v; bh = hi; bw = wi; }
+          }
+        }
+        if (bh == h && bw == w) acc += (float)dy[(((long)n * Ho + ho) * Wo + wo) * C + ch];
+      }
+    dx[i] = (bf16)acc;
+  }
+}
+
+void maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho,
+                 int Wo, int k, int stride, int pad, hipStream_t s) {
+  const long total = (long)N * H * W * C;
+  long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, dy, dx, N, H,
+                     W, C, Ho, Wo, k, stride, pad);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

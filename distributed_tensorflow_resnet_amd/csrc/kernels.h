@@ -1,0 +1,109 @@
+// Host-visible launcher interface of the gfx950 kernel library.  Every launcher
+// takes raw device pointers plus an explicit hipStream_t, performs no
+// allocation and no synchronisation, and is therefore safe inside hipGraph
+// stream capture (the whole training step is captured; see train/engine.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtr {
+
+typedef __bf16 bf16;
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct ConvGeom {
+  int N, H, W, C;     // input activation (NHWC)
+  int Ho, Wo, K;      // output spatial dims, output channels
+  int kh, kw, stride, pad;
+};
+
+struct GemmArgs {
+  const bf16* a;            // x (fwd) or dy (dgrad), NHWC
+  const bf16* b;            // weights: [K][kh][kw][C] (fwd) or [kh][kw][C][K] (dgrad)
+  bf16* out;                // [M][Ncol] bf16 (unless out_f32)
+  float* out_f32;           // optional fp32 output
+  const bf16* residual;     // optional [M][Ncol] residual added in the epilogue
+  const float* pre_scale;   // optional per-A-channel BN scale (fused BN+ReLU on load)
+  const float* pre_shift;
+  const float* bias;        // optional, applied to columns < nbias
+  int nbias;
+  float* stat_part;         // optional [tiles][2][Ncol] Welford partials (mean, M2)
+  int accumulate;           // out += result
+  ConvGeom g;
+  int M, Ncol, Kdim;
+};
+
+void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
+int conv_gemm_bm(int M, int Ncol);
+
+struct WgradArgs {
+  const bf16* dy;           // [N,Ho,Wo,K]
+  const bf16* x;            // [N,H,W,C] (pre-BN tensor if pre_scale given)
+  const float* pre_scale;   // optional fused BN+ReLU on x
+  const float* pre_shift;
+  float* part;              // [splits][K][kh*kw*C] fp32 partials
+  ConvGeom g;
+  int splits;
+  int px_per_split;         // multiple of 64
+};
+void conv_wgrad(const WgradArgs& a, hipStream_t s);
+// grad[tap][ci][co] (+)= scale * sum_s part[s][co][tap*C+ci] for co < K_valid, ci < C_valid
+// (output is the unpadded TF HWIO tensor [taps][C_valid][K_valid])
+void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_valid, int taps,
+                  int C, int C_valid, float scale, int accumulate, hipStream_t s);
+int wgrad_pick_splits(const ConvGeom& g, int* px_per_split);
+
+// ---- BatchNorm (training mode, TF fused semantics) ----
+void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
+                 const float* gamma, const float* beta, float* moving_mean,
+                 float* moving_var, float momentum, float eps, int update_moving,
+                 float* mean, float* rstd, float* scale, float* shift, hipStream_t s);
+void bn_scale_shift_eval(const float* gamma, const float* beta, const float* moving_mean,
+                         const float* moving_var, float eps, int C, float* scale,
+                         float* shift, hipStream_t s);
+// per-channel reductions for BN+ReLU backward: sum(g), sum(g*xhat) with g = dy*[y>0]
+void bn_relu_bwd_reduce(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                        const float* scale, const float* shift, int M, int C, float* part,
+                        int* tiles_out, hipStream_t s);
+int bn_bwd_tiles(int M, int C);
+// finalize: dgamma, dbeta (added to grads), coefficients for apply
+void bn_bwd_finalize(const float* part, int tiles, int M, int C, const float* gamma,
+                     const float* rstd, float* dgamma, float* dbeta, float* coef,
+                     hipStream_t s);
+// dx = coef_a*g - coef_b - coef_c*xhat (+ residual-grad add)
+void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                       const float* scale, const float* shift, const float* coef,
+                       const bf16* add, bf16* dx, int M, int C, hipStream_t s);
+void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M,
+                   int C, hipStream_t s);
+
+void bn_stats(const bf16* x, int M, int C, float* part, hipStream_t s);
+int bn_stats_tile_rows();
+
+// ---- head: BN-ReLU + global average pool, softmax cross-entropy ----
+void bnrelu_avgpool(const bf16* x, const float* scale, const float* shift, bf16* pooled,
+                    int N, int HW, int C, hipStream_t s);
+void avgpool_bwd(const bf16* dpooled, bf16* dx, int N, int HW, int C, hipStream_t s);
+void softmax_xent(const float* logits, int ld, const int* labels, int N, int classes,
+                  float* loss_sum, float* correct, bf16* dlogits, float* dbias,
+                  float grad_scale, float* probs, hipStream_t s);
+
+// ---- max pool (ImageNet stem) ----
+void maxpool_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
+                 int k, int stride, int pad, hipStream_t s);
+void maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho,
+                 int Wo, int k, int stride, int pad, hipStream_t s);
+
+// ---- flat-parameter descriptors ----
+struct ParamSeg {          // one trainable tensor inside the flat buffers
+  long long offset;        // element offset into master/grad/mom (master layout = TF HWIO)
+  long long numel;
+  long long bf_ohwi;       // element offset of the bf16 [Kpad][kh][kw][Cpad] copy (-1: none)
+  long long bf_hwio;       // element offset of the bf16 [kh][kw][C][Kpad] copy (-1: none)
+  int kh, kw, C, K;        // geometry of the master tensor (kh=kw=1 for dense)
+  int cpad;                // padded input channels of the OHWI copy
+  int kpad;                // padded output channels of both copies
+};
+
+}  // namespace dtr

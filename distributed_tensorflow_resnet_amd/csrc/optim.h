@@ -1,0 +1,28 @@
+// Optimizer-side declarations (see optim.hip).
+#pragma once
+#include "kernels.h"
+
+namespace dtr {
+
+// Piecewise learning-rate schedule evaluated on the device from global_step.
+struct LrSchedule {
+  float init;            // rate used at step 0 (the hook's begin())
+  long long warm_steps;  // linear warm-up length (0 = none)
+  float warm_from, warm_to;
+  int nb;                // number of boundaries (<= 7)
+  long long bound[7];
+  float val[8];
+};
+
+void sgd_update_pack(float* master, const float* grad, float* mom, long n, const LrSchedule& s,
+                     const long long* gstep, float momentum, float wd, float grad_scale,
+                     int use_momentum, const ParamSeg* segs, int nseg, bf16* bf, float* lr_out,
+                     int update, hipStream_t st);
+void step_increment(long long* gstep, hipStream_t s);
+int l2_workspace_floats();
+void l2_half_sum(const float* v, long n, float* ws, float* out, hipStream_t s);
+void fill_f32(float* p, long n, float a, hipStream_t s);
+void cast_f32_bf16(const float* a, bf16* b, long n, hipStream_t s);
+void cast_bf16_f32(const bf16* a, float* b, long n, hipStream_t s);
+
+}  // namespace dtr

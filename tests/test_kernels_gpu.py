@@ -1,0 +1,243 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the
+same op (ops/reference.py).  Shapes are the SURVEY Appendix-A shape classes
+(scaled-down batch), plus the awkward cases: stride-2 fixed padding, 1x1
+stride-2 projections, the 7x7/2 stem, channel padding, partial tiles."""
+import math
+
+import pytest
+import torch
+
+from distributed_tensorflow_resnet_amd.ops import functional as fn
+from distributed_tensorflow_resnet_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def _rel(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(BF).float()
+
+
+CONV_CASES = [
+    # N, H, C, K, k, s
+    (4, 32, 16, 16, 3, 1),
+    (4, 32, 16, 16, 1, 1),
+    (4, 32, 16, 32, 3, 2),
+    (4, 32, 16, 32, 1, 2),
+    (4, 16, 32, 32, 3, 1),
+    (4, 16, 32, 64, 3, 2),
+    (4, 8, 64, 64, 3, 1),
+    (2, 14, 256, 1024, 1, 1),
+    (2, 14, 256, 256, 3, 1),
+    (2, 28, 128, 128, 3, 2),
+    (2, 28, 512, 1024, 1, 2),
+    (2, 7, 512, 2048, 1, 1),
+    (3, 9, 32, 48, 3, 2),      # odd sizes / partial tiles
+]
+
+
+@pytest.mark.parametrize("N,H,C,K,k,s", CONV_CASES)
+def test_conv_fwd(gpu, N, H, C, K, k, s):
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    y = fn.conv2d_fwd(x, w.permute(3, 0, 1, 2).contiguous(), s)
+    r = ref.conv2d(x.float(), w.float(), s)
+    assert y.shape == r.shape
+    assert _rel(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K,k,s", CONV_CASES)
+def test_conv_dgrad(gpu, N, H, C, K, k, s):
+    torch.manual_seed(1)
+    x = torch.randn(N, H, H, C, device=gpu)
+    w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    x.requires_grad_(True)
+    r = ref.conv2d(x, w.float(), s)
+    dy = torch.randn_like(r).to(BF)
+    r.backward(dy.float())
+    dx = fn.conv2d_dgrad(dy, w.contiguous(), tuple(x.shape), s)
+    assert _rel(dx, x.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K,k,s", CONV_CASES)
+def test_conv_wgrad(gpu, N, H, C, K, k, s):
+    torch.manual_seed(2)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = torch.zeros(k, k, C, K, device=gpu, requires_grad=True)
+    r = ref.conv2d(x.float(), w, s)
+    dy = torch.randn_like(r).to(BF)
+    r.backward(dy.float())
+    dw = fn.conv2d_wgrad(dy, x, k, k, s)
+    assert dw.shape == w.shape
+    assert _rel(dw, w.grad) < 1e-2
+
+
+def test_conv_stem_padded_channels(gpu):
+    """CIFAR stem: 3 real channels zero-padded to 8; wgrad drops the pad."""
+    torch.manual_seed(3)
+    x3 = torch.randn(4, 32, 32, 3, device=gpu)
+    x8 = torch.zeros(4, 32, 32, 8, device=gpu)
+    x8[..., :3] = x3
+    w = torch.randn(3, 3, 3, 16, device=gpu) * 0.2
+    w8 = torch.zeros(16, 3, 3, 8, device=gpu)
+    w8[..., :3] = w.permute(3, 0, 1, 2)
+    y = fn.conv2d_fwd(x8.to(BF), w8.to(BF), 1)
+    r = ref.conv2d(_bf(x3), _bf(w), 1)
+    assert _rel(y, r) < 1e-2
+    dy = torch.randn_like(r).to(BF)
+    wt = torch.zeros_like(w, requires_grad=True)
+    ref.conv2d(_bf(x3), wt, 1).backward(dy.float())
+    g = torch.empty(3, 3, 3, 16, device=gpu)
+    nat = fn.native()
+    geom = fn.ConvGeom(4, 32, 32, 8, 16, 3, 3, 1)
+    sp, pps = nat.wgrad_pick_splits(geom.as_list())
+    part = torch.empty(sp * 16 * 9 * 8, device=gpu)
+    st = fn._stream()
+    nat.conv_wgrad(dy.data_ptr(), x8.to(BF).data_ptr(), 0, 0, part.data_ptr(), geom.as_list(), sp,
+                   pps, st)
+    nat.wgrad_reduce(part.data_ptr(), g.data_ptr(), sp, 16, 16, 9, 8, 3, 1.0, 0, st)
+    assert _rel(g, wt.grad) < 1e-2
+
+
+def test_conv_imagenet_stem(gpu):
+    torch.manual_seed(4)
+    x3 = torch.randn(2, 64, 64, 3, device=gpu)
+    x8 = torch.zeros(2, 64, 64, 8, device=gpu)
+    x8[..., :3] = x3
+    w = torch.randn(7, 7, 3, 64, device=gpu) * 0.1
+    w8 = torch.zeros(64, 7, 7, 8, device=gpu)
+    w8[..., :3] = w.permute(3, 0, 1, 2)
+    y = fn.conv2d_fwd(x8.to(BF), w8.to(BF), 2)
+    r = ref.conv2d(_bf(x3), _bf(w), 2)
+    assert y.shape == (2, 32, 32, 64)
+    assert _rel(y, r) < 1e-2
+
+
+def test_conv_fused_prologue_epilogue(gpu):
+    """PRE (BN+ReLU on load, zero padding stays zero), residual add, BN stats."""
+    torch.manual_seed(5)
+    N, H, C, K = 4, 16, 32, 32
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    sc = torch.rand(C, device=gpu) + 0.5
+    sh = torch.randn(C, device=gpu) * 0.3
+    w = (torch.randn(3, 3, C, K, device=gpu) / math.sqrt(9 * C)).to(BF)
+    res = torch.randn(N, H, H, K, device=gpu).to(BF)
+    tiles, rows = fn.stat_tiles(N * H * H, K)
+    part = torch.empty(tiles * 2 * K, device=gpu)
+    y = fn.conv2d_fwd(x, w.permute(3, 0, 1, 2).contiguous(), 1, pre_scale=sc, pre_shift=sh,
+                      residual=res, stat_part=part)
+    a = torch.relu(x.float() * sc + sh).to(BF).float()
+    r = ref.conv2d(a, w.float(), 1) + res.float()
+    assert _rel(y, r) < 1e-2
+    # stats of the bf16 output through bn_finalize
+    gamma = torch.rand(K, device=gpu) + 0.5
+    beta = torch.randn(K, device=gpu)
+    mm = torch.zeros(K, device=gpu)
+    mv = torch.ones(K, device=gpu)
+    mean, rstd, scale, shift = fn.bn_finalize(part, tiles, rows, N * H * H, gamma, beta, mm, mv)
+    yf = y.float().reshape(-1, K)
+    _, m_ref, v_ref, uv_ref = ref.batch_norm_train(yf, gamma, beta)
+    torch.testing.assert_close(mean, m_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rstd, torch.rsqrt(v_ref + 1e-5), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(mm, 0.003 * m_ref, rtol=1e-3, atol=1e-6)
+    torch.testing.assert_close(mv, 0.997 + 0.003 * uv_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(scale, gamma * rstd)
+    torch.testing.assert_close(shift, beta - mean * gamma * rstd)
+
+
+def test_bn_stats_and_backward(gpu):
+    torch.manual_seed(6)
+    M, C = 3000, 64
+    x = (torch.randn(M, C, device=gpu) * 2 + 3).to(BF)
+    part, tiles, rows = fn.bn_stats(x)
+    gamma = torch.rand(C, device=gpu) + 0.5
+    beta = torch.randn(C, device=gpu) * 0.1
+    mm, mv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    mean, rstd, scale, shift = fn.bn_finalize(part, tiles, rows, M, gamma, beta, mm, mv)
+    xf = x.float().requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    y, m_ref, v_ref, _ = ref.batch_norm_train(xf, g_, b_)
+    torch.testing.assert_close(mean, m_ref.detach(), rtol=1e-4, atol=1e-4)
+    a = torch.relu(y)
+    dy = torch.randn(M, C, device=gpu).to(BF)
+    add = torch.randn(M, C, device=gpu).to(BF)
+    a.backward(dy.float())
+    dx, dgamma, dbeta = fn.bn_relu_backward(dy, x, mean, rstd, scale, shift, gamma, add=add)
+    assert _rel(dx.float() - add.float(), xf.grad) < 2e-2
+    assert _rel(dgamma, g_.grad) < 1e-3
+    assert _rel(dbeta, b_.grad) < 1e-3
+    y2 = fn.bn_relu_apply(x, scale, shift)
+    assert _rel(y2, a) < 1e-2
+
+
+def test_head_pool_xent(gpu):
+    torch.manual_seed(7)
+    N, HW, C, classes = 64, 8, 64, 10
+    x = torch.randn(N, HW, HW, C, device=gpu).to(BF)
+    sc = torch.rand(C, device=gpu) + 0.5
+    sh = torch.randn(C, device=gpu) * 0.2
+    pooled = fn.bnrelu_avgpool(x, sc, sh)
+    r = torch.relu(x.float() * sc + sh).mean(dim=(1, 2))
+    assert _rel(pooled, r) < 1e-2
+    ld = 16
+    logits = torch.zeros(N, ld, device=gpu)
+    logits[:, :classes] = torch.randn(N, classes, device=gpu) * 3
+    labels = torch.randint(0, classes, (N,), device=gpu)
+    loss, corr, dl, db, probs = fn.softmax_xent(logits, labels, classes, 1.0 / N, want_probs=True)
+    z = logits[:, :classes].clone().requires_grad_(True)
+    lr_ = ref.softmax_cross_entropy(z, labels)
+    lr_.backward()
+    assert abs(loss.item() / N - lr_.item()) < 1e-4
+    acc = (z.argmax(1) == labels).float().sum().item()
+    assert corr.item() == acc
+    assert _rel(dl[:, :classes], z.grad) < 1e-2
+    assert torch.all(dl[:, classes:] == 0)
+    torch.testing.assert_close(db, z.grad.sum(0), rtol=1e-4, atol=1e-6)
+    dp = torch.randn(N, C, device=gpu).to(BF)
+    dx = fn.avgpool_bwd(dp, HW, HW)
+    torch.testing.assert_close(dx.float(), (dp.float() / (HW * HW))[:, None, None, :].expand(N, HW, HW, C),
+                               rtol=1e-2, atol=1e-3)
+
+
+def test_maxpool(gpu):
+    torch.manual_seed(8)
+    x = torch.randn(2, 112, 112, 64, device=gpu).to(BF)
+    y = fn.maxpool_fwd(x)
+    xf = x.float().requires_grad_(True)
+    r = ref.max_pool_same(xf)
+    assert y.shape == r.shape == (2, 56, 56, 64)
+    torch.testing.assert_close(y.float(), r.detach())
+    dy = torch.randn_like(r).to(BF)
+    r.backward(dy.float())
+    dx = fn.maxpool_bwd(x, dy)
+    assert _rel(dx, xf.grad) < 1e-2
+
+
+def test_cifar_augment(gpu):
+    torch.manual_seed(9)
+    img = torch.randint(0, 256, (8, 3, 32, 32), dtype=torch.uint8, device=gpu)
+    out, log = fn.cifar_augment(img, cpad=8, pad=4, seed=123, train=True, log_crops=True)
+    assert out.shape == (8, 32, 32, 8)
+    for n in range(8):
+        oy, ox, flip = log[n].tolist()
+        hwc = img[n].permute(1, 2, 0).float()
+        padded = torch.zeros(40, 40, 3, device=gpu)
+        padded[4:36, 4:36] = hwc
+        crop = padded[oy:oy + 32, ox:ox + 32]
+        if flip:
+            crop = crop.flip(1)
+        r = ref.per_image_standardization(crop)
+        assert _rel(out[n, :, :, :3], r) < 1e-2
+        assert torch.all(out[n, :, :, 3:] == 0)
+    ev = fn.cifar_augment(img, cpad=8, train=False)
+    r0 = ref.per_image_standardization(img[0].permute(1, 2, 0))
+    assert _rel(ev[0, :, :, :3], r0) < 1e-2
