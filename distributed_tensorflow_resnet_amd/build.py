@@ -34,8 +34,11 @@ COMMON_FLAGS = [
 
 
 def _sources():
+    """Device code (*.hip), host-only C++ (*.cpp except the bindings), bindings."""
     hips = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
-    return [os.path.join(CSRC, f) for f in hips], os.path.join(CSRC, "bindings.cpp")
+    hosts = sorted(f for f in os.listdir(CSRC) if f.endswith(".cpp") and f != "bindings.cpp")
+    return ([os.path.join(CSRC, f) for f in hips] + [os.path.join(CSRC, f) for f in hosts],
+            os.path.join(CSRC, "bindings.cpp"))
 
 
 def _headers_digest() -> str:

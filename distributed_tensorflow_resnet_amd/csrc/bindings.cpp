@@ -298,6 +298,10 @@ static void def_op(py::module_& m, py::class_<Plan>& plan, const char* name,
   plan.def(name, [maker, name](Plan& p, Args... args) { return p.add(maker(args...), name); });
 }
 
+namespace dtr {
+uint32_t crc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
+}
+
 static int hip_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -350,6 +354,15 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("param_seg_bytes", []() { return (int)sizeof(ParamSeg); });
   m.def("device_count", &hip_device_count);
+  m.def(
+      "crc32c",
+      [](py::buffer b, uint32_t crc) {
+        py::buffer_info info = b.request();
+        const size_t n = (size_t)info.size * (size_t)info.itemsize;
+        py::gil_scoped_release nogil;
+        return dtr::crc32c_extend(crc, reinterpret_cast<const uint8_t*>(info.ptr), n);
+      },
+      py::arg("data"), py::arg("crc") = 0);
   m.def("device_synchronize", []() {
     py::gil_scoped_release nogil;
     return (int)hipDeviceSynchronize();

@@ -1,0 +1,88 @@
+"""Process-group context: one process per GPU, torch.distributed over RCCL.
+
+Replaces the reference's two distribution runtimes:
+  * Horovod (`hvd.init()`, `hvd.DistributedOptimizer`, BroadcastGlobalVariablesHook)
+  * TF parameter servers (`tf.train.Server`, `replica_device_setter`,
+    `SyncReplicasOptimizer`, gRPC)
+with synchronous data parallelism: backend "nccl" (= RCCL on ROCm, ring /
+tree collectives over the xGMI links) for GPU ranks, "gloo" for CPU ranks.
+Rendezvous is the standard env:// contract (RANK, WORLD_SIZE, LOCAL_RANK,
+MASTER_ADDR, MASTER_PORT) set by torchrun or parallel/launch.py.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+class DistContext:
+    """Thin, explicit wrapper so the engine never touches global state."""
+
+    def __init__(self, backend: str | None = None, device: torch.device | None = None,
+                 timeout_s: float = 600.0):
+        self.rank, self.world_size, self.local_rank = env_world()
+        self.backend = backend
+        self.device = device
+        self.initialized_here = False
+        if self.world_size > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            self.backend = backend
+            kw = {}
+            if backend == "nccl" and device is not None:
+                kw["device_id"] = device
+            dist.init_process_group(backend=backend, init_method="env://", rank=self.rank,
+                                    world_size=self.world_size,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            self.initialized_here = True
+        elif dist.is_initialized():
+            self.backend = dist.get_backend()
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def active(self) -> bool:
+        return self.world_size > 1 and dist.is_initialized()
+
+    def all_reduce_async(self, t: torch.Tensor):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        if self.active:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        if self.active:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.active:
+            dist.broadcast(t, src)
+        return t
+
+    def barrier(self):
+        if self.active:
+            if self.backend == "nccl" and self.device is not None:
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def shutdown(self):
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()

@@ -1,0 +1,750 @@
+"""GPU training engine: flat buffers + one static native plan per step.
+
+This replaces the reference's TF graph + MonitoredTrainingSession hot loop
+(`mon_sess.run(train_op)`, resnet_cifar_main.py:339-358).  The
+ResNet v2 graph is static, so instead of an autograd tape the engine records
+ONE native plan (csrc/bindings.cpp `Plan`) holding every launch of a training
+step with all pointers bound:
+
+  forward   input augmentation -> stem -> blocks -> BN-ReLU+avg-pool -> dense ->
+            softmax-xent (+training precision, +dense-bias grad)
+            * BN-ReLU is never materialised: each conv applies the previous BN's
+              scale/shift + ReLU while staging its A operand (PRE), and emits the
+              next BN's Welford partials from its epilogue (STATS);
+            * the residual add is fused into the last conv of each block;
+  backward  hand-scheduled reverse pass: per conv a dgrad (MFMA) and a split-K
+            wgrad (MFMA, fused BN-ReLU recompute of its input) + deterministic
+            reduce into the flat fp32 gradient; per BN one reduce / finalize /
+            apply (ReLU mask and residual-gradient add fused);
+  allreduce cut points after the op that finalises each gradient bucket
+            (parallel/buckets.py) -> RCCL all-reduce on torch.distributed's
+            NCCL stream, overlapping the rest of backward;
+  optimizer one fused SGD-momentum + weight-decay + bf16 re-pack launch, LR from
+            the device-resident global_step, then global_step += 1.
+
+The plan runs natively segment by segment (no Python per op) and the whole
+step is captured once into a hipGraph (torch.cuda.CUDAGraph), so a step costs
+one graph launch on the host.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import native
+from ..models.params import ParamStore
+from ..models.spec import BNSpec, ConvSpec, ModelSpec
+from ..parallel.buckets import assign_buckets, schedule_buckets
+
+BF16 = torch.bfloat16
+BN_DECAY = 0.997
+BN_EPS = 1e-5
+
+SEG_DTYPE = np.dtype([
+    ("offset", "<i8"), ("numel", "<i8"), ("bf_ohwi", "<i8"), ("bf_hwio", "<i8"),
+    ("kh", "<i4"), ("kw", "<i4"), ("C", "<i4"), ("K", "<i4"), ("cpad", "<i4"), ("kpad", "<i4"),
+])
+
+
+@dataclass
+class LRSchedule:
+    """Piecewise LR evaluated on the device (see csrc/optim.h LrSchedule)."""
+    init: float
+    bounds: list
+    values: list
+    warm_steps: int = 0
+    warm_from: float = 0.0
+    warm_to: float = 0.0
+
+    def at(self, step: int) -> float:
+        """Host mirror of the device formula (used by hooks/tests)."""
+        if step <= 0:
+            return self.init
+        t = step - 1
+        if t < self.warm_steps:
+            return self.warm_from + (self.warm_to - self.warm_from) * t / self.warm_steps
+        for b, v in zip(self.bounds, self.values):
+            if t < b:
+                return v
+        return self.values[-1]
+
+
+def cifar_lr_schedule() -> LRSchedule:
+    """resnet_cifar_main.py:304-324 (begin() = 0.1)."""
+    return LRSchedule(0.1, [40000, 60000, 80000], [0.1, 0.01, 0.001, 0.0001])
+
+
+def imagenet_lr_schedule() -> LRSchedule:
+    """resnet_imagenet_main.py:306-329: warm-up 0.1->0.4 over 6240 steps (begin()=0.4)."""
+    return LRSchedule(0.4, [37440, 74880, 99840], [0.4, 0.04, 0.004, 0.0004],
+                      warm_steps=6240, warm_from=0.1, warm_to=0.4)
+
+
+def constant_lr(lr: float) -> LRSchedule:
+    return LRSchedule(lr, [], [lr])
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b
+
+
+@dataclass
+class _BN:
+    spec: BNSpec
+    gamma: int          # pointers into master / grad / stats buffers
+    beta: int
+    dgamma: int
+    dbeta: int
+    mmean: int
+    mvar: int
+    mean: torch.Tensor = None
+    rstd: torch.Tensor = None
+    scale: torch.Tensor = None
+    shift: torch.Tensor = None
+    # stat source of the forward partials: (tiles, tile_rows, M)
+    src: tuple = None
+    names: tuple = ()
+
+
+@dataclass
+class _Conv:
+    spec: ConvSpec
+    cin: int            # effective (padded) input channels
+    ohwi: int           # bf16 pointers
+    hwio: int
+    grad: int           # fp32 gradient pointer (TF HWIO)
+    cin_valid: int
+    name: str = ""
+
+
+class Engine:
+    """Owns all device state of one data-parallel rank."""
+
+    def __init__(self, spec: ModelSpec, batch_size: int, *, weight_decay: float,
+                 lr_schedule: LRSchedule, optimizer: str = "mom", momentum: float = 0.9,
+                 device=None, dist_ctx=None, bucket_mb: float = 25.0, seed: int = 0,
+                 input_mode: str = "auto", global_batch: int | None = None,
+                 use_graph: bool = True, data_seed: int = 1234):
+        self.nat = native(required=True)
+        self.spec = spec
+        self.N = batch_size
+        self.device = torch.device(device or "cuda")
+        self.dist = dist_ctx
+        self.world = dist_ctx.world_size if dist_ctx is not None else 1
+        self.global_batch = global_batch or batch_size * self.world
+        self.wd = float(weight_decay)
+        self.momentum = float(momentum)
+        self.use_momentum = optimizer == "mom"
+        self.sched = lr_schedule
+        self.use_graph = use_graph
+        self.data_seed = data_seed
+        if input_mode == "auto":
+            input_mode = "cifar_u8" if spec.dataset.startswith("cifar") else "nhwc"
+        self.input_mode = input_mode
+        self.kpad = _ceil(spec.num_classes, 16) * 16
+        self.cpad_in = 8
+
+        dev = self.device
+        self.params = ParamStore(spec, device=dev)
+        self.params.initialize(seed)
+        self.grad = torch.zeros(self.params.n_train, device=dev)
+        self.mom = torch.zeros(self.params.n_train, device=dev)
+        self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.scalars = torch.zeros(8, device=dev)  # loss_sum, correct, lr, l2
+        self._build_weight_layout()
+        self._alloc_activations()
+        self.plan = self.nat.Plan()
+        self._keep = []   # tensors referenced by the plan
+        self.ready_index: dict[str, int] = {}
+        self._build_train_plan()
+        if self.dist is not None and self.world > 1:
+            self.buckets = assign_buckets(self.params.train_slots, int(bucket_mb * 2 ** 20))
+            self.bucket_sched = schedule_buckets(self.buckets, self.ready_index)
+        else:
+            self.buckets, self.bucket_sched = [], []
+        self.graph = None
+        self._captured = False
+        self.eval_plans = {}
+        self.repack()
+
+    # ------------------------------------------------------------------ layout
+    def _build_weight_layout(self):
+        spec = self.spec
+        ps = self.params
+        mptr = ps.master.data_ptr()
+        gptr = self.grad.data_ptr()
+        segs = []
+        bf_total = 0
+        self.convs: dict[str, _Conv] = {}
+        conv_specs = {c.name: c for c in spec.all_convs()}
+        for s in ps.train_slots:
+            rec = np.zeros(1, dtype=SEG_DTYPE)[0]
+            rec["offset"], rec["numel"] = s.offset, s.numel
+            rec["bf_ohwi"] = rec["bf_hwio"] = -1
+            if s.kind == "conv":
+                c = conv_specs[s.name.split("/")[0]]
+                taps = c.kh * c.kw
+                cpad = self.cpad_in if c.cin < 8 else c.cin
+                rec["kh"], rec["kw"], rec["C"], rec["K"] = c.kh, c.kw, c.cin, c.cout
+                rec["cpad"], rec["kpad"] = cpad, c.cout
+                rec["bf_ohwi"] = bf_total
+                bf_total += c.cout * taps * cpad
+                if c.cin >= 8:   # the stem never needs dgrad
+                    rec["bf_hwio"] = bf_total
+                    bf_total += taps * c.cin * c.cout
+            elif s.kind == "dense_kernel":
+                F, classes = s.shape
+                rec["kh"], rec["kw"], rec["C"], rec["K"] = 1, 1, F, classes
+                rec["cpad"], rec["kpad"] = F, self.kpad
+                rec["bf_ohwi"] = bf_total
+                bf_total += self.kpad * F
+                rec["bf_hwio"] = bf_total
+                bf_total += F * self.kpad
+            else:
+                rec["kh"] = rec["kw"] = 1
+                rec["C"], rec["K"] = 1, 1
+                rec["cpad"], rec["kpad"] = 1, 1
+            segs.append(rec)
+        seg_arr = np.array(segs, dtype=SEG_DTYPE)
+        assert SEG_DTYPE.itemsize == self.nat.param_seg_bytes()
+        self.segs = torch.from_numpy(seg_arr.view(np.uint8).copy()).to(self.device)
+        self.nseg = len(segs)
+        self.wbf = torch.zeros(max(bf_total, 1), dtype=BF16, device=self.device)
+        bptr = self.wbf.data_ptr()
+        for rec, s in zip(seg_arr, ps.train_slots):
+            if s.kind == "conv":
+                c = conv_specs[s.name.split("/")[0]]
+                cin = self.cpad_in if c.cin < 8 else c.cin
+                self.convs[c.name] = _Conv(
+                    c, cin, bptr + 2 * int(rec["bf_ohwi"]),
+                    bptr + 2 * int(rec["bf_hwio"]) if rec["bf_hwio"] >= 0 else 0,
+                    gptr + 4 * s.offset, c.cin, s.name)
+            elif s.kind == "dense_kernel":
+                self.dense_ohwi = bptr + 2 * int(rec["bf_ohwi"])
+                self.dense_hwio = bptr + 2 * int(rec["bf_hwio"])
+                self.dense_grad = gptr + 4 * s.offset
+                self.dense_name = s.name
+        bslot = ps.slot("dense/bias")
+        self.dense_bias = mptr + 4 * bslot.offset
+        self.dense_bias_grad = gptr + 4 * bslot.offset
+
+        # BatchNorm bookkeeping
+        self.bns: dict[str, _BN] = {}
+        sptr = ps.stats.data_ptr()
+        bn_specs = [b for blk in spec.blocks for b in blk.bns] + [spec.final_bn]
+        total_c = sum(b.channels for b in bn_specs)
+        self.bnbuf = torch.zeros(4 * total_c, device=self.device)
+        off = 0
+        for b in bn_specs:
+            g = ps.slot(f"{b.name}/gamma")
+            be = ps.slot(f"{b.name}/beta")
+            mm = ps.slot(f"{b.name}/moving_mean")
+            mv = ps.slot(f"{b.name}/moving_variance")
+            C = b.channels
+            e = _BN(b, mptr + 4 * g.offset, mptr + 4 * be.offset, gptr + 4 * g.offset,
+                    gptr + 4 * be.offset, sptr + 4 * mm.offset, sptr + 4 * mv.offset,
+                    names=(g.name, be.name))
+            e.mean = self.bnbuf[off:off + C]
+            e.rstd = self.bnbuf[total_c + off:total_c + off + C]
+            e.scale = self.bnbuf[2 * total_c + off:2 * total_c + off + C]
+            e.shift = self.bnbuf[3 * total_c + off:3 * total_c + off + C]
+            off += C
+            self.bns[b.name] = e
+
+    def _alloc_activations(self):
+        spec, N, dev = self.spec, self.N, self.device
+        H, W = spec.image_h, spec.image_w
+        if self.input_mode == "cifar_u8":
+            self.img_u8 = torch.zeros((N, 3, H, W), dtype=torch.uint8, device=dev)
+        self.x_in = torch.zeros((N, H, W, self.cpad_in), dtype=BF16, device=dev)
+        self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
+        st = spec.stem
+        self.stem_out = torch.empty((N, st.ho, st.wo, st.cout), dtype=BF16, device=dev)
+        if spec.maxpool:
+            mh = _ceil(st.ho, 2)
+            self.pool_out = torch.empty((N, mh, mh, st.cout), dtype=BF16, device=dev)
+        self.X = []     # block inputs (X[i] = input of block i, X[-1] = last output)
+        self.H1, self.H2 = [], []
+        x0 = self.pool_out if spec.maxpool else self.stem_out
+        self.X.append(x0)
+        max_act = x0.numel()
+        sc_max = 0
+        for b in spec.blocks:
+            f = b.convs[0].cout
+            if b.kind == "building":
+                self.H1.append(torch.empty((N, b.ho, b.wo, f), dtype=BF16, device=dev))
+                self.H2.append(None)
+            else:
+                self.H1.append(torch.empty((N, b.h, b.w, f), dtype=BF16, device=dev))
+                self.H2.append(torch.empty((N, b.ho, b.wo, f), dtype=BF16, device=dev))
+            self.X.append(torch.empty((N, b.ho, b.wo, b.cout), dtype=BF16, device=dev))
+            if b.proj is not None:
+                sc_max = max(sc_max, N * b.ho * b.wo * b.cout)
+            max_act = max(max_act, N * b.h * b.w * b.cin, N * b.ho * b.wo * b.cout,
+                          N * b.h * b.w * f)
+        max_act = max(max_act, self.stem_out.numel())
+        self.sc_buf = torch.empty(max(sc_max, 1), dtype=BF16, device=dev)
+        self.G = [torch.empty(max_act, dtype=BF16, device=dev) for _ in range(3)]
+        F = spec.dense_in
+        self.pooled = torch.empty((N, F), dtype=BF16, device=dev)
+        self.dpooled = torch.empty((N, F), dtype=BF16, device=dev)
+        self.logits = torch.empty((N, self.kpad), device=dev)
+        self.dlogits = torch.empty((N, self.kpad), dtype=BF16, device=dev)
+        # scratch: BN forward partials, BN backward partials, wgrad split-K slabs
+        max_stat = 1
+        max_bwd = 1
+        for b in list(self.bns.values()):
+            C = b.spec.channels
+            M = N * b.spec.h * b.spec.w
+            bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
+            max_stat = max(max_stat, _ceil(M, bm) * 2 * C)
+            max_bwd = max(max_bwd, self.nat.bn_bwd_tiles(M, C) * 2 * C)
+        self.stat_part = torch.empty(max_stat, device=dev)
+        self.bwd_part = torch.empty(max_bwd, device=dev)
+        max_c = max(b.spec.channels for b in self.bns.values())
+        self.coef = torch.empty(3 * max_c, device=dev)
+        wg = 1
+        for c in self.convs.values():
+            sp, _ = self.nat.wgrad_pick_splits(self._geom(c, N))
+            wg = max(wg, sp * c.spec.cout * c.spec.kh * c.spec.kw * c.cin)
+        g = self._dense_geom(N)
+        sp, _ = self.nat.wgrad_pick_splits(g)
+        wg = max(wg, sp * self.kpad * F)
+        self.wg_part = torch.empty(wg, device=dev)
+        self.l2_ws = torch.empty(self.nat.l2_workspace_floats(), device=dev)
+
+    # ------------------------------------------------------------------ helpers
+    def _geom(self, c: _Conv, N):
+        s = c.spec
+        return [N, s.h, s.w, c.cin, s.ho, s.wo, s.cout, s.kh, s.kw, s.stride, (s.kh - 1) // 2]
+
+    def _dense_geom(self, N):
+        return [N, 1, 1, self.spec.dense_in, 1, 1, self.kpad, 1, 1, 1, 0]
+
+    def _conv_fwd(self, plan, c: _Conv, x, out, N, pre: _BN | None = None, residual=None,
+                  stats_for: _BN | None = None):
+        geom = self._geom(c, N)
+        stat_ptr = 0
+        if stats_for is not None:
+            M = N * c.spec.ho * c.spec.wo
+            bm = self.nat.conv_gemm_bm(M, c.spec.cout)
+            stats_for.src = (_ceil(M, bm), bm, M)
+            stat_ptr = self.stat_part.data_ptr()
+        plan.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
+                       0 if residual is None else residual.data_ptr(),
+                       0 if pre is None else pre.scale.data_ptr(),
+                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom)
+
+    def _bn_finalize(self, plan, bn: _BN, train=True):
+        tiles, rows, M = bn.src
+        plan.bn_finalize(self.stat_part.data_ptr(), tiles, rows, M, bn.spec.channels, bn.gamma,
+                         bn.beta, bn.mmean, bn.mvar, BN_DECAY, BN_EPS, int(train),
+                         bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
+                         bn.shift.data_ptr())
+
+    def _mark(self, plan, *names):
+        idx = plan.size()
+        for n in names:
+            self.ready_index[n] = idx
+
+    def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False):
+        """wgrad (+reduce into the flat gradient) and optionally dgrad into dx."""
+        geom = self._geom(c, N)
+        sp, pps = self.nat.wgrad_pick_splits(geom)
+        plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
+                        0 if pre is None else pre.scale.data_ptr(),
+                        0 if pre is None else pre.shift.data_ptr(),
+                        self.wg_part.data_ptr(), geom, sp, pps)
+        s = c.spec
+        plan.wgrad_reduce(self.wg_part.data_ptr(), c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin,
+                          c.cin_valid, 1.0, 0)
+        self._mark(plan, c.name)
+        if dx is not None:
+            plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
+                           int(accumulate), geom)
+
+    def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None):
+        C = bn.spec.channels
+        M = x.numel() // C
+        tiles = self.nat.bn_bwd_tiles(M, C)
+        plan.bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
+                           bn.scale.data_ptr(), bn.shift.data_ptr(), M, C,
+                           self.bwd_part.data_ptr())
+        plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
+                             bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
+        self._mark(plan, *bn.names)
+        plan.bn_bwd_apply(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
+                          bn.scale.data_ptr(), bn.shift.data_ptr(), self.coef.data_ptr(),
+                          0 if add is None else add.data_ptr(), dx.data_ptr(), M, C)
+
+    def _g(self, i, shape):
+        n = math.prod(shape)
+        return self.G[i][:n].view(shape)
+
+    # ------------------------------------------------------------------ plan
+    def _build_train_plan(self):
+        plan, spec, N = self.plan, self.spec, self.N
+        self.seg = {}
+        b0 = plan.size()
+        # ---- input
+        if self.input_mode == "cifar_u8":
+            plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
+                               spec.image_w, self.cpad_in, 4, self.data_seed,
+                               self.gstep.data_ptr(), 1, 0)
+        # ---- forward
+        stem = self.convs[spec.stem.name]
+        blocks = spec.blocks
+        first_bn = self.bns[blocks[0].bns[0].name]
+        if spec.maxpool:
+            self._conv_fwd(plan, stem, self.x_in, self.stem_out, N)
+            st = spec.stem
+            ph = _ceil(st.ho, 2)
+            pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
+            plan.maxpool_fwd(self.stem_out.data_ptr(), self.pool_out.data_ptr(),
+                             [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
+            M = N * ph * ph
+            plan.bn_stats(self.pool_out.data_ptr(), M, st.cout, self.stat_part.data_ptr())
+            first_bn.src = (self.nat.bn_bwd_tiles(M, st.cout), self.nat.bn_stats_tile_rows(), M)
+        else:
+            self._conv_fwd(plan, stem, self.x_in, self.stem_out, N, stats_for=first_bn)
+        for i, b in enumerate(blocks):
+            X, Xn = self.X[i], self.X[i + 1]
+            bns = [self.bns[s.name] for s in b.bns]
+            convs = [self.convs[c.name] for c in b.convs]
+            nxt = self.bns[blocks[i + 1].bns[0].name] if i + 1 < len(blocks) else \
+                self.bns[spec.final_bn.name]
+            self._bn_finalize(plan, bns[0])
+            residual = X
+            if b.proj is not None:
+                pc = self.convs[b.proj.name]
+                sc = self.sc_buf[:N * b.ho * b.wo * b.cout].view(N, b.ho, b.wo, b.cout)
+                self._conv_fwd(plan, pc, X, sc, N, pre=bns[0])
+                residual = sc
+            if b.kind == "building":
+                self._conv_fwd(plan, convs[0], X, self.H1[i], N, pre=bns[0], stats_for=bns[1])
+                self._bn_finalize(plan, bns[1])
+                self._conv_fwd(plan, convs[1], self.H1[i], Xn, N, pre=bns[1], residual=residual,
+                               stats_for=nxt)
+            else:
+                self._conv_fwd(plan, convs[0], X, self.H1[i], N, pre=bns[0], stats_for=bns[1])
+                self._bn_finalize(plan, bns[1])
+                self._conv_fwd(plan, convs[1], self.H1[i], self.H2[i], N, pre=bns[1],
+                               stats_for=bns[2])
+                self._bn_finalize(plan, bns[2])
+                self._conv_fwd(plan, convs[2], self.H2[i], Xn, N, pre=bns[2], residual=residual,
+                               stats_for=nxt)
+        fbn = self.bns[spec.final_bn.name]
+        self._bn_finalize(plan, fbn)
+        XL = self.X[-1]
+        HL, WL, F = XL.shape[1], XL.shape[2], XL.shape[3]
+        plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
+                            self.pooled.data_ptr(), N, HL * WL, F)
+        plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
+                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N))
+        sp = self.scalars.data_ptr()
+        plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
+                          spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
+                          self.dense_bias_grad, 1.0 / self.global_batch, 0)
+        self._mark(plan, "dense/bias")
+        plan.l2_half_sum(self.params.master.data_ptr(), self.params.n_train,
+                         self.l2_ws.data_ptr(), sp + 12)
+        self.seg["fwd"] = (b0, plan.size())
+
+        # ---- backward
+        b1 = plan.size()
+        dg = self._dense_geom(N)
+        spl, pps = self.nat.wgrad_pick_splits(dg)
+        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0,
+                        self.wg_part.data_ptr(), dg, spl, pps)
+        plan.wgrad_reduce(self.wg_part.data_ptr(), self.dense_grad, spl, self.kpad,
+                          spec.num_classes, 1, F, F, 1.0, 0)
+        self._mark(plan, self.dense_name)
+        plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
+                       0, 0, 0, 0, 0, 0, dg)
+        dact = self._g(0, (N, HL, WL, F))
+        plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
+        d = 1
+        dout = self._g(d, tuple(XL.shape))
+        self._bn_bwd(plan, fbn, dact, XL, dout)
+        for i in range(len(blocks) - 1, -1, -1):
+            b = blocks[i]
+            X = self.X[i]
+            bns = [self.bns[s.name] for s in b.bns]
+            convs = [self.convs[c.name] for c in b.convs]
+            o1, o2 = [j for j in range(3) if j != d]
+            if b.kind == "building":
+                h1 = self.H1[i]
+                da = self._g(o1, tuple(h1.shape))
+                self._conv_bwd(plan, convs[1], dout, h1, N, bns[1], dx=da)
+                dh = self._g(o2, tuple(h1.shape))
+                self._bn_bwd(plan, bns[1], da, h1, dh)
+                dcur = dh
+            else:
+                h1, h2 = self.H1[i], self.H2[i]
+                da = self._g(o1, tuple(h2.shape))
+                self._conv_bwd(plan, convs[2], dout, h2, N, bns[2], dx=da)
+                dh2 = self._g(o2, tuple(h2.shape))
+                self._bn_bwd(plan, bns[2], da, h2, dh2)
+                da = self._g(o1, tuple(h1.shape))
+                self._conv_bwd(plan, convs[1], dh2, h1, N, bns[1], dx=da)
+                dh1 = self._g(o2, tuple(h1.shape))
+                self._bn_bwd(plan, bns[1], da, h1, dh1)
+                dcur = dh1
+            da1 = self._g(o1, tuple(X.shape))
+            self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=da1)
+            if b.proj is not None:
+                self._conv_bwd(plan, self.convs[b.proj.name], dout, X, N, bns[0], dx=da1,
+                               accumulate=True)
+            dx = self._g(o2, tuple(X.shape))
+            self._bn_bwd(plan, bns[0], da1, X, dx, add=None if b.proj is not None else dout)
+            dout, d = dx, o2
+        # stem (no dgrad: the input needs no gradient)
+        if spec.maxpool:
+            dstem = self._g((d + 1) % 3, tuple(self.stem_out.shape))
+            st = spec.stem
+            ph = _ceil(st.ho, 2)
+            pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
+            plan.maxpool_bwd(self.stem_out.data_ptr(), dout.data_ptr(), dstem.data_ptr(),
+                             [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
+            self._conv_bwd(plan, stem, dstem, self.x_in, N, None)
+        else:
+            self._conv_bwd(plan, stem, dout, self.x_in, N, None)
+        self.seg["bwd"] = (b1, plan.size())
+
+        # ---- optimizer
+        b2 = plan.size()
+        s = self.sched
+        plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
+                             self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
+                             s.warm_from, s.warm_to, list(s.bounds), list(s.values),
+                             self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
+                             int(self.use_momentum), self.segs.data_ptr(), self.nseg,
+                             self.wbf.data_ptr(), sp + 8, 1)
+        plan.step_increment(self.gstep.data_ptr())
+        self.seg["opt"] = (b2, plan.size())
+        missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
+        assert not missing, f"gradients never produced: {missing[:4]}"
+
+    # ------------------------------------------------------------------ running
+    def repack(self):
+        """Refresh the bf16 weight copies from the fp32 master (no update)."""
+        s = self.sched
+        self.nat.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
+                                 self.mom.data_ptr(), self.params.n_train, s.init, 0, 0.0, 0.0, [],
+                                 [s.init], 0, 0.0, 0.0, 1.0, 0, self.segs.data_ptr(), self.nseg,
+                                 self.wbf.data_ptr(), 0, 0, torch.cuda.current_stream().cuda_stream)
+
+    def _run(self, name, stream):
+        a, b = self.seg[name]
+        self.plan.run(a, b, stream)
+
+    def _step_eager(self):
+        st = torch.cuda.current_stream().cuda_stream
+        self._run("fwd", st)
+        a, b = self.seg["bwd"]
+        works = []
+        if self.bucket_sched:
+            prev = a
+            for idx, lo, hi in self.bucket_sched:
+                if idx > prev:
+                    self.plan.run(prev, idx, st)
+                    prev = idx
+                works.append(self.dist.all_reduce_async(self.grad[lo:hi]))
+            if b > prev:
+                self.plan.run(prev, b, st)
+            for w in works:
+                w.wait()
+        else:
+            self.plan.run(a, b, st)
+        self._run("opt", st)
+
+    def capture(self, warmup: int = 2):
+        """Run `warmup` real steps on a side stream, then capture one step."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_eager()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_eager()
+        self.graph = g
+        self._captured = True
+        return warmup
+
+    def step(self):
+        """One training step (global_step += 1 on the device)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step_eager()
+
+    # ------------------------------------------------------------------ io
+    def set_batch(self, images, labels):
+        """Copy a host/device batch into the static input buffers."""
+        if self.input_mode == "cifar_u8":
+            self.img_u8.copy_(images, non_blocking=True)
+        else:
+            x = images
+            if x.dim() == 4 and x.shape[-1] != self.cpad_in:
+                xp = torch.zeros(self.x_in.shape, dtype=BF16, device=self.device)
+                xp[..., :x.shape[-1]] = x.to(self.device, BF16)
+                x = xp
+            self.x_in.copy_(x, non_blocking=True)
+        self.labels.copy_(labels.to(torch.int32), non_blocking=True)
+
+    def fill_synthetic(self, seed: int = 0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        if self.input_mode == "cifar_u8":
+            self.img_u8.copy_(torch.randint(0, 256, tuple(self.img_u8.shape), generator=g,
+                                            dtype=torch.uint8))
+        else:
+            npix = self.N * self.spec.image_h * self.spec.image_w
+            self.nat.synthetic_images(self.x_in.data_ptr(), npix, 3, self.cpad_in, seed,
+                                      torch.cuda.current_stream().cuda_stream)
+        self.labels.copy_(torch.randint(0, self.spec.num_classes, (self.N,), generator=g,
+                                        dtype=torch.int32))
+
+    def metrics(self) -> dict:
+        """Host read of the last step's scalars (synchronises)."""
+        v = self.scalars.detach().cpu().tolist()
+        loss_sum, correct, lr, l2 = v[0], v[1], v[2], v[3]
+        if self.dist is not None and self.world > 1:
+            t = torch.tensor([loss_sum, correct], device=self.device)
+            self.dist.all_reduce_sum(t)
+            loss_sum, correct = t.tolist()
+            n = self.N * self.world
+        else:
+            n = self.N
+        xent = loss_sum / n
+        return {"global_step": int(self.gstep.item()), "cross_entropy": xent,
+                "cost": xent + self.wd * l2, "precision": correct / n, "lr": lr, "l2": l2}
+
+    def sync_from_params(self):
+        """After loading master/stats from a checkpoint: reset step and repack."""
+        self.gstep.fill_(self.params.global_step)
+        self.repack()
+
+    def broadcast_parameters(self, src: int = 0):
+        """hvd.BroadcastGlobalVariablesHook(0) equivalent: weights, momentum,
+        BN moving statistics and global_step from `src` to every rank."""
+        if self.dist is None or self.world == 1:
+            return
+        for t in (self.params.master, self.params.stats, self.mom, self.gstep):
+            self.dist.broadcast(t, src)
+        self.repack()
+
+    # ------------------------------------------------------------------ eval
+    def build_eval_plan(self, batch: int):
+        """Forward-only plan in inference mode (BN from moving statistics)."""
+        if batch in self.eval_plans:
+            return self.eval_plans[batch]
+        ev = _EvalPlan(self, batch)
+        self.eval_plans[batch] = ev
+        return ev
+
+
+class _EvalPlan:
+    """Inference forward (resnet_cifar_main.py:361-421 evaluate()): batch-norm
+    with moving statistics, no statistics update, softmax probabilities."""
+
+    def __init__(self, eng: Engine, N: int):
+        self.eng = eng
+        self.N = N
+        nat, spec, dev = eng.nat, eng.spec, eng.device
+        H, W = spec.image_h, spec.image_w
+        self.img_u8 = torch.zeros((N, 3, H, W), dtype=torch.uint8, device=dev)
+        self.x_in = torch.zeros((N, H, W, eng.cpad_in), dtype=BF16, device=dev)
+        self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.probs = torch.zeros((N, eng.kpad), device=dev)
+        self.logits = torch.zeros((N, eng.kpad), device=dev)
+        self.scalars = torch.zeros(4, device=dev)
+        p = nat.Plan()
+        self.plan = p
+        self.input_plan = nat.Plan()
+        self.input_plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, H, W,
+                                      eng.cpad_in, 4, 0, 0, 0, 0)
+        st = spec.stem
+        stem = eng.convs[st.name]
+        bufs = []
+
+        def buf(shape):
+            t = torch.empty(shape, dtype=BF16, device=dev)
+            bufs.append(t)
+            return t
+
+        for bn in eng.bns.values():
+            p.bn_eval(bn.gamma, bn.beta, bn.mmean, bn.mvar, BN_EPS, bn.spec.channels,
+                      bn.scale.data_ptr(), bn.shift.data_ptr())
+        y = buf((N, st.ho, st.wo, st.cout))
+        p.conv_gemm(0, self.x_in.data_ptr(), stem.ohwi, y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
+                    eng._geom(stem, N))
+        if spec.maxpool:
+            ph = _ceil(st.ho, 2)
+            pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
+            z = buf((N, ph, ph, st.cout))
+            p.maxpool_fwd(y.data_ptr(), z.data_ptr(),
+                          [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
+            y = z
+        x = y
+        for b in spec.blocks:
+            bns = [eng.bns[s.name] for s in b.bns]
+            convs = [eng.convs[c.name] for c in b.convs]
+            res = x
+            if b.proj is not None:
+                pc = eng.convs[b.proj.name]
+                res = buf((N, b.ho, b.wo, b.cout))
+                self._conv(p, pc, x, res, bns[0])
+            h = x
+            for j, c in enumerate(convs):
+                last = j == len(convs) - 1
+                o = buf((N, c.spec.ho, c.spec.wo, c.spec.cout))
+                self._conv(p, c, h, o, bns[j], residual=res if last else None)
+                h = o
+            x = h
+        fbn = eng.bns[spec.final_bn.name]
+        F = spec.dense_in
+        self.pooled = torch.empty((N, F), dtype=BF16, device=dev)
+        p.bnrelu_avgpool(x.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
+                         self.pooled.data_ptr(), N, x.shape[1] * x.shape[2], F)
+        p.conv_gemm(0, self.pooled.data_ptr(), eng.dense_ohwi, 0, self.logits.data_ptr(), 0, 0, 0,
+                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N))
+        sp = self.scalars.data_ptr()
+        p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
+                       spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
+        self._bufs = bufs
+
+    def _conv(self, p, c, x, out, pre, residual=None):
+        p.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
+                    0 if residual is None else residual.data_ptr(), pre.scale.data_ptr(),
+                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N))
+
+    def run(self, images=None, labels=None, raw_u8: bool = True):
+        """Returns (loss_sum, correct, probs[N, classes]) for one eval batch.
+
+        NOTE: shares the per-BN scale/shift buffers with the training plan, so
+        it must not run concurrently with a training step (the evaluator runs
+        in its own process, like the reference's side-car)."""
+        st = torch.cuda.current_stream().cuda_stream
+        if images is not None:
+            if raw_u8:
+                self.img_u8.copy_(images)
+                self.input_plan.run(0, self.input_plan.size(), st)
+            else:
+                x = images.to(self.eng.device)
+                if x.shape[-1] != self.eng.cpad_in:
+                    xp = torch.zeros(self.x_in.shape, device=self.eng.device)
+                    xp[..., :x.shape[-1]] = x.float()
+                    x = xp
+                self.x_in.copy_(x.to(BF16))
+        if labels is not None:
+            self.labels.copy_(labels.to(torch.int32))
+        self.plan.run(0, self.plan.size(), st)
+        v = self.scalars.cpu().tolist()
+        return v[0], v[1], self.probs[:, :self.eng.spec.num_classes]

@@ -1,0 +1,137 @@
+"""End-to-end: one engine training step (native plan, bf16 MFMA kernels) against
+the fp32 autograd execution of the same TF-semantics network (models/resnet_torch.py)."""
+import copy
+
+import pytest
+import torch
+
+from distributed_tensorflow_resnet_amd.models.params import ParamStore
+from distributed_tensorflow_resnet_amd.models.resnet_torch import TorchResNet
+from distributed_tensorflow_resnet_amd.models.spec import cifar_spec, imagenet_spec
+from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _make(spec, N, gpu, wd=2e-4):
+    eng = Engine(spec, N, weight_decay=wd, lr_schedule=cifar_lr_schedule(), device=gpu,
+                 input_mode="nhwc", use_graph=False)
+    torch.manual_seed(0)
+    imgs = torch.randn(N, spec.image_h, spec.image_w, 3, device=gpu).to(torch.bfloat16).float()
+    labels = torch.randint(0, spec.num_classes, (N,), device=gpu)
+    eng.set_batch(imgs, labels)
+    ref_store = ParamStore(spec, device=gpu)
+    ref_store.master.copy_(eng.params.master)
+    ref_store.stats.copy_(eng.params.stats)
+    return eng, imgs, labels, ref_store
+
+
+@pytest.mark.parametrize("spec_fn,N", [
+    (lambda: cifar_spec(8), 16),
+    (lambda: cifar_spec(20), 32),
+    (lambda: imagenet_spec(50, image_hw=64), 4),
+    (lambda: imagenet_spec(18, image_hw=64), 4),
+])
+def test_engine_step_matches_autograd(gpu, spec_fn, N):
+    spec = spec_fn()
+    eng, imgs, labels, ref_store = _make(spec, N, gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    eng._run("fwd", st)
+    eng._run("bwd", st)
+    torch.cuda.synchronize()
+    model = TorchResNet(spec, ref_store, emulate_bf16=True)
+    logits = model(imgs, True)
+    xent, cost = model.loss(logits, labels, 2e-4)
+    xent.backward()
+    m = eng.scalars.cpu()
+    assert abs(m[0].item() / N - xent.item()) < 2e-2 * max(1.0, xent.item())
+    g_ref = ref_store.master.grad
+    worst = []
+    for s in eng.params.train_slots:
+        a = eng.grad[s.offset:s.offset + s.numel]
+        b = g_ref[s.offset:s.offset + s.numel]
+        worst.append((_rel(a, b), s.name))
+    worst.sort(reverse=True)
+    print("worst per-tensor gradient rel err:", worst[:6], "global", _rel(eng.grad, g_ref))
+    assert _rel(eng.grad, g_ref) < 2e-2, worst[:5]
+    assert worst[0][0] < 0.1, worst[:5]
+    # BN moving statistics updated like TF (decay 0.997, Bessel variance)
+    assert _rel(eng.params.stats, ref_store.stats) < 1e-3
+
+
+def test_optimizer_step_and_pack(gpu):
+    spec = cifar_spec(8)
+    eng, imgs, labels, _ = _make(spec, 16, gpu)
+    w0 = eng.params.master.clone()
+    eng.step()
+    torch.cuda.synchronize()
+    g = eng.grad
+    lr = 0.1  # step 0 uses the hook's begin() value
+    expect = w0 - lr * (g + 2e-4 * w0)
+    torch.testing.assert_close(eng.params.master, expect, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(eng.mom, g + 2e-4 * w0, rtol=1e-5, atol=1e-7)
+    assert int(eng.gstep.item()) == 1
+    m = eng.metrics()
+    assert abs(m["lr"] - 0.1) < 1e-7
+    # bf16 copies track the master (forward OHWI layout of conv2d_2)
+    c = eng.convs["conv2d_2"]
+    s = eng.params.slot("conv2d_2/kernel")
+    w = eng.params.master[s.offset:s.offset + s.numel].view(s.shape)  # HWIO
+    n = w.numel()
+    off = (c.ohwi - eng.wbf.data_ptr()) // 2
+    ohwi = eng.wbf[off:off + n].view(s.shape[3], s.shape[0], s.shape[1], s.shape[2])
+    torch.testing.assert_close(ohwi.float(), w.permute(3, 0, 1, 2).to(torch.bfloat16).float())
+
+
+def test_graph_replay_matches_eager(gpu):
+    spec = cifar_spec(8)
+    e1, imgs, labels, _ = _make(spec, 16, gpu)
+    e2 = Engine(spec, 16, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu,
+                input_mode="nhwc")
+    e2.params.master.copy_(e1.params.master)
+    e2.params.stats.copy_(e1.params.stats)
+    e2.repack()
+    e2.set_batch(imgs, labels)
+    for _ in range(4):
+        e1.step()
+    e2.capture(warmup=2)
+    e2.step()
+    e2.step()
+    torch.cuda.synchronize()
+    assert int(e2.gstep.item()) == 4
+    torch.testing.assert_close(e1.params.master, e2.params.master, rtol=0, atol=0)
+
+
+def test_training_reduces_loss(gpu):
+    spec = cifar_spec(20)
+    eng = Engine(spec, 64, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu)
+    eng.fill_synthetic(0)
+    eng.capture(warmup=2)
+    first = None
+    for i in range(60):
+        eng.step()
+        if i == 0:
+            first = eng.metrics()["cross_entropy"]
+    last = eng.metrics()["cross_entropy"]
+    assert last < first * 0.7, (first, last)
+
+
+def test_eval_plan_matches_autograd_eval(gpu):
+    spec = cifar_spec(8)
+    eng, imgs, labels, ref_store = _make(spec, 16, gpu)
+    for _ in range(3):
+        eng.step()
+    torch.cuda.synchronize()
+    ref_store.master.copy_(eng.params.master)
+    ref_store.stats.copy_(eng.params.stats)
+    ev = eng.build_eval_plan(8)
+    loss_sum, correct, probs = ev.run(imgs[:8], labels[:8], raw_u8=False)
+    model = TorchResNet(spec, ref_store)
+    with torch.no_grad():
+        logits = model(imgs[:8], False)
+    p_ref = torch.softmax(logits, 1)
+    assert _rel(probs, p_ref) < 2e-2
