@@ -45,7 +45,8 @@ static ConvGeom geom_from(const std::vector<int>& v) {
 // ---------------------------------------------------------------- op makers
 static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32, ptr_t residual,
                            ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
-                           ptr_t stat_part, int accumulate, std::vector<int> geom) {
+                           ptr_t stat_part, int accumulate, std::vector<int> geom,
+                           std::vector<ptr_t> bnb) {
   GemmArgs g{};
   g.a = P<const bf16>(a);
   g.b = P<const bf16>(b);
@@ -58,6 +59,16 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   g.nbias = nbias;
   g.stat_part = P<float>(stat_part);
   g.accumulate = accumulate;
+  if (!bnb.empty()) {  // [x, mean, rstd, scale, shift, part]: fused BN-ReLU backward reduce
+    if (bnb.size() != 6) throw std::invalid_argument("bnb needs 6 pointers");
+    if (mode != MODE_DGRAD) throw std::invalid_argument("bnb is dgrad-only");
+    g.bnb_x = P<const bf16>(bnb[0]);
+    g.bnb_mean = P<const float>(bnb[1]);
+    g.bnb_rstd = P<const float>(bnb[2]);
+    g.bnb_scale = P<const float>(bnb[3]);
+    g.bnb_shift = P<const float>(bnb[4]);
+    g.bnb_part = P<float>(bnb[5]);
+  }
   g.g = geom_from(geom);
   const ConvGeom& c = g.g;
   const int taps = c.kh * c.kw;
@@ -184,19 +195,21 @@ static Launch mk_softmax_xent(ptr_t logits, int ld, ptr_t labels, int N, int cla
   };
 }
 
-static Launch mk_maxpool_fwd(ptr_t x, ptr_t y, std::vector<int> geom, int k) {
+static Launch mk_maxpool_fwd(ptr_t x, ptr_t y, ptr_t argmax, std::vector<int> geom, int k) {
   ConvGeom g = geom_from(geom);
+  if (g.C % 8) throw std::invalid_argument("maxpool: C % 8");
   return [=](hipStream_t s) {
-    maxpool_fwd(P<const bf16>(x), P<bf16>(y), g.N, g.H, g.W, g.C, g.Ho, g.Wo, k, g.stride, g.pad,
-                s);
+    maxpool_fwd(P<const bf16>(x), P<bf16>(y), P<uint8_t>(argmax), g.N, g.H, g.W, g.C, g.Ho, g.Wo,
+                k, g.stride, g.pad, s);
   };
 }
 
-static Launch mk_maxpool_bwd(ptr_t x, ptr_t dy, ptr_t dx, std::vector<int> geom, int k) {
+static Launch mk_maxpool_bwd(ptr_t argmax, ptr_t dy, ptr_t dx, std::vector<int> geom, int k) {
   ConvGeom g = geom_from(geom);
+  if (g.C % 8) throw std::invalid_argument("maxpool: C % 8");
   return [=](hipStream_t s) {
-    maxpool_bwd(P<const bf16>(x), P<const bf16>(dy), P<bf16>(dx), g.N, g.H, g.W, g.C, g.Ho, g.Wo,
-                k, g.stride, g.pad, s);
+    maxpool_bwd(P<const uint8_t>(argmax), P<const bf16>(dy), P<bf16>(dx), g.N, g.H, g.W, g.C, g.Ho,
+                g.Wo, k, g.stride, g.pad, s);
   };
 }
 

@@ -246,30 +246,49 @@ void bn_relu_bwd_reduce(const bf16* dy, const bf16* x, const float* mean, const 
   DTR_CHECK_LAUNCH();
 }
 
-// dgamma/dbeta (accumulated into the flat gradient) + apply coefficients.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ rstd, float* dgamma,
-                                       float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// dgamma/dbeta (written into the flat gradient) + apply coefficients.
+// Block = 64 channels x 16 tile-rows: each thread folds every 16th tile
+// (coalesced over channels, independent loads in flight), then a fixed-order
+// LDS combine -- deterministic, and ~100x faster than one serial thread per
+// channel over 500-1600 partial tiles.
+__global__ void __launch_bounds__(1024)
+bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
+                       const float* __restrict__ gamma, const float* __restrict__ rstd,
+                       float* dgamma, float* dbeta, float* coef) {
+  __shared__ float s0[16][64], s1[16][64];
+  const int cx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
   float sg = 0.f, sgx = 0.f;
-  for (int t = 0; t < tiles; ++t) {
-    sg += part[(long)t * 2 * C + c];
-    sgx += part[(long)t * 2 * C + C + c];
+  if (c < C) {
+#pragma unroll 4
+    for (int t = ty; t < tiles; t += 16) {
+      sg += part[(long)t * 2 * C + c];
+      sgx += part[(long)t * 2 * C + C + c];
+    }
   }
-  dbeta[c] = sg;
-  dgamma[c] = sgx;
-  const float a = gamma[c] * rstd[c];
-  coef[c] = a;
-  coef[C + c] = a * sg / (float)M;
-  coef[2 * C + c] = a * sgx / (float)M;
+  s0[ty][cx] = sg;
+  s1[ty][cx] = sgx;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a0 += s0[k][cx];
+      a1 += s1[k][cx];
+    }
+    dbeta[c] = a0;
+    dgamma[c] = a1;
+    const float a = gamma[c] * rstd[c];
+    coef[c] = a;
+    coef[C + c] = a * a0 / (float)M;
+    coef[2 * C + c] = a * a1 / (float)M;
+  }
 }
 
 void bn_bwd_finalize(const float* part, int tiles, int M, int C, const float* gamma,
                      const float* rstd, float* dgamma, float* dbeta, float* coef,
                      hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, s, part, tiles,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, tiles,
                      M, C, gamma, rstd, dgamma, dbeta, coef);
   DTR_CHECK_LAUNCH();
 }

@@ -18,17 +18,40 @@
 // 16-lane groups of ds_read_b128 hit 16 distinct bank slots.  Fused extras:
 //   * PRE : apply the previous layer's BatchNorm+ReLU (per-input-channel affine)
 //           while staging A, so BN-ReLU outputs are never materialised in HBM;
-//   * epilogue bias / residual add / accumulate-into-output / fp32 output;
+//   * epilogue: the fp32 accumulator tile is staged through LDS and written
+//           back as 16-byte row vectors (8 channels per lane) with bias /
+//           residual add / accumulate-into-output fused and ONE bf16 rounding;
 //   * STATS: per-workgroup per-channel (mean, M2) Welford partials of the bf16
-//           output, finalised by bn_finalize (Chan's parallel combine).
+//           output, finalised by bn_finalize (Chan's parallel combine);
+//   * BNB (dgrad): the BatchNorm+ReLU backward reduction of the produced
+//           gradient g = d_a * [x*scale+shift > 0]:  per-tile sum(g) and
+//           sum(g * xhat), so no separate pass re-reads d_a and x.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace dtr {
 
-template <int BM, int BN, int WM, int WN, int MODE, bool PRE, bool STATS>
+enum { F_PRE = 1, F_STATS = 2, F_BNB = 4 };
+
+// Epilogue staging: one wave-row (WTM rows x BN) of the fp32 tile at a time.
+template <int WTM, int BN>
+struct EpiLayout {
+  static constexpr int LDC = BN + 4;              // fp32 staging row stride (floats)
+  static constexpr int CPR = BN / 8;              // 8-channel chunks per row
+  static constexpr int RPP = 256 / CPR;           // rows per pass
+  static constexpr int TILE = WTM * LDC;          // floats
+  static constexpr int RED = 2 * RPP * BN + BN;   // floats (two reduction planes + means)
+  static constexpr size_t BYTES = (size_t)(TILE + RED) * sizeof(float);
+};
+
+template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 __global__ void __launch_bounds__(256)
 conv_gemm_kernel(GemmArgs args) {
+  constexpr bool PRE = (FLAGS & F_PRE) != 0;
+  constexpr bool STATS = (FLAGS & F_STATS) != 0;
+  constexpr bool BNB = (FLAGS & F_BNB) != 0;
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MR = WTM / 16, NR = WTN / 16;
@@ -206,94 +229,181 @@ conv_gemm_kernel(GemmArgs args) {
   }
 
   // ---------------- epilogue ----------------
-  // Lane owns column n0 + wn*WTN + b*16 + fr, rows m0 + wm*WTM + a*16 + fq*4 + i.
+  // Processed in WM phases, one wave-row (WTM rows) at a time:
+  //  (a) that row of waves writes its fragments (+bias) to an fp32 LDS tile
+  //      (the K loop ended with a barrier: staging buffers/PRE table are dead);
+  //  (b) all 256 threads sweep it as 16-byte row vectors (8 channels per lane):
+  //      residual / accumulate, ONE bf16 rounding, 16-B store, BN partials;
+  //  (c) STATS: per-phase two-pass (mean, M2) folded across phases with Chan's
+  //      formula in fixed order; BNB: sums carried in registers.
+  using EL = EpiLayout<WTM, BN>;
+  float* cs = reinterpret_cast<float*>(smem);
+  float* red = cs + EL::TILE;
+  float* red2 = red + EL::RPP * BN;
+  float* mean_s = red + 2 * EL::RPP * BN;
+  const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
+  const int col0 = n0 + cc * 8;
+  const bool colok = col0 < NC;  // NC % 16 == 0 -> a chunk is all-in or all-out
+  float s1[8], s2[8];
 #pragma unroll
-  for (int b = 0; b < NR; ++b) {
-    const int col = n0 + wn * WTN + b * 16 + fr;
-    const float bias = (args.bias != nullptr && col < args.nbias) ? args.bias[col] : 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  float bsc[8], bsh[8], bmu[8], brs[8];
+  if constexpr (BNB) {
 #pragma unroll
-    for (int a = 0; a < MR; ++a) {
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = colok ? args.bnb_scale[col0 + j] : 0.f;
+      bsh[j] = colok ? args.bnb_shift[col0 + j] : 0.f;
+      bmu[j] = colok ? args.bnb_mean[col0 + j] : 0.f;
+      brs[j] = colok ? args.bnb_rstd[col0 + j] : 0.f;
+    }
+  }
+  float wn_run = 0.f, wmean_run = 0.f, wm2_run = 0.f;  // STATS, thread tid < BN owns column tid
+
+#pragma unroll 1
+  for (int ph = 0; ph < WM; ++ph) {
+    const int prow0 = m0 + ph * WTM;
+    const int nph = min(WTM, M - prow0);   // block-uniform
+    if (nph <= 0) break;
+    if (wm == ph) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wm * WTM + a * 16 + fq * 4 + i;
-        float v = acc[a][b][i] + bias;
-        if (row < M && col < NC) {
-          const long o = (long)row * NC + col;
-          if (args.residual) v += (float)args.residual[o];
-          if (args.out_f32) {
-            if (args.accumulate) v += args.out_f32[o];
-            args.out_f32[o] = v;
-          } else {
-            if (args.accumulate) v += (float)args.out[o];
-            const bf16 vb = (bf16)v;
-            args.out[o] = vb;
-            v = (float)vb;
-          }
-        } else {
-          v = 0.f;
-        }
-        acc[a][b][i] = v;
+      for (int b = 0; b < NR; ++b) {
+        const int cl = wn * WTN + b * 16 + fr;
+        const int col = n0 + cl;
+        const float bias = (args.bias != nullptr && col < args.nbias) ? args.bias[col] : 0.f;
+#pragma unroll
+        for (int a = 0; a < MR; ++a)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            cs[(a * 16 + fq * 4 + i) * EL::LDC + cl] = acc[a][b][i] + bias;
       }
     }
+    __syncthreads();
+    float p1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p1[j] = 0.f;
+    for (int r = r0; r < nph; r += EL::RPP) {
+      if (!colok) break;
+      const int row = prow0 + r;
+      float* cp = cs + r * EL::LDC + cc * 8;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cp);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cp + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const long o = (long)row * NC + col0;
+      if (args.residual) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(args.residual + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+      }
+      if (args.out_f32) {
+        float* op = args.out_f32 + o;
+        if (args.accumulate) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(op);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(op + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] += a0[j];
+            v[4 + j] += a1[j];
+          }
+        }
+        *reinterpret_cast<f32x4*>(op) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(op + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        if (args.accumulate) {
+          const bf16x8 av = *reinterpret_cast<const bf16x8*>(args.out + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
+        }
+        bf16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ob[j] = (bf16)v[j];
+          v[j] = (float)ob[j];
+        }
+        *reinterpret_cast<bf16x8*>(args.out + o) = ob;
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p1[j] += v[j];
+        *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+      if constexpr (BNB) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = (float)xv[j];
+          const float gg = (xf * bsc[j] + bsh[j] > 0.f) ? v[j] : 0.f;
+          s1[j] += gg;
+          s2[j] += gg * (xf - bmu[j]) * brs[j];
+        }
+      }
+    }
+    if constexpr (STATS) {
+      // phase mean
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[r0 * BN + cc * 8 + j] = p1[j];
+      __syncthreads();
+      if (tid < BN) {
+        float t = 0.f;
+        for (int k = 0; k < EL::RPP; ++k) t += red[k * BN + tid];
+        mean_s[tid] = t / (float)nph;
+      }
+      __syncthreads();
+      float mu[8], q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mu[j] = mean_s[cc * 8 + j];
+        q[j] = 0.f;
+      }
+      for (int r = r0; r < nph; r += EL::RPP) {
+        if (!colok) break;
+        const float* cp = cs + r * EL::LDC + cc * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = cp[j] - mu[j];
+          q[j] += d * d;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red2[r0 * BN + cc * 8 + j] = q[j];
+      __syncthreads();
+      if (tid < BN) {
+        float m2 = 0.f;
+        for (int k = 0; k < EL::RPP; ++k) m2 += red2[k * BN + tid];
+        const float nb = (float)nph, mb = mean_s[tid];
+        const float n = wn_run + nb;
+        const float d = mb - wmean_run;
+        wmean_run += d * nb / n;
+        wm2_run += m2 + d * d * wn_run * nb / n;
+        wn_run = n;
+      }
+    }
+    __syncthreads();  // the next phase overwrites the staging tile
   }
 
   if constexpr (STATS) {
-    // Per-channel Welford partial over this workgroup's valid rows:
-    // pass 1 sums -> tile mean; pass 2 squared deviations from the register copy.
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN]; LDS tiles are dead now
-    const int nvalid = min(BM, M - m0);
-    float mean_c[NR];
+    if (tid < BN && n0 + tid < NC) {
+      float* tile_out = args.stat_part + (long)blockIdx.x * 2 * NC;
+      tile_out[n0 + tid] = wmean_run;       // tile mean
+      tile_out[NC + n0 + tid] = wm2_run;    // tile M2
+    }
+  }
+  if constexpr (BNB) {
 #pragma unroll
-    for (int b = 0; b < NR; ++b) {
-      float s = 0.f;
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s += acc[a][b][i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (fq == 0) red[wm * BN + wn * WTN + b * 16 + fr] = s;
+    for (int j = 0; j < 8; ++j) {
+      red[r0 * BN + cc * 8 + j] = s1[j];
+      red2[r0 * BN + cc * 8 + j] = s2[j];
     }
     __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NR; ++b) {
-      const int c = wn * WTN + b * 16 + fr;
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
-      mean_c[b] = s / (float)nvalid;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NR; ++b) {
-      float s = 0.f;
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m0 + wm * WTM + a * 16 + fq * 4 + i;
-          const float d = acc[a][b][i] - mean_c[b];
-          s += (row < M) ? d * d : 0.f;
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (fq == 0) red[wm * BN + wn * WTN + b * 16 + fr] = s;
-    }
-    __syncthreads();
-    if (wm == 0 && fq == 0) {
-#pragma unroll
-      for (int b = 0; b < NR; ++b) {
-        const int c = wn * WTN + b * 16 + fr;
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) s += red[w * BN + c];
-        const int col = n0 + c;
-        if (col < NC) {
-          float* p = args.stat_part + (long)blockIdx.x * 2 * NC;
-          p[col] = mean_c[b];
-          p[NC + col] = s;
-        }
+    if (tid < BN && n0 + tid < NC) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = 0; k < EL::RPP; ++k) {
+        t1 += red[k * BN + tid];
+        t2 += red2[k * BN + tid];
       }
+      float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
+      tile_out[n0 + tid] = t1;        // sum g
+      tile_out[NC + n0 + tid] = t2;   // sum g * xhat
     }
   }
 }
@@ -301,25 +411,31 @@ conv_gemm_kernel(GemmArgs args) {
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int MODE, bool PRE, bool STATS>
+template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_cfg(const GemmArgs& a, hipStream_t s) {
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)2 * (BM + BN) * 64 * sizeof(bf16);
-  if (PRE) lds += (size_t)2 * Acin * sizeof(float);
+  if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);
+  lds = std::max(lds, EpiLayout<BM / WM, BN>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, PRE, STATS>), grid, dim3(256),
-                     lds, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS>), grid, dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
 }
 
 template <int BM, int BN, int WM, int WN, int MODE>
 static void launch_flags(const GemmArgs& a, hipStream_t s) {
   const bool pre = a.pre_scale != nullptr, st = a.stat_part != nullptr;
-  if (pre && st) launch_cfg<BM, BN, WM, WN, MODE, true, true>(a, s);
-  else if (pre) launch_cfg<BM, BN, WM, WN, MODE, true, false>(a, s);
-  else if (st) launch_cfg<BM, BN, WM, WN, MODE, false, true>(a, s);
-  else launch_cfg<BM, BN, WM, WN, MODE, false, false>(a, s);
+  const bool bnb = a.bnb_part != nullptr;
+  if constexpr (MODE == MODE_FWD) {
+    if (pre && st) launch_cfg<BM, BN, WM, WN, MODE, F_PRE | F_STATS>(a, s);
+    else if (pre) launch_cfg<BM, BN, WM, WN, MODE, F_PRE>(a, s);
+    else if (st) launch_cfg<BM, BN, WM, WN, MODE, F_STATS>(a, s);
+    else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
+  } else {
+    if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB>(a, s);
+    else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
+  }
 }
 
 // Tile selection by output width; BM shrinks for small M so the grid still

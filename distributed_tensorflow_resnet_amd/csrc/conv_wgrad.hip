@@ -219,9 +219,9 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   const long NT = (long)g.kh * g.kw * g.C;
   const long tiles = ((g.K + bm - 1) / bm) * ((NT + bn - 1) / bn);
   const long P = (long)g.N * g.Ho * g.Wo;
-  long splits = 1024 / tiles;
+  long splits = 512 / tiles;
   if (splits < 1) splits = 1;
-  long maxs = P / 512;
+  long maxs = P / 1024;
   if (maxs < 1) maxs = 1;
   if (splits > maxs) splits = maxs;
   long pps = (P + splits - 1) / splits;
@@ -244,31 +244,41 @@ void conv_wgrad(const WgradArgs& a, hipStream_t s) {
 
 // Deterministic split-K reduction + layout change [co][tap][ci] -> HWIO [tap][ci][co],
 // dropping padded output channels (co >= Kv) and padded input channels (ci >= Cv).
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ grad,
-                                    int splits, int K, int Kv, int taps, int C, int Cv,
-                                    float scale, int accumulate) {
+// Block = 64 consecutive partial columns x 16 split-rows: coalesced slab reads,
+// 16 independent accumulation chains per column, fixed-order LDS combine.
+__global__ void __launch_bounds__(1024)
+wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ grad, int splits, int K,
+                    int Kv, int taps, int C, int Cv, float scale, int accumulate) {
+  __shared__ float red[16][65];
   const long NT = (long)taps * C;
   const long total = (long)K * NT;
-  const long NTv = (long)taps * Cv;
-  const long outn = (long)Kv * NTv;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < outn;
-       idx += (long)gridDim.x * blockDim.x) {
-    const long co = idx / NTv, nv = idx - co * NTv;
-    const long tap = nv / Cv, ci = nv - tap * Cv;
-    const long src = co * NT + tap * C + ci;
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += part[(long)sp * total + src];
-    const long o = nv * Kv + co;
-    grad[o] = accumulate ? grad[o] + s * scale : s * scale;
+  const int cx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long idx = (long)blockIdx.x * 64 + cx;  // index into one slab [co][tap*C+ci]
+  float s = 0.f;
+  if (idx < total) {
+#pragma unroll 4
+    for (int sp = ty; sp < splits; sp += 16) s += part[(long)sp * total + idx];
+  }
+  red[ty][cx] = s;
+  __syncthreads();
+  if (ty == 0 && idx < total) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += red[k][cx];
+    const long co = idx / NT, n = idx - co * NT;
+    const long tap = n / C, ci = n - tap * C;
+    if (co < Kv && ci < Cv) {
+      const long o = (tap * Cv + ci) * Kv + co;
+      grad[o] = accumulate ? grad[o] + a * scale : a * scale;
+    }
   }
 }
 
 void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_valid, int taps,
                   int C, int C_valid, float scale, int accumulate, hipStream_t s) {
-  const long total = (long)K_valid * taps * C_valid;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, part, grad_hwio,
+  const long total = (long)K * taps * C;
+  const unsigned blocks = (unsigned)((total + 63) / 64);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(1024), 0, s, part, grad_hwio,
                      splits, K, K_valid, taps, C, C_valid, scale, accumulate);
   DTR_CHECK_LAUNCH();
 }

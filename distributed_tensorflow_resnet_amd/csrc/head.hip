@@ -5,8 +5,8 @@
 //     precision (argmax == label, resnet_cifar_main.py:284-286) and the dense
 //     bias gradient (resnet_model.py:77-80)
 //   * 3x3/2 SAME max-pool of the ImageNet stem (resnet_model_official.py:314-316;
-//     TF SAME pads 0 before / 1 after for 112 -> 56), backward by recomputed
-//     first-max argmax (deterministic gather, no atomics).
+//     TF SAME pads 0 before / 1 after for 112 -> 56); the forward records the
+//     first-max window index, the backward gathers through it (deterministic).
 #include "common.h"
 #include "kernels.h"
 
@@ -172,10 +172,15 @@ void softmax_xent(const float* logits, int ld, const int* labels, int N, int cla
 
 // ---------------------------------------------------------------------------
 // max pool (NHWC), window k, stride s, pad_top=pad_left=pad; out-of-range taps
-// are excluded (TF SAME semantics).
+// are excluded (TF SAME semantics).  The forward records, per output element,
+// the window position (r*k+c) of the FIRST maximum in row-major window order;
+// the backward is then a gather: every input element sums dy over the <= 4
+// windows whose recorded argmax is itself (deterministic, no atomics), with
+// 8 channels per thread (16-B bf16 loads, 8-B index loads).
 // ---------------------------------------------------------------------------
-__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H,
-                                   int W, int C, int Ho, int Wo, int k, int st, int pad) {
+__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                   uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
+                                   int Wo, int k, int st, int pad) {
   const int G = C / 8;
   const long total = (long)N * Ho * Wo * G;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -187,8 +192,12 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
     const int ho = (int)(t % Ho);
     const int n = (int)(t / Ho);
     float m[8];
+    int a[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      a[j] = 0;
+    }
     for (int r = 0; r < k; ++r) {
       const int hi = ho * st - pad + r;
       if (hi < 0 || hi >= H) continue;
@@ -198,72 +207,83 @@ __global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict_
         const bf16x8 v =
             *reinterpret_cast<const bf16x8*>(x + (((long)n * H + hi) * W + wi) * C + grp * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)v[j];
+          if (f > m[j]) {
+            m[j] = f;
+            a[j] = r * k + c;
+          }
+        }
       }
     }
-    bf16x8 r;
+    bf16x8 r8;
+    unsigned long long packed = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (bf16)m[j];
-    *reinterpret_cast<bf16x8*>(y + i * 8) = r;
+    for (int j = 0; j < 8; ++j) {
+      r8[j] = (bf16)m[j];
+      packed |= (unsigned long long)(a[j] & 0xFF) << (8 * j);
+    }
+    *reinterpret_cast<bf16x8*>(y + i * 8) = r8;
+    if (idx) *reinterpret_cast<unsigned long long*>(idx + i * 8) = packed;
   }
 }
 
-void maxpool_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
-                 int stride, int pad, hipStream_t s) {
+void maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho,
+                 int Wo, int k, int stride, int pad, hipStream_t s) {
   const long total = (long)N * Ho * Wo * (C / 8);
   long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, N, H, W,
-                     C, Ho, Wo, k, stride, pad);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, idx, N, H,
+                     W, C, Ho, Wo, k, stride, pad);
   DTR_CHECK_LAUNCH();
 }
 
-// dx[h][w] = sum over windows containing (h,w) whose first argmax is (h,w).
-__global__ void maxpool_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+__global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ idx, const bf16* __restrict__ dy,
                                    bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                    int Wo, int k, int st, int pad) {
-  const long total = (long)N * H * W * C;
+  const int G = C / 8;
+  const long total = (long)N * H * W * G;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int ch = (int)(i % C);
-    long t = i / C;
+    const int grp = (int)(i % G);
+    long t = i / G;
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
     const int n = (int)(t / H);
-    float acc = 0.f;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // outputs whose window covers h: ho*st - pad <= h <= ho*st - pad + k - 1
     const int ho_lo = max(0, (h + pad - k + st) / st), ho_hi = min(Ho - 1, (h + pad) / st);
     const int wo_lo = max(0, (w + pad - k + st) / st), wo_hi = min(Wo - 1, (w + pad) / st);
-    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int r = h - (ho * st - pad);
+      if (r < 0 || r >= k) continue;
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        if (h < ho * st - pad || w < wo * st - pad) continue;
-        // first-max in row-major window order
-        float best = -INFINITY;
-        int bh = -1, bw = -1;
-        for (int r = 0; r < k; ++r) {
-          const int hi = ho * st - pad + r;
-          if (hi < 0 || hi >= H) continue;
-          for (int c = 0; c < k; ++c) {
-            const int wi = wo * st - pad + c;
-            if (wi < 0 || wi >= W) continue;
-            const float v = (float)x[(((long)n * H + hi) * W + wi) * C + ch];
-            if (v > best) { best = v; bh = hi; bw = wi; }
-          }
-        }
-        if (bh == h && bw == w) acc += (float)dy[(((long)n * Ho + ho) * Wo + wo) * C + ch];
+        const int c = w - (wo * st - pad);
+        if (c < 0 || c >= k) continue;
+        const long o = (((long)n * Ho + ho) * Wo + wo) * C + grp * 8;
+        const unsigned long long a = *reinterpret_cast<const unsigned long long*>(idx + o);
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(dy + o);
+        const unsigned pos = (unsigned)(r * k + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((a >> (8 * j)) & 0xFF) == pos) acc[j] += (float)d[j];
       }
-    dx[i] = (bf16)acc;
+    }
+    bf16x8 r8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r8[j] = (bf16)acc[j];
+    *reinterpret_cast<bf16x8*>(dx + i * 8) = r8;
   }
 }
 
-void maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho,
+void maxpool_bwd(const uint8_t* idx, const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho,
                  int Wo, int k, int stride, int pad, hipStream_t s) {
-  const long total = (long)N * H * W * C;
+  const long total = (long)N * H * W * (C / 8);
   long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, dy, dx, N, H,
-                     W, C, Ho, Wo, k, stride, pad);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, idx, dy, dx, N,
+                     H, W, C, Ho, Wo, k, stride, pad);
   DTR_CHECK_LAUNCH();
 }
 

@@ -29,6 +29,13 @@ struct GemmArgs {
   const float* bias;        // optional, applied to columns < nbias
   int nbias;
   float* stat_part;         // optional [tiles][2][Ncol] Welford partials (mean, M2)
+  // optional fused BN+ReLU backward reduction (dgrad): x = BN input [M][Ncol]
+  const bf16* bnb_x;
+  const float* bnb_mean;
+  const float* bnb_rstd;
+  const float* bnb_scale;
+  const float* bnb_shift;
+  float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;
@@ -90,10 +97,10 @@ void softmax_xent(const float* logits, int ld, const int* labels, int N, int cla
                   float grad_scale, float* probs, hipStream_t s);
 
 // ---- max pool (ImageNet stem) ----
-void maxpool_fwd(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
-                 int k, int stride, int pad, hipStream_t s);
-void maxpool_bwd(const bf16* x, const bf16* dy, bf16* dx, int N, int H, int W, int C, int Ho,
+void maxpool_fwd(const bf16* x, bf16* y, uint8_t* argmax, int N, int H, int W, int C, int Ho,
                  int Wo, int k, int stride, int pad, hipStream_t s);
+void maxpool_bwd(const uint8_t* argmax, const bf16* dy, bf16* dx, int N, int H, int W, int C,
+                 int Ho, int Wo, int k, int stride, int pad, hipStream_t s);
 
 // ---- flat-parameter descriptors ----
 struct ParamSeg {          // one trainable tensor inside the flat buffers

@@ -192,11 +192,18 @@ def cifar_spec(resnet_size: int = 50, num_classes: int = 10, image_hw: int = 32)
                      final_bn, cin, params)
 
 
-def imagenet_spec(resnet_size: int = 50, num_classes: int = 1000, image_hw: int = 224) -> ModelSpec:
-    """imagenet_resnet_v2_generator (official:281-347) with the size table (:350-366)."""
-    if resnet_size not in IMAGENET_SIZES:
+def imagenet_spec(resnet_size: int = 50, num_classes: int = 1000, image_hw: int = 224,
+                  block: str | None = None, layers: list | None = None) -> ModelSpec:
+    """imagenet_resnet_v2_generator (official:281-347) with the size table (:350-366).
+
+    ``block``/``layers`` override the table (the generator's own arguments,
+    official:281) for custom depths, e.g. shallow test networks."""
+    if block is not None and layers is not None:
+        kind = block
+    elif resnet_size not in IMAGENET_SIZES:
         raise ValueError(f"Not a valid resnet_size: {resnet_size}")
-    kind, layers = IMAGENET_SIZES[resnet_size]
+    else:
+        kind, layers = IMAGENET_SIZES[resnet_size]
     params: list = []
     namer = _Namer()
     stem = _add_conv(params, namer, 7, 3, 64, 2, image_hw, image_hw)

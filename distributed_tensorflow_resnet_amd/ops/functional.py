@@ -102,12 +102,15 @@ def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residu
                        0 if out_f32 else out.data_ptr(), out.data_ptr() if out_f32 else 0,
                        _ptr(residual), _ptr(pre_scale), _ptr(pre_shift), _ptr(bias),
                        0 if bias is None else bias.numel(), _ptr(stat_part), int(accumulate),
-                       g.as_list(), _stream())
+                       g.as_list(), [], _stream())
     return out
 
 
-def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False):
-    """dx = conv2d_transpose(dy, W) with TF fixed padding; w_hwio [kh][kw][C][K]."""
+def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False, bnb=None):
+    """dx = conv2d_transpose(dy, W) with TF fixed padding; w_hwio [kh][kw][C][K].
+
+    ``bnb=(x, mean, rstd, scale, shift, part)`` additionally emits the
+    BN+ReLU backward partials of dx (per tile: sum g, sum g*xhat, g = dx*[relu])."""
     _check(dy, BF16, 4, "dy")
     _check(w_hwio, BF16, 4, "w_hwio")
     N, H, W, C = x_shape
@@ -117,8 +120,9 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
         raise ValueError(f"dgrad shape mismatch dy={tuple(dy.shape)} geom={g}")
     if out is None:
         out = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+    bl = [] if bnb is None else [t.data_ptr() for t in bnb]
     native().conv_gemm(1, dy.data_ptr(), w_hwio.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                       int(accumulate), g.as_list(), _stream())
+                       int(accumulate), g.as_list(), bl, _stream())
     return out
 
 
@@ -236,23 +240,25 @@ def softmax_xent(logits, labels, classes, grad_scale, want_probs=False):
 
 
 def maxpool_fwd(x, k=3, stride=2):
-    """TF max_pooling2d(pool k, stride, padding='SAME') on NHWC."""
+    """TF max_pooling2d(pool k, stride, padding='SAME') on NHWC.
+    Returns (y, argmax) where argmax holds the window position of the first max."""
     _check(x, BF16, 4, "x")
     N, H, W, C = x.shape
     Ho, Wo = -(-H // stride), -(-W // stride)
     pad = max((Ho - 1) * stride + k - H, 0) // 2
     y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=BF16)
-    native().maxpool_fwd(x.data_ptr(), y.data_ptr(), [N, H, W, C, Ho, Wo, C, k, k, stride, pad], k,
-                         _stream())
-    return y
+    am = torch.empty((N, Ho, Wo, C), device=x.device, dtype=torch.uint8)
+    native().maxpool_fwd(x.data_ptr(), y.data_ptr(), am.data_ptr(),
+                         [N, H, W, C, Ho, Wo, C, k, k, stride, pad], k, _stream())
+    return y, am
 
 
-def maxpool_bwd(x, dy, k=3, stride=2):
-    N, H, W, C = x.shape
+def maxpool_bwd(argmax, dy, x_shape, k=3, stride=2):
+    N, H, W, C = x_shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     pad = max((Ho - 1) * stride + k - H, 0) // 2
-    dx = torch.empty_like(x)
-    native().maxpool_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(),
+    dx = torch.empty(x_shape, device=dy.device, dtype=BF16)
+    native().maxpool_bwd(argmax.data_ptr(), dy.data_ptr(), dx.data_ptr(),
                          [N, H, W, C, Ho, Wo, C, k, k, stride, pad], k, _stream())
     return dx
 

@@ -267,6 +267,7 @@ class Engine:
         if spec.maxpool:
             mh = _ceil(st.ho, 2)
             self.pool_out = torch.empty((N, mh, mh, st.cout), dtype=BF16, device=dev)
+            self.pool_arg = torch.empty((N, mh, mh, st.cout), dtype=torch.uint8, device=dev)
         self.X = []     # block inputs (X[i] = input of block i, X[-1] = last output)
         self.H1, self.H2 = [], []
         x0 = self.pool_out if spec.maxpool else self.stem_out
@@ -302,7 +303,8 @@ class Engine:
             M = N * b.spec.h * b.spec.w
             bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
             max_stat = max(max_stat, _ceil(M, bm) * 2 * C)
-            max_bwd = max(max_bwd, self.nat.bn_bwd_tiles(M, C) * 2 * C)
+            tl = max(self.nat.bn_bwd_tiles(M, C), _ceil(M, self.nat.conv_gemm_bm(M, C)))
+            max_bwd = max(max_bwd, tl * 2 * C)
         self.stat_part = torch.empty(max_stat, device=dev)
         self.bwd_part = torch.empty(max_bwd, device=dev)
         max_c = max(b.spec.channels for b in self.bns.values())
@@ -337,7 +339,7 @@ class Engine:
         plan.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                        0 if residual is None else residual.data_ptr(),
                        0 if pre is None else pre.scale.data_ptr(),
-                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom)
+                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [])
 
     def _bn_finalize(self, plan, bn: _BN, train=True):
         tiles, rows, M = bn.src
@@ -351,8 +353,12 @@ class Engine:
         for n in names:
             self.ready_index[n] = idx
 
-    def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False):
-        """wgrad (+reduce into the flat gradient) and optionally dgrad into dx."""
+    def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False,
+                  bnb: tuple | None = None):
+        """wgrad (+reduce into the flat gradient) and optionally dgrad into dx.
+
+        ``bnb=(bn, bn_input)``: the dgrad epilogue also emits that BN's backward
+        partials (sum g, sum g*xhat of dx) into bwd_part."""
         geom = self._geom(c, N)
         sp, pps = self.nat.wgrad_pick_splits(geom)
         plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
@@ -364,16 +370,28 @@ class Engine:
                           c.cin_valid, 1.0, 0)
         self._mark(plan, c.name)
         if dx is not None:
+            bl = []
+            if bnb is not None:
+                bn, bx = bnb
+                bl = [bx.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
+                      bn.shift.data_ptr(), self.bwd_part.data_ptr()]
+                Mx = N * s.h * s.w
+                self._bnb_tiles = _ceil(Mx, self.nat.conv_gemm_bm(Mx, c.cin))
             plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                           int(accumulate), geom)
+                           int(accumulate), geom, bl)
 
-    def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None):
+    def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None, reduced: bool = False):
+        """BN+ReLU backward.  ``reduced``: the producing dgrad already wrote the
+        partial sums (conv epilogue BNB), so only finalize + apply remain."""
         C = bn.spec.channels
         M = x.numel() // C
-        tiles = self.nat.bn_bwd_tiles(M, C)
-        plan.bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
-                           bn.scale.data_ptr(), bn.shift.data_ptr(), M, C,
-                           self.bwd_part.data_ptr())
+        if reduced:
+            tiles = self._bnb_tiles
+        else:
+            tiles = self.nat.bn_bwd_tiles(M, C)
+            plan.bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(),
+                               bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(), M, C,
+                               self.bwd_part.data_ptr())
         plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
                              bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
         self._mark(plan, *bn.names)
@@ -405,6 +423,7 @@ class Engine:
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
             plan.maxpool_fwd(self.stem_out.data_ptr(), self.pool_out.data_ptr(),
+                             self.pool_arg.data_ptr(),
                              [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
             M = N * ph * ph
             plan.bn_stats(self.pool_out.data_ptr(), M, st.cout, self.stat_part.data_ptr())
@@ -444,7 +463,7 @@ class Engine:
         plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                             self.pooled.data_ptr(), N, HL * WL, F)
         plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
-                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N))
+                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [])
         sp = self.scalars.data_ptr()
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
@@ -464,7 +483,7 @@ class Engine:
                           spec.num_classes, 1, F, F, 1.0, 0)
         self._mark(plan, self.dense_name)
         plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
-                       0, 0, 0, 0, 0, 0, dg)
+                       0, 0, 0, 0, 0, 0, dg, [])
         dact = self._g(0, (N, HL, WL, F))
         plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
         d = 1
@@ -479,28 +498,30 @@ class Engine:
             if b.kind == "building":
                 h1 = self.H1[i]
                 da = self._g(o1, tuple(h1.shape))
-                self._conv_bwd(plan, convs[1], dout, h1, N, bns[1], dx=da)
+                self._conv_bwd(plan, convs[1], dout, h1, N, bns[1], dx=da, bnb=(bns[1], h1))
                 dh = self._g(o2, tuple(h1.shape))
-                self._bn_bwd(plan, bns[1], da, h1, dh)
+                self._bn_bwd(plan, bns[1], da, h1, dh, reduced=True)
                 dcur = dh
             else:
                 h1, h2 = self.H1[i], self.H2[i]
                 da = self._g(o1, tuple(h2.shape))
-                self._conv_bwd(plan, convs[2], dout, h2, N, bns[2], dx=da)
+                self._conv_bwd(plan, convs[2], dout, h2, N, bns[2], dx=da, bnb=(bns[2], h2))
                 dh2 = self._g(o2, tuple(h2.shape))
-                self._bn_bwd(plan, bns[2], da, h2, dh2)
+                self._bn_bwd(plan, bns[2], da, h2, dh2, reduced=True)
                 da = self._g(o1, tuple(h1.shape))
-                self._conv_bwd(plan, convs[1], dh2, h1, N, bns[1], dx=da)
+                self._conv_bwd(plan, convs[1], dh2, h1, N, bns[1], dx=da, bnb=(bns[1], h1))
                 dh1 = self._g(o2, tuple(h1.shape))
-                self._bn_bwd(plan, bns[1], da, h1, dh1)
+                self._bn_bwd(plan, bns[1], da, h1, dh1, reduced=True)
                 dcur = dh1
             da1 = self._g(o1, tuple(X.shape))
-            self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=da1)
-            if b.proj is not None:
+            proj = b.proj is not None
+            self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=da1,
+                           bnb=None if proj else (bns[0], X))
+            if proj:
                 self._conv_bwd(plan, self.convs[b.proj.name], dout, X, N, bns[0], dx=da1,
-                               accumulate=True)
+                               accumulate=True, bnb=(bns[0], X))
             dx = self._g(o2, tuple(X.shape))
-            self._bn_bwd(plan, bns[0], da1, X, dx, add=None if b.proj is not None else dout)
+            self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
         # stem (no dgrad: the input needs no gradient)
         if spec.maxpool:
@@ -508,7 +529,7 @@ class Engine:
             st = spec.stem
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
-            plan.maxpool_bwd(self.stem_out.data_ptr(), dout.data_ptr(), dstem.data_ptr(),
+            plan.maxpool_bwd(self.pool_arg.data_ptr(), dout.data_ptr(), dstem.data_ptr(),
                              [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
             self._conv_bwd(plan, stem, dstem, self.x_in, N, None)
         else:
@@ -684,12 +705,12 @@ class _EvalPlan:
                       bn.scale.data_ptr(), bn.shift.data_ptr())
         y = buf((N, st.ho, st.wo, st.cout))
         p.conv_gemm(0, self.x_in.data_ptr(), stem.ohwi, y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
-                    eng._geom(stem, N))
+                    eng._geom(stem, N), [])
         if spec.maxpool:
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
             z = buf((N, ph, ph, st.cout))
-            p.maxpool_fwd(y.data_ptr(), z.data_ptr(),
+            p.maxpool_fwd(y.data_ptr(), z.data_ptr(), 0,
                           [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
             y = z
         x = y
@@ -714,7 +735,7 @@ class _EvalPlan:
         p.bnrelu_avgpool(x.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                          self.pooled.data_ptr(), N, x.shape[1] * x.shape[2], F)
         p.conv_gemm(0, self.pooled.data_ptr(), eng.dense_ohwi, 0, self.logits.data_ptr(), 0, 0, 0,
-                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N))
+                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [])
         sp = self.scalars.data_ptr()
         p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
                        spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
@@ -723,7 +744,7 @@ class _EvalPlan:
     def _conv(self, p, c, x, out, pre, residual=None):
         p.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                     0 if residual is None else residual.data_ptr(), pre.scale.data_ptr(),
-                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N))
+                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [])
 
     def run(self, images=None, labels=None, raw_u8: bool = True):
         """Returns (loss_sum, correct, probs[N, classes]) for one eval batch.

@@ -211,14 +211,14 @@ def test_head_pool_xent(gpu):
 def test_maxpool(gpu):
     torch.manual_seed(8)
     x = torch.randn(2, 112, 112, 64, device=gpu).to(BF)
-    y = fn.maxpool_fwd(x)
+    y, am = fn.maxpool_fwd(x)
     xf = x.float().requires_grad_(True)
     r = ref.max_pool_same(xf)
     assert y.shape == r.shape == (2, 56, 56, 64)
     torch.testing.assert_close(y.float(), r.detach())
     dy = torch.randn_like(r).to(BF)
     r.backward(dy.float())
-    dx = fn.maxpool_bwd(x, dy)
+    dx = fn.maxpool_bwd(am, dy, tuple(x.shape))
     assert _rel(dx, xf.grad) < 1e-2
 
 
@@ -241,3 +241,32 @@ def test_cifar_augment(gpu):
     ev = fn.cifar_augment(img, cpad=8, train=False)
     r0 = ref.per_image_standardization(img[0].permute(1, 2, 0))
     assert _rel(ev[0, :, :, :3], r0) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K,k,s", [(4, 16, 32, 64, 3, 1), (2, 28, 128, 512, 1, 1),
+                                         (4, 32, 16, 32, 3, 2)])
+def test_dgrad_fused_bn_backward_partials(gpu, N, H, C, K, k, s):
+    """dgrad epilogue BNB: per-tile (sum g, sum g*xhat) == standalone reduction."""
+    torch.manual_seed(10)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)           # BN input (pre-activation)
+    w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    g = fn.ConvGeom(N, H, H, C, K, k, k, s)
+    dy = torch.randn(N, g.Ho, g.Wo, K, device=gpu).to(BF)
+    mean = torch.randn(C, device=gpu) * 0.1
+    rstd = torch.rand(C, device=gpu) + 0.5
+    scale = torch.rand(C, device=gpu) + 0.5
+    shift = torch.randn(C, device=gpu) * 0.2
+    M = N * H * H
+    tiles = -(-M // fn.native().conv_gemm_bm(M, C))
+    part = torch.zeros(tiles * 2 * C, device=gpu)
+    dx = fn.conv2d_dgrad(dy, w.contiguous(), tuple(x.shape), s,
+                         bnb=(x, mean, rstd, scale, shift, part))
+    dx_ref = fn.conv2d_dgrad(dy, w.contiguous(), tuple(x.shape), s)
+    torch.testing.assert_close(dx.float(), dx_ref.float(), rtol=0, atol=0)
+    xf = x.float().reshape(-1, C)
+    gg = dx.float().reshape(-1, C) * ((xf * scale + shift) > 0).float()
+    sg = gg.sum(0)
+    sgx = (gg * (xf - mean) * rstd).sum(0)
+    p = part.view(tiles, 2, C).sum(0)
+    torch.testing.assert_close(p[0], sg, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(p[1], sgx, rtol=1e-4, atol=1e-3)
