@@ -35,14 +35,17 @@ namespace dtr {
 
 enum { F_PRE = 1, F_STATS = 2, F_BNB = 4 };
 
-// Epilogue staging: one wave-row (WTM rows x BN) of the fp32 tile at a time.
-template <int WTM, int BN>
+// Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
+// it fits in 64 KiB (one phase), else one wave-row per phase (128x128 tiles).
+template <int BM, int BN, int WM>
 struct EpiLayout {
   static constexpr int LDC = BN + 4;              // fp32 staging row stride (floats)
   static constexpr int CPR = BN / 8;              // 8-channel chunks per row
   static constexpr int RPP = 256 / CPR;           // rows per pass
-  static constexpr int TILE = WTM * LDC;          // floats
   static constexpr int RED = 2 * RPP * BN + BN;   // floats (two reduction planes + means)
+  static constexpr int PHASES = ((BM * LDC + RED) * 4 <= 64 * 1024) ? 1 : WM;
+  static constexpr int PR = BM / PHASES;          // rows staged per phase
+  static constexpr int TILE = PR * LDC;           // floats
   static constexpr size_t BYTES = (size_t)(TILE + RED) * sizeof(float);
 };
 
@@ -229,14 +232,14 @@ conv_gemm_kernel(GemmArgs args) {
   }
 
   // ---------------- epilogue ----------------
-  // Processed in WM phases, one wave-row (WTM rows) at a time:
-  //  (a) that row of waves writes its fragments (+bias) to an fp32 LDS tile
+  // Processed in EL::PHASES phases of EL::PR rows (1 phase unless the tile is 128x128):
+  //  (a) the waves owning those rows write their fragments (+bias) to an fp32 LDS tile
   //      (the K loop ended with a barrier: staging buffers/PRE table are dead);
   //  (b) all 256 threads sweep it as 16-byte row vectors (8 channels per lane):
   //      residual / accumulate, ONE bf16 rounding, 16-B store, BN partials;
   //  (c) STATS: per-phase two-pass (mean, M2) folded across phases with Chan's
   //      formula in fixed order; BNB: sums carried in registers.
-  using EL = EpiLayout<WTM, BN>;
+  using EL = EpiLayout<BM, BN, WM>;
   float* cs = reinterpret_cast<float*>(smem);
   float* red = cs + EL::TILE;
   float* red2 = red + EL::RPP * BN;
@@ -260,11 +263,12 @@ conv_gemm_kernel(GemmArgs args) {
   float wn_run = 0.f, wmean_run = 0.f, wm2_run = 0.f;  // STATS, thread tid < BN owns column tid
 
 #pragma unroll 1
-  for (int ph = 0; ph < WM; ++ph) {
-    const int prow0 = m0 + ph * WTM;
-    const int nph = min(WTM, M - prow0);   // block-uniform
+  for (int ph = 0; ph < EL::PHASES; ++ph) {
+    const int prow0 = m0 + ph * EL::PR;
+    const int nph = min(EL::PR, M - prow0);   // block-uniform
     if (nph <= 0) break;
-    if (wm == ph) {
+    if ((wm * WTM) / EL::PR == ph) {
+      const int rbase = wm * WTM - ph * EL::PR;
 #pragma unroll
       for (int b = 0; b < NR; ++b) {
         const int cl = wn * WTN + b * 16 + fr;
@@ -274,7 +278,7 @@ conv_gemm_kernel(GemmArgs args) {
         for (int a = 0; a < MR; ++a)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            cs[(a * 16 + fq * 4 + i) * EL::LDC + cl] = acc[a][b][i] + bias;
+            cs[(rbase + a * 16 + fq * 4 + i) * EL::LDC + cl] = acc[a][b][i] + bias;
       }
     }
     __syncthreads();
@@ -416,7 +420,7 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)2 * (BM + BN) * 64 * sizeof(bf16);
   if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);
-  lds = std::max(lds, EpiLayout<BM / WM, BN>::BYTES);
+  lds = std::max(lds, EpiLayout<BM, BN, WM>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS>), grid, dim3(256), lds, s, a);

@@ -566,6 +566,10 @@ class Engine:
     def _step_eager(self):
         st = torch.cuda.current_stream().cuda_stream
         self._run("fwd", st)
+        self._run_bwd(st)
+        self._run("opt", st)
+
+    def _run_bwd(self, st):
         a, b = self.seg["bwd"]
         works = []
         if self.bucket_sched:
@@ -581,7 +585,22 @@ class Engine:
                 w.wait()
         else:
             self.plan.run(a, b, st)
+
+    def step_timed(self) -> dict:
+        """One eager step with HIP-event timing per phase (ProfilerHook)."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        st = torch.cuda.current_stream().cuda_stream
+        ev[0].record()
+        self._run("fwd", st)
+        ev[1].record()
+        self._run_bwd(st)
+        ev[2].record()
         self._run("opt", st)
+        ev[3].record()
+        torch.cuda.synchronize()
+        return {"forward": ev[0].elapsed_time(ev[1]),
+                "backward+allreduce": ev[1].elapsed_time(ev[2]),
+                "optimizer": ev[2].elapsed_time(ev[3])}
 
     def capture(self, warmup: int = 2):
         """Run `warmup` real steps on a side stream, then capture one step."""

@@ -1,0 +1,224 @@
+"""Session hooks with the reference's cadence and keys (SURVEY §5 metrics row).
+
+resnet_cifar_main.py:288-324 / resnet_imagenet_main.py:292-329 install:
+  SummarySaverHook(save_steps=100, output_dir=log_dir)   cross_entropy, cost,
+                                                         learning_rate, Precision
+  LoggingTensorHook(every_n_iter=20 | 40)                step, loss, precision, lr
+  StopAtStepHook(last_step=train_steps)
+  _LearningRateSetterHook                                piecewise schedule
+and MonitoredTrainingSession adds StepCounterHook (global_step/sec every 100
+steps, the README's "stp/sec") and CheckpointSaverHook (every 60 s on the
+Horovod path, every 1000 steps on the PS path).
+
+Hooks only read device metrics when they are due (a read synchronises).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import time
+
+
+class Hook:
+    def begin(self, session):
+        pass
+
+    def before_run(self, session):
+        pass
+
+    def after_run(self, session, step: int):
+        """`step` = global_step after this run."""
+
+    def end(self, session):
+        pass
+
+
+def log(msg: str):
+    print(msg, flush=True)
+
+
+class LearningRateSetterHook(Hook):
+    """The LR itself is evaluated on the device from global_step (engine
+    LRSchedule); this hook mirrors it on the host for logs/summaries."""
+
+    def __init__(self, schedule):
+        self.schedule = schedule
+        self.lr = schedule.init
+
+    def before_run(self, session):
+        self.lr = self.schedule.at(session.global_step)
+
+
+class LoggingTensorHook(Hook):
+    def __init__(self, every_n_iter: int = 20, precision_key: str = "precision"):
+        self.n = every_n_iter
+        self.key = precision_key
+
+    def after_run(self, session, step):
+        if self.n > 0 and step % self.n == 0 and session.is_chief:
+            m = session.metrics()
+            log(f"INFO:tensorflow:step = {m['global_step']}, loss = {m['cost']:.6f}, "
+                f"{self.key} = {m['precision']:.4f}, lr = {m['lr']:.6g}")
+
+
+class StepCounterHook(Hook):
+    """global_step/sec + examples/sec every `every_n_steps` (tf StepCounterHook)."""
+
+    def __init__(self, every_n_steps: int = 100, batch_size: int = 1, writer=None):
+        self.n = every_n_steps
+        self.batch = batch_size
+        self.writer = writer
+        self.t0 = None
+        self.s0 = None
+        self.last_rate = None
+
+    def begin(self, session):
+        self.t0, self.s0 = time.perf_counter(), session.global_step
+
+    def after_run(self, session, step):
+        if self.n > 0 and step - self.s0 >= self.n:
+            session.synchronize()
+            t = time.perf_counter()
+            rate = (step - self.s0) / (t - self.t0)
+            self.last_rate = rate
+            if session.is_chief:
+                log(f"INFO:tensorflow:global_step/sec: {rate:.4f}  "
+                    f"(examples/sec: {rate * self.batch:.1f})")
+                if self.writer is not None:
+                    self.writer.add_scalars(step, {"global_step/sec": rate,
+                                                   "examples/sec": rate * self.batch})
+            self.t0, self.s0 = t, step
+
+
+class SummarySaverHook(Hook):
+    def __init__(self, writer, save_steps: int = 100, precision_tag: str = "Precision"):
+        self.writer = writer
+        self.n = save_steps
+        self.tag = precision_tag
+
+    def after_run(self, session, step):
+        if self.writer is not None and self.n > 0 and step % self.n == 0 and session.is_chief:
+            m = session.metrics()
+            self.writer.add_scalars(step, {"cross_entropy": m["cross_entropy"], "cost": m["cost"],
+                                           "learning_rate": m["lr"], self.tag: m["precision"]})
+            self.writer.flush()
+
+    def end(self, session):
+        if self.writer is not None:
+            self.writer.flush()
+
+
+class JsonlMetricsHook(Hook):
+    """Scalars to <dir>/metrics.jsonl (machine-readable twin of the event file)."""
+
+    def __init__(self, path: str, every: int = 100):
+        self.path = path
+        self.n = every
+
+    def after_run(self, session, step):
+        if self.n > 0 and step % self.n == 0 and session.is_chief:
+            m = dict(session.metrics())
+            m["time"] = time.time()
+            os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+            with open(self.path, "a") as fh:
+                fh.write(json.dumps(m) + "\n")
+
+
+class StopAtStepHook(Hook):
+    def __init__(self, last_step: int):
+        self.last_step = last_step
+
+    def begin(self, session):
+        if session.global_step >= self.last_step:
+            session.request_stop()
+
+    def after_run(self, session, step):
+        if step >= self.last_step:
+            session.request_stop()
+
+
+class CheckpointSaverHook(Hook):
+    """Chief-only, every `save_steps` steps and/or `save_secs` seconds, and at end."""
+
+    def __init__(self, saver, save_steps: int = 0, save_secs: float = 0.0):
+        self.saver = saver
+        self.steps = save_steps
+        self.secs = save_secs
+        self.last_t = time.time()
+        self.last_step = None
+
+    def begin(self, session):
+        self.last_step = session.global_step
+
+    def _save(self, session, step):
+        if session.is_chief:
+            p = self.saver.save(session.state_tensors(), step)
+            log(f"INFO:tensorflow:Saving checkpoints for {step} into {p}.")
+        self.last_t = time.time()
+        self.last_step = step
+
+    def after_run(self, session, step):
+        due = (self.steps > 0 and step % self.steps == 0) or \
+              (self.secs > 0 and time.time() - self.last_t >= self.secs)
+        if due and step != self.last_step:
+            self._save(session, step)
+
+    def end(self, session):
+        if session.global_step != self.last_step:
+            self._save(session, session.global_step)
+
+
+class NanGuardHook(Hook):
+    """tf.check_numerics analogue on the loss (opt-in: reads metrics every step)."""
+
+    def __init__(self, every: int = 1):
+        self.n = every
+
+    def after_run(self, session, step):
+        if step % self.n == 0:
+            c = session.metrics()["cost"]
+            if not math.isfinite(c):
+                raise FloatingPointError(f"loss is {c} at step {step}")
+
+
+class FaultInjectionHook(Hook):
+    """Kills this rank at a given step (tests of checkpoint/resume and of the
+    launcher's failure handling).  Env DTR_FAULT_KILL_STEP / DTR_FAULT_KILL_RANK
+    or flags --fault_kill_step / --fault_kill_rank."""
+
+    def __init__(self, step: int, rank: int):
+        self.step, self.rank = step, rank
+
+    def after_run(self, session, step):
+        if step == self.step and session.rank == self.rank:
+            log(f"[fault-injection] rank {self.rank} exiting at step {step}")
+            sys.stdout.flush()
+            os._exit(17)
+
+
+class ProfilerHook(Hook):
+    """Per-phase device timing (forward / backward+allreduce / optimizer) over a
+    step window, using the backend's phase timer (HIP events); `profile_steps`
+    'a:b' measures steps a..b-1 and prints a table."""
+
+    def __init__(self, spec: str):
+        a, b = spec.split(":")
+        self.a, self.b = int(a), int(b)
+        self.acc = {}
+        self.n = 0
+
+    def before_run(self, session):
+        s = session.global_step
+        session.backend.profile_phases = self.a <= s < self.b
+
+    def after_run(self, session, step):
+        t = getattr(session.backend, "last_phase_ms", None)
+        if t and self.a < step <= self.b:
+            for k, v in t.items():
+                self.acc[k] = self.acc.get(k, 0.0) + v
+            self.n += 1
+        if step == self.b and self.n and session.is_chief:
+            log("phase timing (ms/step): " + ", ".join(
+                f"{k}={v / self.n:.3f}" for k, v in self.acc.items()))

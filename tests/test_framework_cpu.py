@@ -1,0 +1,243 @@
+"""CPU tests of the framework around the kernels: flags, LR schedules, record /
+event / example codecs, CIFAR + ImageNet readers, the training driver (train ->
+checkpoint -> resume -> side-car eval), gloo data parallelism with restart after
+an injected fault, and the tools (tf_saver, freeze, predict)."""
+import glob
+import io
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_tensorflow_resnet_amd.data import cifar as cifar_data  # noqa: E402
+from distributed_tensorflow_resnet_amd.data import vgg  # noqa: E402
+from distributed_tensorflow_resnet_amd.models.spec import cifar_spec  # noqa: E402
+from distributed_tensorflow_resnet_amd.ops import reference as ref  # noqa: E402
+from distributed_tensorflow_resnet_amd.parallel.buckets import assign_buckets, schedule_buckets  # noqa: E402
+from distributed_tensorflow_resnet_amd.models.params import ParamStore  # noqa: E402
+from distributed_tensorflow_resnet_amd.train.engine import cifar_lr_schedule, imagenet_lr_schedule  # noqa: E402
+from distributed_tensorflow_resnet_amd.utils import records  # noqa: E402
+from distributed_tensorflow_resnet_amd.utils import tensor_bundle as tb  # noqa: E402
+from distributed_tensorflow_resnet_amd.utils.flags import build_parser  # noqa: E402
+
+
+def run(args, timeout=600, env=None):
+    e = dict(os.environ)
+    e.update({"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "2"})
+    if env:
+        e.update(env)
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout, env=e)
+    return r
+
+
+# ------------------------------------------------------------------ flags / LR
+def test_flag_defaults_match_reference():
+    c = build_parser("cifar").parse_args([])
+    i = build_parser("imagenet").parse_args([])
+    assert (c.dataset, c.batch_size, c.train_steps, c.eval_batch_count) == ("cifar10", 32, 2000, 50)
+    assert (i.dataset, i.batch_size, i.train_steps, i.num_epochs) == ("imagenet", 128, 200, 90)
+    assert c.variable_update == "parameter_server" and c.data_format == "channels_first"
+    assert build_parser("cifar_eval").parse_args([]).mode == "eval"
+    f = build_parser("cifar").parse_args(["--eval_once", "--nosync_replicas", "--use_horovod=True"])
+    assert f.eval_once and not f.sync_replicas and f.use_horovod
+
+
+def test_lr_schedules_match_hooks():
+    c = cifar_lr_schedule()
+    # step 0 uses begin(); step t uses the value computed after run t-1
+    assert c.at(0) == 0.1 and c.at(40000) == 0.1 and c.at(40001) == 0.01
+    assert c.at(60001) == 0.001 and c.at(80001) == 0.0001
+    i = imagenet_lr_schedule()
+    assert i.at(0) == 0.4                      # begin() quirk (resnet_imagenet_main.py:308)
+    assert abs(i.at(1) - 0.1) < 1e-12          # warm-up restarts at 0.1
+    assert abs(i.at(3121) - (0.1 + 0.3 * 3120 / 6240)) < 1e-12
+    assert i.at(6241) == 0.4 and i.at(37441) == 0.04 and i.at(74881) == 0.004
+    assert i.at(99841) == 0.0004
+
+
+def test_buckets_tile_buffer_in_backward_order():
+    store = ParamStore(cifar_spec(20))
+    b = assign_buckets(store.train_slots, 64 * 1024)
+    assert b[0][1] == store.n_train            # first bucket = end of the buffer
+    assert b[-1][0] == 0
+    ready = {s.name: i for i, s in enumerate(reversed(store.train_slots))}
+    sched = schedule_buckets(b, ready)
+    assert [x[0] for x in sched] == sorted(x[0] for x in sched)
+
+
+# ------------------------------------------------------------------ codecs
+def test_tfrecord_example_event_roundtrip(tmp_path):
+    p = str(tmp_path / "x.tfrecord")
+    w = records.RecordWriter(p)
+    exs = [records.make_example({"image/encoded": b"abc", "image/class/label": 7,
+                                 "f": [1.5, -2.0]}) for _ in range(3)]
+    for e in exs:
+        w.write(e)
+    w.close()
+    got = list(records.read_records(p))
+    assert got == exs
+    d = records.parse_example(got[0])
+    assert d["image/encoded"] == [b"abc"] and d["image/class/label"] == [7]
+    assert d["f"] == [1.5, -2.0]
+    ew = records.EventWriter(str(tmp_path / "ev"))
+    ew.add_scalars(100, {"cost": 1.25, "Precision": 0.5})
+    ew.close()
+    evs = records.read_events(ew.path)
+    assert evs[0]["file_version"] == "brain.Event:2"
+    assert evs[1]["step"] == 100 and evs[1]["scalars"] == {"cost": 1.25, "Precision": 0.5}
+
+
+# ------------------------------------------------------------------ data
+def _fake_cifar(root, n_per_file=20, dataset="cifar10"):
+    rng = np.random.default_rng(0)
+    if dataset == "cifar10":
+        d = os.path.join(root, "cifar-10-batches-bin")
+        os.makedirs(d, exist_ok=True)
+        names = [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]
+        nc = 10
+    else:
+        d = os.path.join(root, "cifar-100-binary")
+        os.makedirs(d, exist_ok=True)
+        names = ["train.bin", "test.bin"]
+        nc = 100
+    for n in names:
+        imgs = rng.integers(0, 256, (n_per_file, 3, 32, 32), dtype=np.uint8)
+        labels = rng.integers(0, nc, n_per_file)
+        cifar_data.write_records(os.path.join(d, n), imgs, labels, dataset)
+    return root
+
+
+@pytest.mark.parametrize("dataset", ["cifar10", "cifar100"])
+def test_cifar_reader(tmp_path, dataset):
+    root = _fake_cifar(str(tmp_path), dataset=dataset)
+    tr = cifar_data.CifarData(root, dataset, train=True)
+    te = cifar_data.CifarData(root, dataset, train=False)
+    assert len(tr) == (100 if dataset == "cifar10" else 20) and len(te) == 20
+    assert tr.num_classes == (10 if dataset == "cifar10" else 100)
+    seen = []
+    for r in range(2):
+        xs = [y for _, y in tr.batches(4, num_epochs=1, rank=r, world=2, seed=3)]
+        seen.append(torch.cat(xs))
+    assert len(seen[0]) == len(seen[1])
+    x, y = next(te.batches(5, shuffle=False, num_epochs=1))
+    assert x.shape == (5, 3, 32, 32) and x.dtype == torch.uint8
+    ev = cifar_data.augment_cpu(x, train=False)
+    r0 = ref.per_image_standardization(x[0].permute(1, 2, 0))
+    torch.testing.assert_close(ev[0], r0, rtol=1e-5, atol=1e-5)
+    tr_aug = cifar_data.augment_cpu(x, train=True, generator=torch.Generator().manual_seed(0))
+    assert tr_aug.shape == (5, 32, 32, 3)
+
+
+def test_vgg_preprocessing_and_imagenet_records(tmp_path):
+    from PIL import Image
+
+    from distributed_tensorflow_resnet_amd.data import imagenet
+
+    rng = np.random.default_rng(0)
+    arr = rng.integers(0, 256, (300, 400, 3), dtype=np.uint8)
+    ev = vgg.preprocess_image(arr, 224, 224, is_training=False)
+    assert ev.shape == (224, 224, 3)
+    tr = vgg.preprocess_image(arr, 224, 224, is_training=True, rng=np.random.default_rng(1))
+    assert tr.shape == (224, 224, 3)
+    assert vgg.smallest_size_at_least(300, 400, 256) == (256, 341)
+    buf = io.BytesIO()
+    Image.fromarray(arr).save(buf, format="JPEG")
+    w = records.RecordWriter(str(tmp_path / "validation-00000-of-00128"))
+    for lab in (1, 1000):
+        w.write(records.make_example({"image/encoded": buf.getvalue(), "image/format": b"JPEG",
+                                      "image/class/label": lab}))
+    w.close()
+    batches = list(imagenet.input_fn(False, str(tmp_path), 2, workers=0))
+    x, y = batches[0]
+    assert x.shape == (2, 224, 224, 3) and y.tolist() == [0, 999]   # 1-based -> 0-based
+
+
+# ------------------------------------------------------------------ driver
+def test_driver_train_resume_eval_cpu(tmp_path):
+    root = _fake_cifar(str(tmp_path / "data"))
+    td, ld, ed = (str(tmp_path / d) for d in ("train", "log", "eval"))
+    common = ["--device", "cpu", "--resnet_size", "8", "--batch_size", "8",
+              "--train_data_path", root, "--eval_data_path", root, "--train_dir", td,
+              "--log_dir", ld, "--log_every", "2", "--summary_every", "2",
+              "--save_checkpoint_steps", "3"]
+    r = run(["resnet_cifar_main.py", "--train_steps", "5"] + common)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "global_step/sec" in r.stdout or "step = " in r.stdout
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-5")
+    ev = glob.glob(os.path.join(ld, "events.out.tfevents.*"))
+    assert ev and any("cost" in e["scalars"] for e in records.read_events(ev[0]))
+    r = run(["resnet_cifar_main.py", "--train_steps", "8"] + common)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Restoring parameters from" in r.stdout
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-8")
+    r = run(["resnet_cifar_eval.py", "--device", "cpu", "--resnet_size", "8", "--train_dir", td,
+             "--eval_dir", ed, "--eval_data_path", root, "--eval_once", "--eval_batch_size", "10",
+             "--eval_batch_count", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "best precision" in r.stdout
+    evs = records.read_events(glob.glob(os.path.join(ed, "events.out.tfevents.*"))[0])
+    assert any("Best_Precision" in e["scalars"] and e["step"] == 8 for e in evs)
+    # tools on the produced checkpoint
+    r = run(["tf_saver.py", "--checkpoint_dir", td, "--restore", "--resnet_size", "8"])
+    assert r.returncode == 0 and "dense/bias" in r.stdout, r.stderr[-2000:]
+    fz = str(tmp_path / "frozen.safetensors")
+    r = run(["resnet_cifar_frozen_model.py", "--train_dir", td, "--output", fz, "--resnet_size",
+             "8", "--eval_data_path", root, "--device", "cpu"])
+    assert r.returncode == 0 and "precision:" in r.stdout, r.stderr[-2000:]
+    assert os.path.exists(fz)
+
+
+def test_resnet_single_config1():
+    """BASELINE config 1 plumbing: ResNet-20 CIFAR-10, CPU, batch 32, synthetic."""
+    r = run(["resnet_single.py", "--synthetic", "--train_steps", "3"], timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "total trainable params: 272,538" in r.stdout
+    assert "training done: global_step=3" in r.stdout
+
+
+def test_gloo_data_parallel_with_fault_restart(tmp_path):
+    """2 CPU ranks (gloo): rank 1 is killed at step 3, the launcher restarts the
+    job, ranks resume from the step-2 checkpoint and finish at step 6 with
+    identical replicas."""
+    td = str(tmp_path / "train")
+    r = run(["-m", "distributed_tensorflow_resnet_amd.parallel.launch", "--nproc", "2",
+             "--master_port", "29631", "--max_restarts", "1", "resnet_cifar_main.py",
+             "--device", "cpu", "--resnet_size", "8", "--batch_size", "4", "--synthetic",
+             "--train_steps", "6", "--train_dir", td, "--save_checkpoint_steps", "2",
+             "--variable_update", "horovod", "--log_every", "1",
+             "--fault_kill_step", "3", "--fault_kill_rank", "1"], timeout=900)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "restarting job" in r.stdout
+    assert "Restoring parameters from" in r.stdout
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-6")
+
+
+def test_resnet_model_api_and_mlp():
+    import logist_model
+    import resnet_model
+
+    hps = resnet_model.HParams(num_classes=10, lrn_rate=0.05, weight_decay_rate=2e-4,
+                               optimizer="mom")
+    torch.manual_seed(0)
+    x = torch.randn(8, 32, 32, 3)
+    y = torch.nn.functional.one_hot(torch.randint(0, 10, (8,)), 10).float()
+    m = resnet_model.ResNet(hps, x, y, "train", resnet_size=8)
+    m.build_graph()
+    c0 = float(m.cost)
+    for _ in range(5):
+        m.train_op()
+        m.build_graph()
+    assert float(m.cost) < c0 and m.global_step == 5
+    assert len(m.network.variables()) == 4 * 7 + 10 + 2  # 7 BN x4, 10 convs (3 proj), dense x2
+    lr = logist_model.LRNet(hps, x, y, "train").build_graph()
+    c0 = float(lr.cost)
+    for _ in range(10):
+        lr.train_op()
+        lr.build_graph()
+    assert float(lr.cost) < c0
