@@ -39,18 +39,20 @@ def main(argv=None):
         print("no checkpoint found", file=sys.stderr)
         return 1
     spec = build_spec(a.dataset, a.resnet_size)
-    model = make_inference(spec, EVAL_NUM, a.device)
-    model.load(tb.read_bundle(prefix))
     if a.eval_data_path:
-        x, y = next(CifarData(a.eval_data_path, a.dataset, train=False).batches(
-            EVAL_NUM, shuffle=False, num_epochs=1))
+        data = CifarData(a.eval_data_path, a.dataset, train=False)
+        n = min(EVAL_NUM, len(data))
+        x, y = next(data.batches(n, shuffle=False, num_epochs=1))
     else:
-        x, y = next(synthetic_batches(EVAL_NUM, spec.num_classes, seed=7))
+        n = EVAL_NUM
+        x, y = next(synthetic_batches(n, spec.num_classes, seed=7))
+    model = make_inference(spec, n, a.device)
+    model.load(tb.read_bundle(prefix))
     _, correct, probs = model.run(x, y)
     pred = probs.argmax(1).cpu()
     print("truth:      ", y.tolist())
     print("predictions:", pred.tolist())
-    print(f"precision: {correct / EVAL_NUM:.3f}")
+    print(f"precision: {correct / n:.3f}")
     if a.save_grid:
         from cifar_input import save_image_grid
 

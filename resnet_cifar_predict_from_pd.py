@@ -23,12 +23,17 @@ def main(argv=None):
     ap.add_argument("--eval_data_path", default="")
     ap.add_argument("--device", default="auto")
     a = ap.parse_args(argv)
-    m = FrozenModel(a.frozen, a.device, EVAL_NUM)
+    from distributed_tensorflow_resnet_amd.utils.frozen import read_frozen
+
+    meta, _ = read_frozen(a.frozen)
     if a.eval_data_path:
-        x, y = next(CifarData(a.eval_data_path, m.spec.dataset, train=False).batches(
-            EVAL_NUM, shuffle=False, num_epochs=1))
+        data = CifarData(a.eval_data_path, meta["dataset"], train=False)
+        n = min(EVAL_NUM, len(data))
+        x, y = next(data.batches(n, shuffle=False, num_epochs=1))
     else:
-        x, y = next(synthetic_batches(EVAL_NUM, m.spec.num_classes, seed=7))
+        n = EVAL_NUM
+        x, y = next(synthetic_batches(n, meta["num_classes"], seed=7))
+    m = FrozenModel(a.frozen, a.device, n)
     probs, precision = m.predict(x, y)
     print("predictions:", probs.argmax(1).tolist())
     print(f"precision: {precision:.3f}")
