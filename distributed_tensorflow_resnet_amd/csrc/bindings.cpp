@@ -113,6 +113,12 @@ static Launch mk_wgrad_reduce(ptr_t part, ptr_t grad, int splits, int K, int K_v
   };
 }
 
+static Launch mk_wgrad_reduce_grouped(ptr_t descs, int nd, long long total_chunks, float scale) {
+  return [=](hipStream_t s) {
+    wgrad_reduce_grouped(P<const WgReduceDesc>(descs), nd, total_chunks, scale, s);
+  };
+}
+
 static Launch mk_bn_finalize(ptr_t part, int tiles, int tile_rows, int M, int C, ptr_t gamma,
                              ptr_t beta, ptr_t mmean, ptr_t mvar, float momentum, float eps,
                              int update_moving, ptr_t mean, ptr_t rstd, ptr_t scale,
@@ -332,6 +338,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "conv_gemm", mk_conv_gemm);
   def_op(m, plan, "conv_wgrad", mk_conv_wgrad);
   def_op(m, plan, "wgrad_reduce", mk_wgrad_reduce);
+  def_op(m, plan, "wgrad_reduce_grouped", mk_wgrad_reduce_grouped);
   def_op(m, plan, "bn_finalize", mk_bn_finalize);
   def_op(m, plan, "bn_eval", mk_bn_eval);
   def_op(m, plan, "bn_stats", mk_bn_stats);
@@ -366,6 +373,7 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(sp, pps);
   });
   m.def("param_seg_bytes", []() { return (int)sizeof(ParamSeg); });
+  m.def("wg_desc_bytes", []() { return (int)sizeof(WgReduceDesc); });
   m.def("device_count", &hip_device_count);
   m.def(
       "crc32c",

@@ -219,11 +219,17 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   const long NT = (long)g.kh * g.kw * g.C;
   const long tiles = ((g.K + bm - 1) / bm) * ((NT + bn - 1) / bn);
   const long P = (long)g.N * g.Ho * g.Wo;
-  long splits = 512 / tiles;
-  if (splits < 1) splits = 1;
-  long maxs = P / 1024;
+  // ~768 workgroups (3 per CU) hide the per-tile load latency; cap the fp32
+  // partial slabs at ~32 MB so the split-K reduce stays cheap, and keep >= 256
+  // pixels (4 K-tiles) per split.  (Measured sweep: scripts/sweep_wgrad.py.)
+  long splits = (768 + tiles / 2) / tiles;
+  const long slab = (long)g.K * NT * 4;
+  const long cap_bytes = (32L << 20) / (slab > 0 ? slab : 1);
+  if (splits > cap_bytes) splits = cap_bytes;
+  long maxs = P / 256;
   if (maxs < 1) maxs = 1;
   if (splits > maxs) splits = maxs;
+  if (splits < 1) splits = 1;
   long pps = (P + splits - 1) / splits;
   pps = (pps + 63) / 64 * 64;
   *px_per_split = (int)pps;
@@ -280,6 +286,49 @@ void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_
   const unsigned blocks = (unsigned)((total + 63) / 64);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(1024), 0, s, part, grad_hwio,
                      splits, K, K_valid, taps, C, C_valid, scale, accumulate);
+  DTR_CHECK_LAUNCH();
+}
+
+// Grouped split-K reduction: ONE launch reduces the partial slabs of many
+// convolutions (all convs of a gradient bucket).  Work unit = 64 consecutive
+// slab columns of one conv; a block finds its conv by binary search over the
+// descriptors' first-chunk offsets.
+__global__ void __launch_bounds__(1024)
+wgrad_reduce_grouped_kernel(const WgReduceDesc* __restrict__ d, int nd, float scale) {
+  __shared__ float red[16][65];
+  const long chunk = blockIdx.x;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].chunk0 <= chunk) lo = mid;
+    else hi = mid - 1;
+  }
+  const WgReduceDesc& q = d[lo];
+  const long NT = (long)q.taps * q.C;
+  const long total = (long)q.K * NT;
+  const int cx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long idx = (chunk - q.chunk0) * 64 + cx;
+  float s = 0.f;
+  if (idx < total) {
+#pragma unroll 4
+    for (int sp = ty; sp < q.splits; sp += 16) s += q.part[(long)sp * total + idx];
+  }
+  red[ty][cx] = s;
+  __syncthreads();
+  if (ty == 0 && idx < total) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += red[k][cx];
+    const long co = idx / NT, n = idx - co * NT;
+    const long tap = n / q.C, ci = n - tap * q.C;
+    if (co < q.Kv && ci < q.Cv) q.grad[(tap * q.Cv + ci) * q.Kv + co] = a * scale;
+  }
+}
+
+void wgrad_reduce_grouped(const WgReduceDesc* descs_dev, int nd, long long total_chunks,
+                          float scale, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_reduce_grouped_kernel, dim3((unsigned)total_chunks), dim3(1024), 0, s,
+                     descs_dev, nd, scale);
   DTR_CHECK_LAUNCH();
 }
 

@@ -61,6 +61,15 @@ void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_
                   int C, int C_valid, float scale, int accumulate, hipStream_t s);
 int wgrad_pick_splits(const ConvGeom& g, int* px_per_split);
 
+struct WgReduceDesc {      // one convolution's split-K slabs -> its HWIO gradient
+  const float* part;       // [splits][K][taps*C]
+  float* grad;             // [taps][Cv][Kv]
+  int splits, K, Kv, taps, C, Cv;
+  long long chunk0;        // first 64-column work chunk of this conv in the group
+};
+void wgrad_reduce_grouped(const WgReduceDesc* descs_dev, int nd, long long total_chunks,
+                          float scale, hipStream_t s);
+
 // ---- BatchNorm (training mode, TF fused semantics) ----
 void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
                  const float* gamma, const float* beta, float* moving_mean,

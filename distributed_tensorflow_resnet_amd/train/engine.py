@@ -44,6 +44,11 @@ BF16 = torch.bfloat16
 BN_DECAY = 0.997
 BN_EPS = 1e-5
 
+WGD_DTYPE = np.dtype([
+    ("part", "<u8"), ("grad", "<u8"), ("splits", "<i4"), ("K", "<i4"), ("Kv", "<i4"),
+    ("taps", "<i4"), ("C", "<i4"), ("Cv", "<i4"), ("chunk0", "<i8"),
+])
+
 SEG_DTYPE = np.dtype([
     ("offset", "<i8"), ("numel", "<i8"), ("bf_ohwi", "<i8"), ("bf_hwio", "<i8"),
     ("kh", "<i4"), ("kw", "<i4"), ("C", "<i4"), ("K", "<i4"), ("cpad", "<i4"), ("kpad", "<i4"),
@@ -160,12 +165,15 @@ class Engine:
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
-        self._build_train_plan()
         if self.dist is not None and self.world > 1:
             self.buckets = assign_buckets(self.params.train_slots, int(bucket_mb * 2 ** 20))
+        else:  # one group: a single grouped split-K reduce at the end of backward
+            self.buckets = [(0, self.params.n_train, [s.name for s in self.params.train_slots])]
+        self._build_train_plan()
+        if self.dist is not None and self.world > 1:
             self.bucket_sched = schedule_buckets(self.buckets, self.ready_index)
         else:
-            self.buckets, self.bucket_sched = [], []
+            self.bucket_sched = []
         self.graph = None
         self._captured = False
         self.eval_plans = {}
@@ -309,14 +317,17 @@ class Engine:
         self.bwd_part = torch.empty(max_bwd, device=dev)
         max_c = max(b.spec.channels for b in self.bns.values())
         self.coef = torch.empty(3 * max_c, device=dev)
-        wg = 1
-        for c in self.convs.values():
-            sp, _ = self.nat.wgrad_pick_splits(self._geom(c, N))
-            wg = max(wg, sp * c.spec.cout * c.spec.kh * c.spec.kw * c.cin)
-        g = self._dense_geom(N)
-        sp, _ = self.nat.wgrad_pick_splits(g)
-        wg = max(wg, sp * self.kpad * F)
-        self.wg_part = torch.empty(wg, device=dev)
+        # per-conv split-K partial slabs (persist until the bucket's grouped reduce)
+        self.wg_off = {}
+        tot = 0
+        for name, c in self.convs.items():
+            sp, pps = self.nat.wgrad_pick_splits(self._geom(c, N))
+            self.wg_off[name] = (tot, sp, pps)
+            tot += sp * c.spec.cout * c.spec.kh * c.spec.kw * c.cin
+        sp, pps = self.nat.wgrad_pick_splits(self._dense_geom(N))
+        self.wg_off["dense"] = (tot, sp, pps)
+        tot += sp * self.kpad * F
+        self.wg_part = torch.empty(max(tot, 1), device=dev)
         self.l2_ws = torch.empty(self.nat.l2_workspace_floats(), device=dev)
 
     # ------------------------------------------------------------------ helpers
@@ -360,15 +371,14 @@ class Engine:
         ``bnb=(bn, bn_input)``: the dgrad epilogue also emits that BN's backward
         partials (sum g, sum g*xhat of dx) into bwd_part."""
         geom = self._geom(c, N)
-        sp, pps = self.nat.wgrad_pick_splits(geom)
+        off, sp, pps = self.wg_off[c.spec.name]
+        part = self.wg_part.data_ptr() + 4 * off
         plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
                         0 if pre is None else pre.scale.data_ptr(),
-                        0 if pre is None else pre.shift.data_ptr(),
-                        self.wg_part.data_ptr(), geom, sp, pps)
+                        0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
         s = c.spec
-        plan.wgrad_reduce(self.wg_part.data_ptr(), c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin,
-                          c.cin_valid, 1.0, 0)
-        self._mark(plan, c.name)
+        self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
+        self._produced.add(c.name)
         if dx is not None:
             bl = []
             if bnb is not None:
@@ -394,10 +404,31 @@ class Engine:
                                self.bwd_part.data_ptr())
         plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
                              bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
-        self._mark(plan, *bn.names)
+        self._produced.update(bn.names)
         plan.bn_bwd_apply(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
                           bn.scale.data_ptr(), bn.shift.data_ptr(), self.coef.data_ptr(),
                           0 if add is None else add.data_ptr(), dx.data_ptr(), M, C)
+
+    def _flush_buckets(self, plan, force: bool = False):
+        """Emit one grouped split-K reduce for every bucket whose gradients are
+        all produced (or all remaining buckets if `force`); marks them ready."""
+        for bi, (lo, hi, names) in enumerate(self.buckets):
+            if bi in self._flushed:
+                continue
+            if not force and not all(n in self._produced for n in names):
+                continue
+            descs = [self._pending.pop(n) for n in names if n in self._pending]
+            if descs:
+                arr = np.zeros(len(descs), dtype=WGD_DTYPE)
+                chunk = 0
+                for i, (part, grad, sp, K, Kv, taps, C, Cv) in enumerate(descs):
+                    arr[i] = (part, grad, sp, K, Kv, taps, C, Cv, chunk)
+                    chunk += _ceil(K * taps * C, 64)
+                t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+                self._keep.append(t)
+                plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
+            self._mark(plan, *names)
+            self._flushed.add(bi)
 
     def _g(self, i, shape):
         n = math.prod(shape)
@@ -468,20 +499,20 @@ class Engine:
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
                           self.dense_bias_grad, 1.0 / self.global_batch, 0)
-        self._mark(plan, "dense/bias")
         plan.l2_half_sum(self.params.master.data_ptr(), self.params.n_train,
                          self.l2_ws.data_ptr(), sp + 12)
         self.seg["fwd"] = (b0, plan.size())
 
         # ---- backward
         b1 = plan.size()
+        self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
         dg = self._dense_geom(N)
-        spl, pps = self.nat.wgrad_pick_splits(dg)
-        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0,
-                        self.wg_part.data_ptr(), dg, spl, pps)
-        plan.wgrad_reduce(self.wg_part.data_ptr(), self.dense_grad, spl, self.kpad,
-                          spec.num_classes, 1, F, F, 1.0, 0)
-        self._mark(plan, self.dense_name)
+        off, spl, pps = self.wg_off["dense"]
+        dpart = self.wg_part.data_ptr() + 4 * off
+        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0, dpart, dg, spl, pps)
+        self._pending[self.dense_name] = (dpart, self.dense_grad, spl, self.kpad,
+                                          spec.num_classes, 1, F, F)
+        self._produced.add(self.dense_name)
         plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
                        0, 0, 0, 0, 0, 0, dg, [])
         dact = self._g(0, (N, HL, WL, F))
@@ -523,6 +554,7 @@ class Engine:
             dx = self._g(o2, tuple(X.shape))
             self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
+            self._flush_buckets(plan)
         # stem (no dgrad: the input needs no gradient)
         if spec.maxpool:
             dstem = self._g((d + 1) % 3, tuple(self.stem_out.shape))
@@ -534,6 +566,7 @@ class Engine:
             self._conv_bwd(plan, stem, dstem, self.x_in, N, None)
         else:
             self._conv_bwd(plan, stem, dout, self.x_in, N, None)
+        self._flush_buckets(plan, force=True)
         self.seg["bwd"] = (b1, plan.size())
 
         # ---- optimizer
