@@ -291,19 +291,63 @@ static Launch mk_cast_b2f(ptr_t a, ptr_t b, long n) {
 }
 
 // ---------------------------------------------------------------- Plan
+// A plan is a list of ops, each bound to one of two streams (0 = main,
+// 1 = side), plus cross-stream event record/wait ops.  Recording the side
+// stream's first op behind a wait on a main-stream event makes the fork/join
+// structure capturable into a hipGraph (it becomes graph edges).
+struct PlanOp {
+  Launch fn;       // launch (kind 0)
+  int stream;      // 0 main, 1 side
+  int kind;        // 0 launch, 1 record event, 2 wait event
+  int ev;
+};
+
 struct Plan {
-  std::vector<Launch> ops;
+  std::vector<PlanOp> ops;
   std::vector<std::string> names;
+  std::vector<hipEvent_t> events;
+  int cur = 0;
+  ~Plan() {
+    for (auto e : events) (void)hipEventDestroy(e);
+  }
   int add(Launch l, const std::string& name) {
-    ops.push_back(std::move(l));
+    ops.push_back(PlanOp{std::move(l), cur, 0, -1});
     names.push_back(name);
     return (int)ops.size() - 1;
   }
-  void run(int begin, int end, ptr_t stream) {
+  int new_event() {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("hipEventCreate failed");
+    events.push_back(e);
+    return (int)events.size() - 1;
+  }
+  int record(int ev) {
+    ops.push_back(PlanOp{Launch(), cur, 1, ev});
+    names.push_back("record");
+    return (int)ops.size() - 1;
+  }
+  int wait(int ev) {
+    ops.push_back(PlanOp{Launch(), cur, 2, ev});
+    names.push_back("wait");
+    return (int)ops.size() - 1;
+  }
+  void run(int begin, int end, ptr_t main_stream, ptr_t side_stream) {
     if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
-    hipStream_t s = S(stream);
+    hipStream_t st[2] = {S(main_stream), S(side_stream ? side_stream : main_stream)};
     py::gil_scoped_release nogil;
-    for (int i = begin; i < end; ++i) ops[i](s);
+    for (int i = begin; i < end; ++i) {
+      const PlanOp& o = ops[i];
+      hipStream_t s = st[o.stream];
+      if (o.kind == 0) {
+        o.fn(s);
+      } else if (o.kind == 1) {
+        if (hipEventRecord(events[o.ev], s) != hipSuccess) fprintf(stderr, "hipEventRecord failed\n");
+      } else {
+        if (hipStreamWaitEvent(s, events[o.ev], 0) != hipSuccess)
+          fprintf(stderr, "hipStreamWaitEvent failed\n");
+      }
+    }
   }
   int size() const { return (int)ops.size(); }
 };
@@ -331,8 +375,16 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) native kernels + static-plan executor for ResNet training";
   py::class_<Plan> plan(m, "Plan");
   plan.def(py::init<>())
-      .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"))
+      .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"),
+           py::arg("side_stream") = 0)
       .def("size", &Plan::size)
+      .def("new_event", &Plan::new_event)
+      .def("record", &Plan::record)
+      .def("wait", &Plan::wait)
+      .def("use_stream", [](Plan& p, int s) {
+        if (s != 0 && s != 1) throw std::invalid_argument("stream index must be 0 or 1");
+        p.cur = s;
+      })
       .def("names", [](const Plan& p) { return p.names; });
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);

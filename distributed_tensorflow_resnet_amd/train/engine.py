@@ -160,6 +160,7 @@ class Engine:
         self.mom = torch.zeros(self.params.n_train, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
         self.scalars = torch.zeros(8, device=dev)  # loss_sum, correct, lr, l2
+        self.side = torch.cuda.Stream(device=dev)   # weight-gradient stream
         self._build_weight_layout()
         self._alloc_activations()
         self.plan = self.nat.Plan()
@@ -297,7 +298,7 @@ class Engine:
                           N * b.h * b.w * f)
         max_act = max(max_act, self.stem_out.numel())
         self.sc_buf = torch.empty(max(sc_max, 1), dtype=BF16, device=dev)
-        self.G = [torch.empty(max_act, dtype=BF16, device=dev) for _ in range(3)]
+        self._gbufs = []
         F = spec.dense_in
         self.pooled = torch.empty((N, F), dtype=BF16, device=dev)
         self.dpooled = torch.empty((N, F), dtype=BF16, device=dev)
@@ -373,9 +374,16 @@ class Engine:
         geom = self._geom(c, N)
         off, sp, pps = self.wg_off[c.spec.name]
         part = self.wg_part.data_ptr() + 4 * off
+        # fork: the weight gradient only feeds the bucket's grouped reduce, so it
+        # runs on the side stream, overlapping the dgrad -> BN-backward chain.
+        ev = plan.new_event()
+        plan.record(ev)
+        plan.use_stream(1)
+        plan.wait(ev)
         plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
                         0 if pre is None else pre.scale.data_ptr(),
                         0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
+        plan.use_stream(0)
         s = c.spec
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         self._produced.add(c.name)
@@ -426,13 +434,25 @@ class Engine:
                     chunk += _ceil(K * taps * C, 64)
                 t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
                 self._keep.append(t)
+                plan.use_stream(1)
                 plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
+                plan.use_stream(0)
+            # join: the main stream (and the bucket's all-reduce) waits for the side stream
+            ev = plan.new_event()
+            plan.use_stream(1)
+            plan.record(ev)
+            plan.use_stream(0)
+            plan.wait(ev)
             self._mark(plan, *names)
             self._flushed.add(bi)
 
     def _g(self, i, shape):
-        n = math.prod(shape)
-        return self.G[i][:n].view(shape)
+        """A fresh gradient buffer per backward tensor (the index is ignored):
+        with weight gradients running on the side stream, a rotating pool would
+        need WAR fences; 288 GB of HBM makes per-tensor buffers the simpler choice."""
+        t = torch.empty(shape, dtype=BF16, device=self.device)
+        self._gbufs.append(t)
+        return t
 
     # ------------------------------------------------------------------ plan
     def _build_train_plan(self):
@@ -594,7 +614,7 @@ class Engine:
 
     def _run(self, name, stream):
         a, b = self.seg[name]
-        self.plan.run(a, b, stream)
+        self.plan.run(a, b, stream, self.side.cuda_stream)
 
     def _step_eager(self):
         st = torch.cuda.current_stream().cuda_stream
@@ -606,18 +626,19 @@ class Engine:
         a, b = self.seg["bwd"]
         works = []
         if self.bucket_sched:
+            side = self.side.cuda_stream
             prev = a
             for idx, lo, hi in self.bucket_sched:
                 if idx > prev:
-                    self.plan.run(prev, idx, st)
+                    self.plan.run(prev, idx, st, side)
                     prev = idx
                 works.append(self.dist.all_reduce_async(self.grad[lo:hi]))
             if b > prev:
-                self.plan.run(prev, b, st)
+                self.plan.run(prev, b, st, side)
             for w in works:
                 w.wait()
         else:
-            self.plan.run(a, b, st)
+            self.plan.run(a, b, st, self.side.cuda_stream)
 
     def step_timed(self) -> dict:
         """One eager step with HIP-event timing per phase (ProfilerHook)."""
@@ -808,7 +829,7 @@ class _EvalPlan:
         if images is not None:
             if raw_u8:
                 self.img_u8.copy_(images)
-                self.input_plan.run(0, self.input_plan.size(), st)
+                self.input_plan.run(0, self.input_plan.size(), st, 0)
             else:
                 x = images.to(self.eng.device)
                 if x.shape[-1] != self.eng.cpad_in:
@@ -818,6 +839,6 @@ class _EvalPlan:
                 self.x_in.copy_(x.to(BF16))
         if labels is not None:
             self.labels.copy_(labels.to(torch.int32))
-        self.plan.run(0, self.plan.size(), st)
+        self.plan.run(0, self.plan.size(), st, 0)
         v = self.scalars.cpu().tolist()
         return v[0], v[1], self.probs[:, :self.eng.spec.num_classes]
