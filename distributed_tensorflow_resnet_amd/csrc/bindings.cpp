@@ -46,7 +46,9 @@ static ConvGeom geom_from(const std::vector<int>& v) {
 static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32, ptr_t residual,
                            ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
                            ptr_t stat_part, int accumulate, std::vector<int> geom,
-                           std::vector<ptr_t> bnb) {
+                           std::vector<ptr_t> bnb, std::vector<ptr_t> fin,
+                           std::vector<ptr_t> bfin, float momentum, float eps,
+                           int update_moving) {
   GemmArgs g{};
   g.a = P<const bf16>(a);
   g.b = P<const bf16>(b);
@@ -68,6 +70,19 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     g.bnb_scale = P<const float>(bnb[3]);
     g.bnb_shift = P<const float>(bnb[4]);
     g.bnb_part = P<float>(bnb[5]);
+  }
+  if (!fin.empty()) {  // [counters, gamma, beta, mmean, mvar, mean, rstd, scale, shift]
+    if (fin.size() != 9) throw std::invalid_argument("fin needs 9 pointers");
+    if (stat_part == 0) throw std::invalid_argument("fin requires stat_part");
+    g.fin = BnFwdFin{P<unsigned>(fin[0]), P<const float>(fin[1]), P<const float>(fin[2]),
+                     P<float>(fin[3]), P<float>(fin[4]), P<float>(fin[5]), P<float>(fin[6]),
+                     P<float>(fin[7]), P<float>(fin[8]), momentum, eps, update_moving};
+  }
+  if (!bfin.empty()) {  // [counters, gamma, rstd, dgamma, dbeta, coef]
+    if (bfin.size() != 6) throw std::invalid_argument("bfin needs 6 pointers");
+    if (bnb.empty()) throw std::invalid_argument("bfin requires bnb");
+    g.bfin = BnBwdFin{P<unsigned>(bfin[0]), P<const float>(bfin[1]), P<const float>(bfin[2]),
+                      P<float>(bfin[3]), P<float>(bfin[4]), P<float>(bfin[5])};
   }
   g.g = geom_from(geom);
   const ConvGeom& c = g.g;

@@ -28,6 +28,7 @@
 //           sum(g * xhat), so no separate pass re-reads d_a and x.
 #include <algorithm>
 
+#include "bn_fused.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -388,8 +389,73 @@ conv_gemm_kernel(GemmArgs args) {
   if constexpr (STATS) {
     if (tid < BN && n0 + tid < NC) {
       float* tile_out = args.stat_part + (long)blockIdx.x * 2 * NC;
-      tile_out[n0 + tid] = wmean_run;       // tile mean
-      tile_out[NC + n0 + tid] = wm2_run;    // tile M2
+      if (args.fin.counters != nullptr) {   // handed to the last arriver: write-through (sc1)
+        publish_f32(tile_out + n0 + tid, wmean_run);
+        publish_f32(tile_out + NC + n0 + tid, wm2_run);
+      } else {
+        tile_out[n0 + tid] = wmean_run;     // tile mean
+        tile_out[NC + n0 + tid] = wm2_run;  // tile M2
+      }
+    }
+    const BnFwdFin& F = args.fin;
+    if (F.counters != nullptr &&
+        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
+      // Chan-combine all tiles of columns [n0, n0+BN): thread = (column, tile group)
+      constexpr int G = 256 / BN;
+      const int c = tid % BN, gq2 = tid / BN;
+      const int col = n0 + c;
+      float n = 0.f, mu = 0.f, m2 = 0.f;
+      const int T = gridDim.x;
+      if (col < NC) {   // host guarantees T <= G * FIN_UNROLL: all loads in flight at once
+        float mbv[FIN_UNROLL], qbv[FIN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          mbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + col] : 0.f;
+          qbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + NC + col] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          if (t < T) {
+            const float nb = (float)min(BM, M - t * BM);
+            const float nn = n + nb, d = mbv[u] - mu;
+            mu += d * nb / nn;
+            m2 += qbv[u] + d * d * n * nb / nn;
+            n = nn;
+          }
+        }
+      }
+      red[gq2 * BN + c] = n;
+      red2[gq2 * BN + c] = mu;
+      cs[gq2 * BN + c] = m2;                // staging tile is free now
+      __syncthreads();
+      if (gq2 == 0 && col < NC) {
+        float fn_ = red[c], fmu = red2[c], fm2 = cs[c];
+        for (int k = 1; k < G; ++k) {
+          const float nb = red[k * BN + c], mb = red2[k * BN + c], qb = cs[k * BN + c];
+          const float nn = fn_ + nb;
+          if (nn > 0.f) {
+            const float d = mb - fmu;
+            fmu += d * nb / nn;
+            fm2 += qb + d * d * fn_ * nb / nn;
+            fn_ = nn;
+          }
+        }
+        const float var = fm2 / fn_;
+        const float rs = rsqrtf(var + F.eps);
+        const float sc = F.gamma[col] * rs;
+        F.mean[col] = fmu;
+        F.rstd[col] = rs;
+        F.scale[col] = sc;
+        F.shift[col] = F.beta[col] - fmu * sc;
+        if (F.update_moving) {
+          const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
+          F.mmean[col] -= (1.f - F.momentum) * (F.mmean[col] - fmu);
+          F.mvar[col] -= (1.f - F.momentum) * (F.mvar[col] - uvar);
+        }
+      }
+      reset_counter(F.counters + blockIdx.y);
     }
   }
   if constexpr (BNB) {
@@ -406,8 +472,53 @@ conv_gemm_kernel(GemmArgs args) {
         t2 += red2[k * BN + tid];
       }
       float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
-      tile_out[n0 + tid] = t1;        // sum g
-      tile_out[NC + n0 + tid] = t2;   // sum g * xhat
+      if (args.bfin.counters != nullptr) {
+        publish_f32(tile_out + n0 + tid, t1);
+        publish_f32(tile_out + NC + n0 + tid, t2);
+      } else {
+        tile_out[n0 + tid] = t1;        // sum g
+        tile_out[NC + n0 + tid] = t2;   // sum g * xhat
+      }
+    }
+    const BnBwdFin& F = args.bfin;
+    if (F.counters != nullptr &&
+        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
+      constexpr int G = 256 / BN;
+      const int c = tid % BN, gq2 = tid / BN;
+      const int col = n0 + c;
+      float a1 = 0.f, a2 = 0.f;
+      const int T = gridDim.x;
+      if (col < NC) {
+        float v1[FIN_UNROLL], v2[FIN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          v1[u] = t < T ? args.bnb_part[(long)t * 2 * NC + col] : 0.f;
+          v2[u] = t < T ? args.bnb_part[(long)t * 2 * NC + NC + col] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          a1 += v1[u];
+          a2 += v2[u];
+        }
+      }
+      red[gq2 * BN + c] = a1;
+      red2[gq2 * BN + c] = a2;
+      __syncthreads();
+      if (gq2 == 0 && col < NC) {
+        float sg = 0.f, sgx = 0.f;
+        for (int k = 0; k < G; ++k) {
+          sg += red[k * BN + c];
+          sgx += red2[k * BN + c];
+        }
+        F.dbeta[col] = sg;
+        F.dgamma[col] = sgx;
+        const float a = F.gamma[col] * F.rstd[col];
+        F.coef[col] = a;
+        F.coef[NC + col] = a * sg / (float)M;
+        F.coef[2 * NC + col] = a * sgx / (float)M;
+      }
+      reset_counter(F.counters + blockIdx.y);
     }
   }
 }

@@ -18,6 +18,29 @@ struct ConvGeom {
   int kh, kw, stride, pad;
 };
 
+// Fused BatchNorm finalize in the producing kernel (last-arriver; see bn_fused.h).
+struct BnFwdFin {            // forward statistics -> mean/rstd/scale/shift + moving averages
+  unsigned* counters;        // one per column tile; nullptr = disabled
+  const float* gamma;
+  const float* beta;
+  float* mmean;
+  float* mvar;
+  float* mean;
+  float* rstd;
+  float* scale;
+  float* shift;
+  float momentum, eps;
+  int update_moving;
+};
+struct BnBwdFin {            // backward sums -> dgamma/dbeta/apply coefficients
+  unsigned* counters;        // nullptr = disabled
+  const float* gamma;
+  const float* rstd;
+  float* dgamma;
+  float* dbeta;
+  float* coef;               // [3][C]
+};
+
 struct GemmArgs {
   const bf16* a;            // x (fwd) or dy (dgrad), NHWC
   const bf16* b;            // weights: [K][kh][kw][C] (fwd) or [kh][kw][C][K] (dgrad)
@@ -36,6 +59,8 @@ struct GemmArgs {
   const float* bnb_scale;
   const float* bnb_shift;
   float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
+  BnFwdFin fin;             // with stat_part: finalize in-kernel
+  BnBwdFin bfin;            // with bnb_part: finalize in-kernel
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;

@@ -102,7 +102,7 @@ def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residu
                        0 if out_f32 else out.data_ptr(), out.data_ptr() if out_f32 else 0,
                        _ptr(residual), _ptr(pre_scale), _ptr(pre_shift), _ptr(bias),
                        0 if bias is None else bias.numel(), _ptr(stat_part), int(accumulate),
-                       g.as_list(), [], _stream())
+                       g.as_list(), [], [], [], 0.997, 1e-5, 1, _stream())
     return out
 
 
@@ -122,7 +122,7 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
         out = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
     bl = [] if bnb is None else [t.data_ptr() for t in bnb]
     native().conv_gemm(1, dy.data_ptr(), w_hwio.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                       int(accumulate), g.as_list(), bl, _stream())
+                       int(accumulate), g.as_list(), bl, [], [], 0.997, 1e-5, 1, _stream())
     return out
 
 

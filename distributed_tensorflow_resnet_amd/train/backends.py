@@ -22,7 +22,7 @@ from ..utils.checkpoint import state_to_tf, tf_to_state
 
 
 class GPUBackend:
-    def __init__(self, engine, use_graph: bool = True):
+    def __init__(self, engine, use_graph: bool = False):
         self.engine = engine
         self.use_graph = use_graph
         self._host_step = int(engine.gstep.item())
@@ -184,7 +184,7 @@ class CPUBackend:
 
 def make_backend(spec: ModelSpec, batch_size: int, *, device: str, weight_decay: float,
                  lr_schedule, optimizer: str = "mom", seed: int = 0, dist_ctx=None,
-                 bucket_mb: float = 25.0, use_graph: bool = True, global_batch=None,
+                 bucket_mb: float = 25.0, use_graph: bool = False, global_batch=None,
                  input_mode: str = "auto", data_seed: int = 1234):
     """device: gpu | cpu | auto."""
     if device == "auto":

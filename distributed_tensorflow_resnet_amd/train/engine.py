@@ -133,7 +133,7 @@ class Engine:
                  lr_schedule: LRSchedule, optimizer: str = "mom", momentum: float = 0.9,
                  device=None, dist_ctx=None, bucket_mb: float = 25.0, seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
-                 use_graph: bool = True, data_seed: int = 1234):
+                 use_graph: bool = True, data_seed: int = 1234, fork_wgrad: bool | None = None):
         self.nat = native(required=True)
         self.spec = spec
         self.N = batch_size
@@ -147,6 +147,11 @@ class Engine:
         self.sched = lr_schedule
         self.use_graph = use_graph
         self.data_seed = data_seed
+        if fork_wgrad is None:
+            # measured: eager + forked wgrad stream beats hipGraph replay (which
+            # handles the cross-stream event edges poorly); graphs stay single-stream
+            fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
+        self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
             input_mode = "cifar_u8" if spec.dataset.startswith("cifar") else "nhwc"
         self.input_mode = input_mode
@@ -247,6 +252,8 @@ class Engine:
         bn_specs = [b for blk in spec.blocks for b in blk.bns] + [spec.final_bn]
         total_c = sum(b.channels for b in bn_specs)
         self.bnbuf = torch.zeros(4 * total_c, device=self.device)
+        # last-arriver counters for in-kernel BN finalize: per BN 2 x 128 column tiles
+        self.bn_counters = torch.zeros(len(bn_specs) * 256, dtype=torch.int32, device=self.device)
         off = 0
         for b in bn_specs:
             g = ps.slot(f"{b.name}/gamma")
@@ -261,6 +268,9 @@ class Engine:
             e.rstd = self.bnbuf[total_c + off:total_c + off + C]
             e.scale = self.bnbuf[2 * total_c + off:2 * total_c + off + C]
             e.shift = self.bnbuf[3 * total_c + off:3 * total_c + off + C]
+            e.cnt_fwd = self.bn_counters.data_ptr() + 4 * (256 * len(self.bns))
+            e.cnt_bwd = e.cnt_fwd + 4 * 128
+            e.fused_fwd = e.fused_bwd = False
             off += C
             self.bns[b.name] = e
 
@@ -339,21 +349,39 @@ class Engine:
     def _dense_geom(self, N):
         return [N, 1, 1, self.spec.dense_in, 1, 1, self.kpad, 1, 1, 1, 0]
 
+    def _fuse_finalize(self, M: int, nc: int) -> bool:
+        """In-kernel (last-arriver) BN finalize pays when the combine is one round
+        trip: <= FIN_UNROLL (8) partial tiles per combining thread."""
+        if os.environ.get("DTR_FUSED_BN_FINALIZE", "1") == "0":
+            return False
+        bm = self.nat.conv_gemm_bm(M, nc)
+        bn = 16 if nc <= 16 else 32 if nc <= 32 else 64 if nc <= 64 else (128 if bm == 128 else 64)
+        return _ceil(_ceil(M, bm), 256 // bn) <= 8 and _ceil(nc, bn) <= 128
+
     def _conv_fwd(self, plan, c: _Conv, x, out, N, pre: _BN | None = None, residual=None,
                   stats_for: _BN | None = None):
         geom = self._geom(c, N)
         stat_ptr = 0
+        fin = []
         if stats_for is not None:
             M = N * c.spec.ho * c.spec.wo
             bm = self.nat.conv_gemm_bm(M, c.spec.cout)
             stats_for.src = (_ceil(M, bm), bm, M)
             stat_ptr = self.stat_part.data_ptr()
+            if self._fuse_finalize(M, c.spec.cout):
+                b = stats_for
+                b.fused_fwd = True
+                fin = [b.cnt_fwd, b.gamma, b.beta, b.mmean, b.mvar, b.mean.data_ptr(),
+                       b.rstd.data_ptr(), b.scale.data_ptr(), b.shift.data_ptr()]
         plan.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                        0 if residual is None else residual.data_ptr(),
                        0 if pre is None else pre.scale.data_ptr(),
-                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [])
+                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [], fin, [],
+                       BN_DECAY, BN_EPS, 1)
 
     def _bn_finalize(self, plan, bn: _BN, train=True):
+        if bn.fused_fwd:
+            return  # finalized by the producing conv's last workgroup
         tiles, rows, M = bn.src
         plan.bn_finalize(self.stat_part.data_ptr(), tiles, rows, M, bn.spec.channels, bn.gamma,
                          bn.beta, bn.mmean, bn.mvar, BN_DECAY, BN_EPS, int(train),
@@ -376,10 +404,11 @@ class Engine:
         part = self.wg_part.data_ptr() + 4 * off
         # fork: the weight gradient only feeds the bucket's grouped reduce, so it
         # runs on the side stream, overlapping the dgrad -> BN-backward chain.
-        ev = plan.new_event()
-        plan.record(ev)
-        plan.use_stream(1)
-        plan.wait(ev)
+        if self.fork_wgrad:
+            ev = plan.new_event()
+            plan.record(ev)
+            plan.use_stream(1)
+            plan.wait(ev)
         plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
                         0 if pre is None else pre.scale.data_ptr(),
                         0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
@@ -388,15 +417,19 @@ class Engine:
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         self._produced.add(c.name)
         if dx is not None:
-            bl = []
+            bl, bfl = [], []
             if bnb is not None:
                 bn, bx = bnb
                 bl = [bx.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
                       bn.shift.data_ptr(), self.bwd_part.data_ptr()]
                 Mx = N * s.h * s.w
                 self._bnb_tiles = _ceil(Mx, self.nat.conv_gemm_bm(Mx, c.cin))
+                if self._fuse_finalize(Mx, c.cin):
+                    bn.fused_bwd = True
+                    bfl = [bn.cnt_bwd, bn.gamma, bn.rstd.data_ptr(), bn.dgamma, bn.dbeta,
+                           self.coef.data_ptr()]
             plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                           int(accumulate), geom, bl)
+                           int(accumulate), geom, bl, [], bfl, BN_DECAY, BN_EPS, 1)
 
     def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None, reduced: bool = False):
         """BN+ReLU backward.  ``reduced``: the producing dgrad already wrote the
@@ -410,8 +443,9 @@ class Engine:
             plan.bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(),
                                bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(), M, C,
                                self.bwd_part.data_ptr())
-        plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
-                             bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
+        if not (reduced and bn.fused_bwd):
+            plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
+                                 bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
         self._produced.update(bn.names)
         plan.bn_bwd_apply(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
                           bn.scale.data_ptr(), bn.shift.data_ptr(), self.coef.data_ptr(),
@@ -434,15 +468,16 @@ class Engine:
                     chunk += _ceil(K * taps * C, 64)
                 t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
                 self._keep.append(t)
-                plan.use_stream(1)
+                plan.use_stream(1 if self.fork_wgrad else 0)
                 plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
                 plan.use_stream(0)
-            # join: the main stream (and the bucket's all-reduce) waits for the side stream
-            ev = plan.new_event()
-            plan.use_stream(1)
-            plan.record(ev)
-            plan.use_stream(0)
-            plan.wait(ev)
+            if self.fork_wgrad:
+                # join: the main stream (and the bucket's all-reduce) waits for the side stream
+                ev = plan.new_event()
+                plan.use_stream(1)
+                plan.record(ev)
+                plan.use_stream(0)
+                plan.wait(ev)
             self._mark(plan, *names)
             self._flushed.add(bi)
 
@@ -458,6 +493,8 @@ class Engine:
     def _build_train_plan(self):
         plan, spec, N = self.plan, self.spec, self.N
         self.seg = {}
+        for e in self.bns.values():
+            e.fused_fwd = e.fused_bwd = False
         b0 = plan.size()
         # ---- input
         if self.input_mode == "cifar_u8":
@@ -514,7 +551,7 @@ class Engine:
         plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                             self.pooled.data_ptr(), N, HL * WL, F)
         plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
-                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [])
+                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
@@ -534,7 +571,7 @@ class Engine:
                                           spec.num_classes, 1, F, F)
         self._produced.add(self.dense_name)
         plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
-                       0, 0, 0, 0, 0, 0, dg, [])
+                       0, 0, 0, 0, 0, 0, dg, [], [], [], BN_DECAY, BN_EPS, 1)
         dact = self._g(0, (N, HL, WL, F))
         plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
         d = 1
@@ -778,7 +815,7 @@ class _EvalPlan:
                       bn.scale.data_ptr(), bn.shift.data_ptr())
         y = buf((N, st.ho, st.wo, st.cout))
         p.conv_gemm(0, self.x_in.data_ptr(), stem.ohwi, y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
-                    eng._geom(stem, N), [])
+                    eng._geom(stem, N), [], [], [], BN_DECAY, BN_EPS, 1)
         if spec.maxpool:
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
@@ -808,7 +845,7 @@ class _EvalPlan:
         p.bnrelu_avgpool(x.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                          self.pooled.data_ptr(), N, x.shape[1] * x.shape[2], F)
         p.conv_gemm(0, self.pooled.data_ptr(), eng.dense_ohwi, 0, self.logits.data_ptr(), 0, 0, 0,
-                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [])
+                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
                        spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
@@ -817,7 +854,7 @@ class _EvalPlan:
     def _conv(self, p, c, x, out, pre, residual=None):
         p.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                     0 if residual is None else residual.data_ptr(), pre.scale.data_ptr(),
-                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [])
+                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [], [], [], BN_DECAY, BN_EPS, 1)
 
     def run(self, images=None, labels=None, raw_u8: bool = True):
         """Returns (loss_sum, correct, probs[N, classes]) for one eval batch.
