@@ -53,7 +53,7 @@ def main(argv=None) -> int:
     import torch
 
     from distributed_tensorflow_resnet_amd.models.spec import build_spec
-    from distributed_tensorflow_resnet_amd.parallel.dist import DistContext
+    from distributed_tensorflow_resnet_amd.parallel.dist import DistContext, local_device_index
     from distributed_tensorflow_resnet_amd.train.engine import (Engine, cifar_lr_schedule,
                                                                 imagenet_lr_schedule)
 
@@ -65,7 +65,7 @@ def main(argv=None) -> int:
         if world == 1 and args.gpus > 1:
             print("bench.py: --gpus > 1 must be launched with torchrun", file=sys.stderr)
             return 2
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = local_device_index()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     ctx = DistContext(device=device)

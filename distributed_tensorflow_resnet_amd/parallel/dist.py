@@ -25,6 +25,16 @@ def env_world() -> tuple[int, int, int]:
     return rank, world, local
 
 
+def local_device_index() -> int:
+    """GPU for this rank: LOCAL_RANK, folded onto the visible devices.  Folding
+    only matters for rehearsals that put several ranks on one GPU (with
+    DTR_DIST_BACKEND=gloo, since RCCL refuses duplicate devices);
+    `torch.cuda.device_count()` does not initialise the GPU."""
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    n = torch.cuda.device_count()
+    return local % n if n > 0 else local
+
+
 class DistContext:
     """Thin, explicit wrapper so the engine never touches global state."""
 
@@ -38,7 +48,8 @@ class DistContext:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
+                backend = os.environ.get("DTR_DIST_BACKEND") or (
+                    "nccl" if torch.cuda.is_available() else "gloo")
             self.backend = backend
             kw = {}
             if backend == "nccl" and device is not None:

@@ -18,6 +18,7 @@ from ..data.cifar import augment_cpu
 from ..models.params import ParamStore
 from ..models.resnet_torch import TorchResNet
 from ..models.spec import ModelSpec
+from ..parallel.dist import local_device_index
 from ..utils.checkpoint import state_to_tf, tf_to_state
 
 
@@ -192,7 +193,7 @@ def make_backend(spec: ModelSpec, batch_size: int, *, device: str, weight_decay:
     if device == "gpu":
         from .engine import Engine
 
-        local = dist_ctx.local_rank if dist_ctx is not None else 0
+        local = local_device_index()
         torch.cuda.set_device(local)
         eng = Engine(spec, batch_size, weight_decay=weight_decay, lr_schedule=lr_schedule,
                      optimizer=optimizer, device=torch.device("cuda", local), dist_ctx=dist_ctx,

@@ -21,7 +21,7 @@ import time
 import torch
 
 from ..models.spec import build_spec
-from ..parallel.dist import DistContext
+from ..parallel.dist import DistContext, local_device_index
 from ..utils.checkpoint import Saver
 from ..utils.flags import build_parser, warn_unsupported
 from ..utils.records import EventWriter
@@ -123,7 +123,7 @@ def main(argv=None, kind: str = "cifar") -> int:
     # ---------------------------------------------------------------- train
     dev = None
     if device == "gpu":
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     ctx = DistContext(device=dev)
