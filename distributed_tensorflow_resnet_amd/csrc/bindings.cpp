@@ -431,6 +431,8 @@ PYBIND11_MODULE(_C, m) {
 
   // host-side helpers that mirror the launchers' internal choices
   m.def("conv_gemm_bm", &conv_gemm_bm);
+  m.def("set_conv_direct", &set_conv_direct,
+        "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);

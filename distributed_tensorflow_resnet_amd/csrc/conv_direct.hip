@@ -1,0 +1,214 @@
+// Direct (halo-tiled) 3x3 / stride-1 / pad-1 convolution, forward and data
+// gradient, for the small channel counts of the CIFAR stages (C = K in
+// {16, 32, 64}; resnet_model_official.py:80-91 emits them through
+// conv2d_fixed_padding, SURVEY Appendix A rows "32|16|16|3|1", "16|32|32|3|1",
+// "8|64|64|3|1" -- 46 of the 52 CIFAR ResNet-50 convs).
+//
+// Why a second kernel: the implicit-GEMM path (conv_gemm.hip) gathers an
+// im2col row per output pixel, i.e. every input element is fetched 9 times and
+// the K loop runs ceil(9C/64) dependent global round trips per workgroup.  At
+// C <= 64 the MFMA work is tiny and those round trips ARE the kernel time.
+// Here a workgroup owns R = BM / W whole output rows of one image:
+//   1. it issues, all at once, the loads of the (R+2) x (W+2) x C input halo
+//      (zero rows/columns = TF's fixed padding; the previous layer's BN+ReLU
+//      applied once per element in the PRE variant, never per tap) and the
+//      per-lane B (weight) fragments of its output channels, straight into
+//      VGPRs -- one memory latency for the whole tile;
+//   2. stores the halo to LDS with a 16-B-unit XOR swizzle (unit ^ (col &
+//      (U-1))) so the 16 consecutive-pixel lanes of a ds_read_b128 spread over
+//      the banks;
+//   3. runs ceil(9C/32) v_mfma_f32_16x16x32_bf16 k-steps per 16x16 fragment,
+//      the k index being (tap, channel): lane group q of step s reads channels
+//      [c, c+8) of tap t with s*32 + 8q = t*C + c (taps past 9 carry zero
+//      weights);
+//   4. hands the fp32 fragments to the shared conv epilogue (bias / residual /
+//      BN statistics / BN-backward sums / last-arriver finalize).
+// dgrad is the same convolution over dy with the taps flipped (offset 8 - t)
+// and the HWIO weights read with K contiguous.
+#include <algorithm>
+#include <cstdlib>
+
+#include "conv_epilogue.h"
+
+namespace dtr {
+
+template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
+__global__ void __launch_bounds__(256)
+conv3x3_direct_kernel(GemmArgs args) {
+  constexpr bool PRE = (FLAGS & F_PRE) != 0;
+  constexpr int U = CA / 8;                 // 16-B units per pixel
+  constexpr int R = BM / WI;                // output rows per tile
+  constexpr int HW2 = WI + 2;               // halo row length (pixels)
+  constexpr int HU = (R + 2) * HW2 * U;     // halo units
+  constexpr int HPT = (HU + 255) / 256;     // halo units per thread
+  constexpr int KSTEPS = (9 * CA + 31) / 32;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MR = WTM / 16, NR = WTN / 16;
+  static_assert(BM % WI == 0 && WM * WN == 4 && MR >= 1 && NR >= 1, "tile");
+  static_assert((U & (U - 1)) == 0, "C/8 must be a power of two");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = reinterpret_cast<bf16*>(smem);
+
+  const ConvGeom& g = args.g;
+  const int NC = args.Ncol;
+  const int H = g.H;                        // stride 1: A and output share H x W
+  const int HWp = H * WI;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int img = m0 / HWp;
+  const int h0 = (m0 - img * HWp) / WI;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bf16x8 zero8 = {};
+
+  // ---- 1. all global loads in flight at once: weights (VGPR) + halo (VGPR) ----
+  bf16x8 breg[KSTEPS][NR];
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    const int kk = s * 32 + fq * 8;
+    const int tap = kk / CA, c = kk - tap * CA;
+#pragma unroll
+    for (int nb = 0; nb < NR; ++nb) {
+      const int n = n0 + wn * WTN + nb * 16 + fr;
+      bf16x8 v = zero8;
+      if (tap < 9 && n < NC) {
+        const long off = (MODE == MODE_FWD) ? (long)n * (9 * CA) + kk        // W[co][r][c][ci]
+                                            : ((long)tap * NC + n) * CA + c;  // W[r][c][ci][co]
+        v = *reinterpret_cast<const bf16x8*>(args.b + off);
+      }
+      breg[s][nb] = v;
+    }
+  }
+  bf16x8 hv[HPT];
+  const bf16* abase = args.a + (long)img * HWp * CA;
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int q = tid + i * 256;
+    bf16x8 v = zero8;
+    if (q < HU) {
+      const int u = q % U, pix = q / U;
+      const int hr = pix / HW2, hc = pix - hr * HW2;
+      const int h = h0 - 1 + hr, w = hc - 1;
+      if (h >= 0 && h < H && w >= 0 && w < WI) {
+        v = *reinterpret_cast<const bf16x8*>(abase + ((long)h * WI + w) * CA + u * 8);
+        if constexpr (PRE) v = affine_relu8(v, args.pre_scale + u * 8, args.pre_shift + u * 8);
+      }
+    }
+    hv[i] = v;
+  }
+  // ---- 2. halo -> LDS (swizzled 16-B units) ----
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int q = tid + i * 256;
+    if (q < HU) {
+      const int u = q % U, pix = q / U;
+      const int hc = pix % HW2;
+      *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = hv[i];
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. MFMA over (tap, channel) k-steps ----
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int pbase[MR], pw[MR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a) {
+    const int p = wm * WTM + a * 16 + fr;     // tile-local output pixel
+    const int hl = p / WI, w = p - hl * WI;
+    pbase[a] = hl * HW2 + w;                  // halo pixel of the window's top-left
+    pw[a] = w;
+  }
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    const int kk = s * 32 + fq * 8;
+    int tap = kk / CA;
+    const int unit = (kk - tap * CA) >> 3;
+    tap = tap < 9 ? tap : 8;                  // padded k: zero weights, any finite A
+    const int ta = (MODE == MODE_FWD) ? tap : 8 - tap;
+    const int dy = ta / 3, dx = ta - dy * 3;
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+      const int hc = pw[a] + dx;
+      const int pix = pbase[a] + dy * HW2 + dx;
+      const bf16x8 af =
+          *reinterpret_cast<const bf16x8*>(halo + (pix * U + (unit ^ (hc & (U - 1)))) * 8);
+#pragma unroll
+      for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af, breg[s][b], acc[a][b]);
+    }
+  }
+  __syncthreads();   // halo dead: the epilogue reuses the LDS
+
+  // ---- 4. shared epilogue ----
+  conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
+}
+
+template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
+static void launch_direct_cfg(const GemmArgs& a, hipStream_t s) {
+  constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
+  const size_t lds = (std::max((size_t)HU * 16, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
+  dim3 grid(a.M / BM, (a.Ncol + BN - 1) / BN);
+  hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
+                     dim3(256), lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE>
+static void launch_direct_flags(const GemmArgs& a, hipStream_t s) {
+  const bool pre = a.pre_scale != nullptr, st = a.stat_part != nullptr;
+  if constexpr (MODE == MODE_FWD) {
+    if (pre && st) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_PRE | F_STATS>(a, s);
+    else if (pre) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_PRE>(a, s);
+    else if (st) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_STATS>(a, s);
+    else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, 0>(a, s);
+  } else {
+    if (a.bnb_part != nullptr) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_BNB>(a, s);
+    else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, 0>(a, s);
+  }
+}
+
+static int g_direct_enabled = -1;   // -1: read DTR_DIRECT_CONV once
+
+void set_conv_direct(int enabled) { g_direct_enabled = enabled ? 1 : 0; }
+
+// Returns true (and launches) when the direct kernel covers this conv: 3x3,
+// stride 1, pad 1, A channels == output channels == {16 @ W 32, 32 @ W 16,
+// 64 @ W 8}, and the tile height BM (= conv_gemm_bm, so the BN-stat partial
+// layout is unchanged) divides the image.
+bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
+  if (g_direct_enabled < 0) {
+    const char* e = std::getenv("DTR_DIRECT_CONV");
+    g_direct_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_direct_enabled) return false;
+  const ConvGeom& g = a.g;
+  if (g.kh != 3 || g.kw != 3 || g.stride != 1 || g.pad != 1 || g.H != g.Ho || g.W != g.Wo)
+    return false;
+  if (a.out_f32 != nullptr || a.bias != nullptr) return false;
+  const int ca = (mode == MODE_FWD) ? g.C : g.K;
+  const int nc = a.Ncol;
+  if (ca != nc) return false;
+  const int bm = conv_gemm_bm(a.M, nc);
+  const int hw = g.H * g.W;
+  if (bm % g.W != 0 || hw % bm != 0 || a.M % bm != 0) return false;
+  const bool fwd = mode == MODE_FWD;
+#define DTR_DIRECT(CA_, W_, BM_, WM_, WN_)                                              \
+  if (ca == CA_ && g.W == W_ && bm == BM_) {                                          \
+    if (fwd) launch_direct_flags<CA_, W_, BM_, CA_, WM_, WN_, MODE_FWD>(a, s);        \
+    else launch_direct_flags<CA_, W_, BM_, CA_, WM_, WN_, MODE_DGRAD>(a, s);          \
+    return true;                                                                      \
+  }
+  DTR_DIRECT(16, 32, 256, 4, 1)
+  DTR_DIRECT(16, 32, 64, 4, 1)
+  DTR_DIRECT(32, 16, 128, 2, 2)
+  DTR_DIRECT(32, 16, 64, 2, 2)
+  DTR_DIRECT(64, 8, 64, 1, 4)
+#undef DTR_DIRECT
+  return false;
+}
+
+}  // namespace dtr

@@ -1,0 +1,334 @@
+// Shared conv epilogue (implicit-GEMM conv_gemm.hip and direct conv_direct.hip).
+#pragma once
+#include "bn_fused.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+enum { F_PRE = 1, F_STATS = 2, F_BNB = 4 };
+
+// Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
+// it fits in 64 KiB (one phase), else one wave-row per phase (128x128 tiles).
+template <int BM, int BN, int WM>
+struct EpiLayout {
+  static constexpr int LDC = BN + 4;              // fp32 staging row stride (floats)
+  static constexpr int CPR = BN / 8;              // 8-channel chunks per row
+  static constexpr int RPP = 256 / CPR;           // rows per pass
+  static constexpr int RED = 2 * RPP * BN + BN;   // floats (two reduction planes + means)
+  static constexpr int PHASES = ((BM * LDC + RED) * 4 <= 64 * 1024) ? 1 : WM;
+  static constexpr int PR = BM / PHASES;          // rows staged per phase
+  static constexpr int TILE = PR * LDC;           // floats
+  static constexpr size_t BYTES = (size_t)(TILE + RED) * sizeof(float);
+};
+
+// Shared epilogue of every conv kernel (implicit-GEMM and direct): the wave
+// fragments acc[MR][NR] of the BM x BN tile at (m0, n0) -> LDS-staged 16-byte
+// row stores with bias / residual / accumulate, BN statistics (STATS), BN
+// backward sums (BNB) and the optional last-arriver finalize.  Entered after a
+// workgroup barrier (the caller's LDS is dead).
+template <int BM, int BN, int WM, int WN, int FLAGS>
+__device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
+                                              f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                              char* smem, const int m0, const int n0) {
+  constexpr bool STATS = (FLAGS & F_STATS) != 0;
+  constexpr bool BNB = (FLAGS & F_BNB) != 0;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int MR = WTM / 16, NR = WTN / 16;
+  const int M = args.M, NC = args.Ncol;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  // ---------------- epilogue ----------------
+  // Processed in EL::PHASES phases of EL::PR rows (1 phase unless the tile is 128x128):
+  //  (a) the waves owning those rows write their fragments (+bias) to an fp32 LDS tile
+  //      (the K loop ended with a barrier: staging buffers/PRE table are dead);
+  //  (b) all 256 threads sweep it as 16-byte row vectors (8 channels per lane):
+  //      residual / accumulate, ONE bf16 rounding, 16-B store, BN partials;
+  //  (c) STATS: per-phase two-pass (mean, M2) folded across phases with Chan's
+  //      formula in fixed order; BNB: sums carried in registers.
+  using EL = EpiLayout<BM, BN, WM>;
+  float* cs = reinterpret_cast<float*>(smem);
+  float* red = cs + EL::TILE;
+  float* red2 = red + EL::RPP * BN;
+  float* mean_s = red + 2 * EL::RPP * BN;
+  const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
+  const int col0 = n0 + cc * 8;
+  const bool colok = col0 < NC;  // NC % 16 == 0 -> a chunk is all-in or all-out
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  float bsc[8], bsh[8], bmu[8], brs[8];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = colok ? args.bnb_scale[col0 + j] : 0.f;
+      bsh[j] = colok ? args.bnb_shift[col0 + j] : 0.f;
+      bmu[j] = colok ? args.bnb_mean[col0 + j] : 0.f;
+      brs[j] = colok ? args.bnb_rstd[col0 + j] : 0.f;
+    }
+  }
+  float wn_run = 0.f, wmean_run = 0.f, wm2_run = 0.f;  // STATS, thread tid < BN owns column tid
+
+#pragma unroll 1
+  for (int ph = 0; ph < EL::PHASES; ++ph) {
+    const int prow0 = m0 + ph * EL::PR;
+    const int nph = min(EL::PR, M - prow0);   // block-uniform
+    if (nph <= 0) break;
+    if ((wm * WTM) / EL::PR == ph) {
+      const int rbase = wm * WTM - ph * EL::PR;
+#pragma unroll
+      for (int b = 0; b < NR; ++b) {
+        const int cl = wn * WTN + b * 16 + fr;
+        const int col = n0 + cl;
+        const float bias = (args.bias != nullptr && col < args.nbias) ? args.bias[col] : 0.f;
+#pragma unroll
+        for (int a = 0; a < MR; ++a)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            cs[(rbase + a * 16 + fq * 4 + i) * EL::LDC + cl] = acc[a][b][i] + bias;
+      }
+    }
+    __syncthreads();
+    float p1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p1[j] = 0.f;
+    for (int r = r0; r < nph; r += EL::RPP) {
+      if (!colok) break;
+      const int row = prow0 + r;
+      float* cp = cs + r * EL::LDC + cc * 8;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cp);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cp + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const long o = (long)row * NC + col0;
+      if (args.residual) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(args.residual + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+      }
+      if (args.out_f32) {
+        float* op = args.out_f32 + o;
+        if (args.accumulate) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(op);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(op + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] += a0[j];
+            v[4 + j] += a1[j];
+          }
+        }
+        *reinterpret_cast<f32x4*>(op) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(op + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        if (args.accumulate) {
+          const bf16x8 av = *reinterpret_cast<const bf16x8*>(args.out + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
+        }
+        bf16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ob[j] = (bf16)v[j];
+          v[j] = (float)ob[j];
+        }
+        *reinterpret_cast<bf16x8*>(args.out + o) = ob;
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p1[j] += v[j];
+        *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+      if constexpr (BNB) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = (float)xv[j];
+          const float gg = (xf * bsc[j] + bsh[j] > 0.f) ? v[j] : 0.f;
+          s1[j] += gg;
+          s2[j] += gg * (xf - bmu[j]) * brs[j];
+        }
+      }
+    }
+    if constexpr (STATS) {
+      // phase mean
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[r0 * BN + cc * 8 + j] = p1[j];
+      __syncthreads();
+      if (tid < BN) {
+        float t = 0.f;
+        for (int k = 0; k < EL::RPP; ++k) t += red[k * BN + tid];
+        mean_s[tid] = t / (float)nph;
+      }
+      __syncthreads();
+      float mu[8], q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mu[j] = mean_s[cc * 8 + j];
+        q[j] = 0.f;
+      }
+      for (int r = r0; r < nph; r += EL::RPP) {
+        if (!colok) break;
+        const float* cp = cs + r * EL::LDC + cc * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = cp[j] - mu[j];
+          q[j] += d * d;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red2[r0 * BN + cc * 8 + j] = q[j];
+      __syncthreads();
+      if (tid < BN) {
+        float m2 = 0.f;
+        for (int k = 0; k < EL::RPP; ++k) m2 += red2[k * BN + tid];
+        const float nb = (float)nph, mb = mean_s[tid];
+        const float n = wn_run + nb;
+        const float d = mb - wmean_run;
+        wmean_run += d * nb / n;
+        wm2_run += m2 + d * d * wn_run * nb / n;
+        wn_run = n;
+      }
+    }
+    __syncthreads();  // the next phase overwrites the staging tile
+  }
+
+  if constexpr (STATS) {
+    if (tid < BN && n0 + tid < NC) {
+      float* tile_out = args.stat_part + (long)blockIdx.x * 2 * NC;
+      if (args.fin.counters != nullptr) {   // handed to the last arriver: write-through (sc1)
+        publish_f32(tile_out + n0 + tid, wmean_run);
+        publish_f32(tile_out + NC + n0 + tid, wm2_run);
+      } else {
+        tile_out[n0 + tid] = wmean_run;     // tile mean
+        tile_out[NC + n0 + tid] = wm2_run;  // tile M2
+      }
+    }
+    const BnFwdFin& F = args.fin;
+    if (F.counters != nullptr &&
+        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
+      // Chan-combine all tiles of columns [n0, n0+BN): thread = (column, tile group)
+      constexpr int G = 256 / BN;
+      const int c = tid % BN, gq2 = tid / BN;
+      const int col = n0 + c;
+      float n = 0.f, mu = 0.f, m2 = 0.f;
+      const int T = gridDim.x;
+      if (col < NC) {   // host guarantees T <= G * FIN_UNROLL: all loads in flight at once
+        float mbv[FIN_UNROLL], qbv[FIN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          mbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + col] : 0.f;
+          qbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + NC + col] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          if (t < T) {
+            const float nb = (float)min(BM, M - t * BM);
+            const float nn = n + nb, d = mbv[u] - mu;
+            mu += d * nb / nn;
+            m2 += qbv[u] + d * d * n * nb / nn;
+            n = nn;
+          }
+        }
+      }
+      red[gq2 * BN + c] = n;
+      red2[gq2 * BN + c] = mu;
+      cs[gq2 * BN + c] = m2;                // staging tile is free now
+      __syncthreads();
+      if (gq2 == 0 && col < NC) {
+        float fn_ = red[c], fmu = red2[c], fm2 = cs[c];
+        for (int k = 1; k < G; ++k) {
+          const float nb = red[k * BN + c], mb = red2[k * BN + c], qb = cs[k * BN + c];
+          const float nn = fn_ + nb;
+          if (nn > 0.f) {
+            const float d = mb - fmu;
+            fmu += d * nb / nn;
+            fm2 += qb + d * d * fn_ * nb / nn;
+            fn_ = nn;
+          }
+        }
+        const float var = fm2 / fn_;
+        const float rs = rsqrtf(var + F.eps);
+        const float sc = F.gamma[col] * rs;
+        F.mean[col] = fmu;
+        F.rstd[col] = rs;
+        F.scale[col] = sc;
+        F.shift[col] = F.beta[col] - fmu * sc;
+        if (F.update_moving) {
+          const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
+          F.mmean[col] -= (1.f - F.momentum) * (F.mmean[col] - fmu);
+          F.mvar[col] -= (1.f - F.momentum) * (F.mvar[col] - uvar);
+        }
+      }
+      reset_counter(F.counters + blockIdx.y);
+    }
+  }
+  if constexpr (BNB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[r0 * BN + cc * 8 + j] = s1[j];
+      red2[r0 * BN + cc * 8 + j] = s2[j];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < NC) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = 0; k < EL::RPP; ++k) {
+        t1 += red[k * BN + tid];
+        t2 += red2[k * BN + tid];
+      }
+      float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
+      if (args.bfin.counters != nullptr) {
+        publish_f32(tile_out + n0 + tid, t1);
+        publish_f32(tile_out + NC + n0 + tid, t2);
+      } else {
+        tile_out[n0 + tid] = t1;        // sum g
+        tile_out[NC + n0 + tid] = t2;   // sum g * xhat
+      }
+    }
+    const BnBwdFin& F = args.bfin;
+    if (F.counters != nullptr &&
+        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
+      constexpr int G = 256 / BN;
+      const int c = tid % BN, gq2 = tid / BN;
+      const int col = n0 + c;
+      float a1 = 0.f, a2 = 0.f;
+      const int T = gridDim.x;
+      if (col < NC) {
+        float v1[FIN_UNROLL], v2[FIN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          const int t = gq2 + u * G;
+          v1[u] = t < T ? args.bnb_part[(long)t * 2 * NC + col] : 0.f;
+          v2[u] = t < T ? args.bnb_part[(long)t * 2 * NC + NC + col] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < FIN_UNROLL; ++u) {
+          a1 += v1[u];
+          a2 += v2[u];
+        }
+      }
+      red[gq2 * BN + c] = a1;
+      red2[gq2 * BN + c] = a2;
+      __syncthreads();
+      if (gq2 == 0 && col < NC) {
+        float sg = 0.f, sgx = 0.f;
+        for (int k = 0; k < G; ++k) {
+          sg += red[k * BN + c];
+          sgx += red2[k * BN + c];
+        }
+        F.dbeta[col] = sg;
+        F.dgamma[col] = sgx;
+        const float a = F.gamma[col] * F.rstd[col];
+        F.coef[col] = a;
+        F.coef[NC + col] = a * sg / (float)M;
+        F.coef[2 * NC + col] = a * sgx / (float)M;
+      }
+      reset_counter(F.counters + blockIdx.y);
+    }
+  }
+}
+
+}  // namespace dtr

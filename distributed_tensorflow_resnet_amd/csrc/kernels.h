@@ -67,6 +67,9 @@ struct GemmArgs {
 };
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
+// Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
+bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
+void set_conv_direct(int enabled);
 int conv_gemm_bm(int M, int Ncol);
 
 struct WgradArgs {

@@ -270,3 +270,63 @@ def test_dgrad_fused_bn_backward_partials(gpu, N, H, C, K, k, s):
     p = part.view(tiles, 2, C).sum(0)
     torch.testing.assert_close(p[0], sg, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(p[1], sgx, rtol=1e-4, atol=1e-3)
+
+
+@pytest.fixture
+def generic_conv():
+    """Run a block with the direct 3x3 kernel disabled, then re-enable it."""
+    nat = fn.native()
+
+    class _Ctx:
+        def __enter__(self):
+            nat.set_conv_direct(0)
+
+        def __exit__(self, *a):
+            nat.set_conv_direct(1)
+    return _Ctx()
+
+
+# Every instantiation of the direct 3x3/s1 kernel (conv_direct.hip): (C, W, BM)
+# = (16, 32, 256|64), (32, 16, 128|64), (64, 8, 64); BM follows conv_gemm_bm.
+@pytest.mark.parametrize("N,H,C", [(128, 32, 16), (8, 32, 16), (256, 16, 32), (8, 16, 32),
+                                   (16, 8, 64)])
+def test_direct_conv3x3_matches_reference_and_generic(gpu, generic_conv, N, H, C):
+    torch.manual_seed(11)
+    M = N * H * H
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(3, 3, C, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+    sc = torch.rand(C, device=gpu) + 0.5
+    sh = torch.randn(C, device=gpu) * 0.3
+    res = torch.randn(N, H, H, C, device=gpu).to(BF)
+    tiles, rows = fn.stat_tiles(M, C)
+    outs = []
+    for direct in (True, False):
+        part = torch.zeros(tiles * 2 * C, device=gpu)
+        bpart = torch.zeros(tiles * 2 * C, device=gpu)
+        mean = torch.randn(C, device=gpu) * 0.1
+        rstd = torch.rand(C, device=gpu) + 0.5
+        if direct:
+            y = fn.conv2d_fwd(x, w_ohwi, 1, pre_scale=sc, pre_shift=sh, residual=res,
+                              stat_part=part)
+            dx = fn.conv2d_dgrad(res, w, tuple(x.shape), 1, bnb=(x, mean * 0, rstd * 0 + 1, sc,
+                                                                   sh, bpart))
+        else:
+            with generic_conv:
+                y = fn.conv2d_fwd(x, w_ohwi, 1, pre_scale=sc, pre_shift=sh, residual=res,
+                                  stat_part=part)
+                dx = fn.conv2d_dgrad(res, w, tuple(x.shape), 1,
+                                     bnb=(x, mean * 0, rstd * 0 + 1, sc, sh, bpart))
+        outs.append((y, part.view(tiles, 2, C), dx, bpart.view(tiles, 2, C)))
+    a = torch.relu(x.float() * sc + sh).to(BF).float()
+    r = ref.conv2d(a, w.float(), 1) + res.float()
+    assert _rel(outs[0][0], r) < 1e-2
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2
+    torch.testing.assert_close(outs[0][1][:, 0], outs[1][1][:, 0], rtol=2e-2, atol=2e-2)
+    # dgrad: dx = conv_transpose(res, w); reference via autograd of the fp32 conv
+    xr = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
+    ref.conv2d(xr, w.float(), 1).backward(res.float())
+    assert _rel(outs[0][2], xr.grad) < 1e-2
+    assert _rel(outs[0][2], outs[1][2]) < 1e-2
+    sums_d, sums_g = outs[0][3].sum(0), outs[1][3].sum(0)
+    assert _rel(sums_d, sums_g) < 2e-2
