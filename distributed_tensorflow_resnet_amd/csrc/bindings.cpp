@@ -47,8 +47,8 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                            ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
                            ptr_t stat_part, int accumulate, std::vector<int> geom,
                            std::vector<ptr_t> bnb, std::vector<ptr_t> fin,
-                           std::vector<ptr_t> bfin, float momentum, float eps,
-                           int update_moving) {
+                           std::vector<ptr_t> bfin, std::vector<ptr_t> pfin, float momentum,
+                           float eps, int update_moving) {
   GemmArgs g{};
   g.a = P<const bf16>(a);
   g.b = P<const bf16>(b);
@@ -71,18 +71,29 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     g.bnb_shift = P<const float>(bnb[4]);
     g.bnb_part = P<float>(bnb[5]);
   }
-  if (!fin.empty()) {  // [counters, gamma, beta, mmean, mvar, mean, rstd, scale, shift]
-    if (fin.size() != 9) throw std::invalid_argument("fin needs 9 pointers");
+  if (!fin.empty()) {  // [counters, gamma, beta, mmean, mvar, mean, rstd, scale, shift, gpart,
+                       //  group, groups_only]
+    if (fin.size() != 12) throw std::invalid_argument("fin needs 12 entries");
     if (stat_part == 0) throw std::invalid_argument("fin requires stat_part");
     g.fin = BnFwdFin{P<unsigned>(fin[0]), P<const float>(fin[1]), P<const float>(fin[2]),
                      P<float>(fin[3]), P<float>(fin[4]), P<float>(fin[5]), P<float>(fin[6]),
-                     P<float>(fin[7]), P<float>(fin[8]), momentum, eps, update_moving};
+                     P<float>(fin[7]), P<float>(fin[8]), momentum, eps, update_moving,
+                     P<float>(fin[9]), (int)fin[10], (int)fin[11]};
   }
-  if (!bfin.empty()) {  // [counters, gamma, rstd, dgamma, dbeta, coef]
-    if (bfin.size() != 6) throw std::invalid_argument("bfin needs 6 pointers");
+  if (!bfin.empty()) {  // [counters, gamma, rstd, dgamma, dbeta, coef, gpart, group]
+    if (bfin.size() != 8) throw std::invalid_argument("bfin needs 8 entries");
     if (bnb.empty()) throw std::invalid_argument("bfin requires bnb");
     g.bfin = BnBwdFin{P<unsigned>(bfin[0]), P<const float>(bfin[1]), P<const float>(bfin[2]),
-                      P<float>(bfin[3]), P<float>(bfin[4]), P<float>(bfin[5])};
+                      P<float>(bfin[3]), P<float>(bfin[4]), P<float>(bfin[5]),
+                      P<float>(bfin[6]), (int)bfin[7]};
+  }
+  if (!pfin.empty()) {  // [part, cnt, rows_per, M, gamma, beta, mean, rstd, scale, shift, mmean, mvar]
+    if (pfin.size() != 12) throw std::invalid_argument("pfin needs 12 entries");
+    if (pre_scale == 0) throw std::invalid_argument("pfin requires the PRE prologue");
+    g.pfin = BnPreFin{P<const float>(pfin[0]), (int)pfin[1], (int)pfin[2], (int)pfin[3],
+                      P<const float>(pfin[4]), P<const float>(pfin[5]), P<float>(pfin[6]),
+                      P<float>(pfin[7]), P<float>(pfin[8]), P<float>(pfin[9]),
+                      P<float>(pfin[10]), P<float>(pfin[11]), momentum, eps, update_moving};
   }
   g.g = geom_from(geom);
   const ConvGeom& c = g.g;
@@ -101,6 +112,23 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   if (g.Ncol % 16) throw std::invalid_argument("conv: output channels must be a multiple of 16");
   if ((pre_scale != 0) && mode != MODE_FWD)
     throw std::invalid_argument("fused BN+ReLU prologue is forward-only");
+  if (g.pfin.cnt > 0) {
+    const int C = c.C;   // PRE is forward-only: the A channels
+    if (C > 256 || (C & (C - 1)) != 0 || g.pfin.cnt > (256 / C) * 8)
+      throw std::invalid_argument("pfin: C must be a power of two <= 256 and cnt <= 8*256/C");
+  }
+  // In-kernel finalize bounds (conv_epilogue.h combines): every level's item count
+  // must fit one round of loads, cnt <= (256 / BN) * FIN_UNROLL.
+  for (int which = 0; which < 2; ++which) {
+    const bool on = which == 0 ? g.fin.counters != nullptr : g.bfin.counters != nullptr;
+    if (!on) continue;
+    const int grp = which == 0 ? g.fin.group : g.bfin.group;
+    const int bm = conv_gemm_bm(g.M, g.Ncol), bn = conv_gemm_bn(g.M, g.Ncol);
+    const int T = (g.M + bm - 1) / bm, cap = (256 / bn) * 8;
+    const bool ok = grp == 0 ? T <= cap : (grp <= cap && (T + grp - 1) / grp <= cap);
+    if (!ok || (grp != 0 && (which == 0 ? g.fin.gpart : g.bfin.gpart) == nullptr))
+      throw std::invalid_argument("fused BN finalize: tile count exceeds the combine bound");
+  }
   return [g, mode](hipStream_t s) { conv_gemm(g, mode, s); };
 }
 
@@ -431,6 +459,7 @@ PYBIND11_MODULE(_C, m) {
 
   // host-side helpers that mirror the launchers' internal choices
   m.def("conv_gemm_bm", &conv_gemm_bm);
+  m.def("conv_gemm_bn", &conv_gemm_bn);
   m.def("set_conv_direct", &set_conv_direct,
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);

@@ -14,6 +14,7 @@
 // (counters start zeroed at allocation).
 #pragma once
 #include "common.h"
+#include "kernels.h"
 
 namespace dtr {
 
@@ -51,6 +52,76 @@ __device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned total, int*
 
 __device__ __forceinline__ void reset_counter(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer-side finalize (BnPreFin, kernels.h): all 256 threads combine the
+// producer's partials for C channels (C a power of two <= 256; thread = (channel
+// c = tid % C, slice q = tid / C), items q, q + G, ... with G = 256 / C, at most
+// FIN_UNROLL each -- one round of loads), fold the G slices in fixed order and
+// write the BN scale/shift table sc_s/sh_s (LDS).  Block (0,0) also writes the
+// global mean/rstd/scale/shift and the moving averages.  `scratch` = 768 LDS
+// floats.  Ends with a barrier (the table is ready for every thread).
+__device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float* sc_s,
+                                                float* sh_s, float* scratch) {
+  const int tid = threadIdx.x;
+  const int G = 256 / C;
+  const int c = tid % C, q = tid / C;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (q < G) {
+    float mv[FIN_UNROLL], qv[FIN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = q + u * G;
+      mv[u] = t < P.cnt ? P.part[(long)t * 2 * C + c] : 0.f;
+      qv[u] = t < P.cnt ? P.part[(long)t * 2 * C + C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = q + u * G;
+      if (t < P.cnt) {
+        const float nb = (float)min(P.rows_per, P.M - t * P.rows_per);
+        const float nn = n + nb, d = mv[u] - mu;
+        mu += d * nb / nn;
+        m2 += qv[u] + d * d * n * nb / nn;
+        n = nn;
+      }
+    }
+    scratch[tid] = n;
+    scratch[256 + tid] = mu;
+    scratch[512 + tid] = m2;
+  }
+  __syncthreads();
+  if (q == 0) {
+    float fn_ = scratch[c], fmu = scratch[256 + c], fm2 = scratch[512 + c];
+    for (int k = 1; k < G; ++k) {
+      const float nb = scratch[k * C + c], mb = scratch[256 + k * C + c];
+      const float qb = scratch[512 + k * C + c];
+      const float nn = fn_ + nb;
+      if (nn > 0.f) {
+        const float d = mb - fmu;
+        fmu += d * nb / nn;
+        fm2 += qb + d * d * fn_ * nb / nn;
+        fn_ = nn;
+      }
+    }
+    const float rs = rsqrtf(fm2 / fn_ + P.eps);
+    const float sc = P.gamma[c] * rs;
+    const float sh = P.beta[c] - fmu * sc;
+    sc_s[c] = sc;
+    sh_s[c] = sh;
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      P.mean[c] = fmu;
+      P.rstd[c] = rs;
+      P.scale[c] = sc;
+      P.shift[c] = sh;
+      if (P.update_moving) {
+        const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
+        P.mmean[c] -= (1.f - P.momentum) * (P.mmean[c] - fmu);
+        P.mvar[c] -= (1.f - P.momentum) * (P.mvar[c] - uvar);
+      }
+    }
+  }
+  __syncthreads();
 }
 
 }  // namespace dtr

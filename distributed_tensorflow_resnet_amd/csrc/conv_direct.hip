@@ -49,6 +49,8 @@ conv3x3_direct_kernel(GemmArgs args) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = reinterpret_cast<bf16*>(smem);
+  float* pre_s = reinterpret_cast<float*>(smem + HU * 16);   // PRE: [2][CA] scale, shift
+  float* fin_scratch = pre_s + 2 * CA;                        // 768 floats (BnPreFin)
 
   const ConvGeom& g = args.g;
   const int NC = args.Ncol;
@@ -81,6 +83,7 @@ conv3x3_direct_kernel(GemmArgs args) {
     }
   }
   bf16x8 hv[HPT];
+  unsigned hmask = 0;
   const bf16* abase = args.a + (long)img * HWp * CA;
 #pragma unroll
   for (int i = 0; i < HPT; ++i) {
@@ -92,10 +95,23 @@ conv3x3_direct_kernel(GemmArgs args) {
       const int h = h0 - 1 + hr, w = hc - 1;
       if (h >= 0 && h < H && w >= 0 && w < WI) {
         v = *reinterpret_cast<const bf16x8*>(abase + ((long)h * WI + w) * CA + u * 8);
-        if constexpr (PRE) v = affine_relu8(v, args.pre_scale + u * 8, args.pre_shift + u * 8);
+        if constexpr (PRE) hmask |= 1u << i;   // padding stays zero (TF pads after BN-ReLU)
       }
     }
     hv[i] = v;
+  }
+  // ---- BN scale/shift table for the fused BN+ReLU (finalized here when this is
+  //      the BN's first consumer); its loads overlap the halo loads in flight ----
+  if constexpr (PRE) {
+    if (args.pfin.cnt > 0) {
+      bn_prefin_table(args.pfin, CA, pre_s, pre_s + CA, fin_scratch);
+    } else {
+      if (tid < CA) {
+        pre_s[tid] = args.pre_scale[tid];
+        pre_s[CA + tid] = args.pre_shift[tid];
+      }
+      __syncthreads();
+    }
   }
   // ---- 2. halo -> LDS (swizzled 16-B units) ----
 #pragma unroll
@@ -104,7 +120,11 @@ conv3x3_direct_kernel(GemmArgs args) {
     if (q < HU) {
       const int u = q % U, pix = q / U;
       const int hc = pix % HW2;
-      *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = hv[i];
+      bf16x8 v = hv[i];
+      if constexpr (PRE) {
+        if ((hmask >> i) & 1u) v = affine_relu8(v, pre_s + u * 8, pre_s + CA + u * 8);
+      }
+      *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = v;
     }
   }
   __syncthreads();
@@ -150,7 +170,8 @@ conv3x3_direct_kernel(GemmArgs args) {
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_direct_cfg(const GemmArgs& a, hipStream_t s) {
   constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
-  const size_t lds = (std::max((size_t)HU * 16, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
+  constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(2 * CA + 768) * sizeof(float);
+  const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
   dim3 grid(a.M / BM, (a.Ncol + BN - 1) / BN);
   hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
                      dim3(256), lds, s, a);

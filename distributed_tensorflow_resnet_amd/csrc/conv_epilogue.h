@@ -22,6 +22,100 @@ struct EpiLayout {
   static constexpr size_t BYTES = (size_t)(TILE + RED) * sizeof(float);
 };
 
+// Last-arriver combines (bn_fused.h protocol).  Thread (c = tid % BN, q = tid / BN)
+// loads items q, q + G, ... (G = 256 / BN; the host keeps cnt <= G * FIN_UNROLL so
+// every load is in flight at once), folds them, then thread q == 0 of each column
+// folds the G partial results from LDS in fixed order -> deterministic.  Results
+// are valid in threads tid < BN (column n0 + tid).
+//   welford_combine: items are (mean, M2) pairs at src[i * 2NC + col] / [+ NC]; item
+//                    i of the range holds min(rows_per, rows_left - i * rows_per) rows.
+//   sum_combine:     items are (sum1, sum2) pairs, added.
+template <int BN>
+__device__ __forceinline__ void welford_combine(const float* src, int NC, int n0, int first,
+                                                int cnt, int rows_per, int rows_left,
+                                                float* red, float* red2, float* red3,
+                                                float& out_n, float& out_mu, float& out_m2) {
+  constexpr int G = 256 / BN;
+  const int tid = threadIdx.x, c = tid % BN, q = tid / BN, col = n0 + c;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (col < NC) {
+    float mv[FIN_UNROLL], qv[FIN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = q + u * G;
+      const long o = (long)(first + t) * 2 * NC + col;
+      mv[u] = t < cnt ? src[o] : 0.f;
+      qv[u] = t < cnt ? src[o + NC] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = q + u * G;
+      if (t < cnt) {
+        const float nb = (float)min(rows_per, rows_left - t * rows_per);
+        const float nn = n + nb, d = mv[u] - mu;
+        mu += d * nb / nn;
+        m2 += qv[u] + d * d * n * nb / nn;
+        n = nn;
+      }
+    }
+  }
+  red[q * BN + c] = n;
+  red2[q * BN + c] = mu;
+  red3[q * BN + c] = m2;
+  __syncthreads();
+  if (q == 0 && col < NC) {
+    float fn_ = red[c], fmu = red2[c], fm2 = red3[c];
+    for (int k = 1; k < G; ++k) {
+      const float nb = red[k * BN + c], mb = red2[k * BN + c], qb = red3[k * BN + c];
+      const float nn = fn_ + nb;
+      if (nn > 0.f) {
+        const float d = mb - fmu;
+        fmu += d * nb / nn;
+        fm2 += qb + d * d * fn_ * nb / nn;
+        fn_ = nn;
+      }
+    }
+    out_n = fn_;
+    out_mu = fmu;
+    out_m2 = fm2;
+  }
+}
+
+template <int BN>
+__device__ __forceinline__ void sum_combine(const float* src, int NC, int n0, int first, int cnt,
+                                            float* red, float* red2, float& o1, float& o2) {
+  constexpr int G = 256 / BN;
+  const int tid = threadIdx.x, c = tid % BN, q = tid / BN, col = n0 + c;
+  float a1 = 0.f, a2 = 0.f;
+  if (col < NC) {
+    float v1[FIN_UNROLL], v2[FIN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = q + u * G;
+      const long o = (long)(first + t) * 2 * NC + col;
+      v1[u] = t < cnt ? src[o] : 0.f;
+      v2[u] = t < cnt ? src[o + NC] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      a1 += v1[u];
+      a2 += v2[u];
+    }
+  }
+  red[q * BN + c] = a1;
+  red2[q * BN + c] = a2;
+  __syncthreads();
+  if (q == 0 && col < NC) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < G; ++k) {
+      s1 += red[k * BN + c];
+      s2 += red2[k * BN + c];
+    }
+    o1 = s1;
+    o2 = s2;
+  }
+}
+
 // Shared epilogue of every conv kernel (implicit-GEMM and direct): the wave
 // fragments acc[MR][NR] of the BM x BN tile at (m0, n0) -> LDS-staged 16-byte
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN
@@ -206,64 +300,54 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     const BnFwdFin& F = args.fin;
-    if (F.counters != nullptr &&
-        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
-      // Chan-combine all tiles of columns [n0, n0+BN): thread = (column, tile group)
-      constexpr int G = 256 / BN;
-      const int c = tid % BN, gq2 = tid / BN;
-      const int col = n0 + c;
-      float n = 0.f, mu = 0.f, m2 = 0.f;
+    if (F.counters != nullptr) {
+      int* flag = reinterpret_cast<int*>(mean_s);
       const int T = gridDim.x;
-      if (col < NC) {   // host guarantees T <= G * FIN_UNROLL: all loads in flight at once
-        float mbv[FIN_UNROLL], qbv[FIN_UNROLL];
-#pragma unroll
-        for (int u = 0; u < FIN_UNROLL; ++u) {
-          const int t = gq2 + u * G;
-          mbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + col] : 0.f;
-          qbv[u] = t < T ? args.stat_part[(long)t * 2 * NC + NC + col] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < FIN_UNROLL; ++u) {
-          const int t = gq2 + u * G;
-          if (t < T) {
-            const float nb = (float)min(BM, M - t * BM);
-            const float nn = n + nb, d = mbv[u] - mu;
-            mu += d * nb / nn;
-            m2 += qbv[u] + d * d * n * nb / nn;
-            n = nn;
+      bool last;
+      float fn_ = 0.f, fmu = 0.f, fm2 = 0.f;
+      if (F.group == 0) {          // single level: combine every tile
+        last = last_arriver(F.counters + blockIdx.y, T, flag);
+        if (last) welford_combine<BN>(args.stat_part, NC, n0, 0, T, BM, M, red, red2, cs,
+                                      fn_, fmu, fm2);
+      } else {                     // two levels: groups of F.group tiles, then the groups
+        const int GS = F.group, ng = (T + GS - 1) / GS, gi = blockIdx.x / GS;
+        const int gsize = min(GS, T - gi * GS);
+        last = last_arriver(F.counters + gridDim.y + blockIdx.y * ng + gi, gsize, flag);
+        if (last) {
+          welford_combine<BN>(args.stat_part, NC, n0, gi * GS, gsize, BM, M - gi * GS * BM,
+                              red, red2, cs, fn_, fmu, fm2);
+          if (tid < BN && n0 + tid < NC) {
+            publish_f32(F.gpart + (long)gi * 2 * NC + n0 + tid, fmu);
+            publish_f32(F.gpart + (long)gi * 2 * NC + NC + n0 + tid, fm2);
+          }
+          reset_counter(F.counters + gridDim.y + blockIdx.y * ng + gi);
+          if (F.groups_only) {
+            last = false;   // a consumer's BnPreFin combines the group partials
+          } else {
+            last = last_arriver(F.counters + blockIdx.y, ng, flag);
+            if (last) welford_combine<BN>(F.gpart, NC, n0, 0, ng, GS * BM, M, red, red2, cs,
+                                          fn_, fmu, fm2);
           }
         }
       }
-      red[gq2 * BN + c] = n;
-      red2[gq2 * BN + c] = mu;
-      cs[gq2 * BN + c] = m2;                // staging tile is free now
-      __syncthreads();
-      if (gq2 == 0 && col < NC) {
-        float fn_ = red[c], fmu = red2[c], fm2 = cs[c];
-        for (int k = 1; k < G; ++k) {
-          const float nb = red[k * BN + c], mb = red2[k * BN + c], qb = cs[k * BN + c];
-          const float nn = fn_ + nb;
-          if (nn > 0.f) {
-            const float d = mb - fmu;
-            fmu += d * nb / nn;
-            fm2 += qb + d * d * fn_ * nb / nn;
-            fn_ = nn;
+      if (last) {
+        const int col = n0 + tid;
+        if (tid < BN && col < NC) {
+          const float var = fm2 / fn_;
+          const float rs = rsqrtf(var + F.eps);
+          const float sc = F.gamma[col] * rs;
+          F.mean[col] = fmu;
+          F.rstd[col] = rs;
+          F.scale[col] = sc;
+          F.shift[col] = F.beta[col] - fmu * sc;
+          if (F.update_moving) {
+            const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
+            F.mmean[col] -= (1.f - F.momentum) * (F.mmean[col] - fmu);
+            F.mvar[col] -= (1.f - F.momentum) * (F.mvar[col] - uvar);
           }
         }
-        const float var = fm2 / fn_;
-        const float rs = rsqrtf(var + F.eps);
-        const float sc = F.gamma[col] * rs;
-        F.mean[col] = fmu;
-        F.rstd[col] = rs;
-        F.scale[col] = sc;
-        F.shift[col] = F.beta[col] - fmu * sc;
-        if (F.update_moving) {
-          const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
-          F.mmean[col] -= (1.f - F.momentum) * (F.mmean[col] - fmu);
-          F.mvar[col] -= (1.f - F.momentum) * (F.mvar[col] - uvar);
-        }
+        reset_counter(F.counters + blockIdx.y);
       }
-      reset_counter(F.counters + blockIdx.y);
     }
   }
   if constexpr (BNB) {
@@ -289,44 +373,41 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     const BnBwdFin& F = args.bfin;
-    if (F.counters != nullptr &&
-        last_arriver(F.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(mean_s))) {
-      constexpr int G = 256 / BN;
-      const int c = tid % BN, gq2 = tid / BN;
-      const int col = n0 + c;
-      float a1 = 0.f, a2 = 0.f;
+    if (F.counters != nullptr) {
+      int* flag = reinterpret_cast<int*>(mean_s);
       const int T = gridDim.x;
-      if (col < NC) {
-        float v1[FIN_UNROLL], v2[FIN_UNROLL];
-#pragma unroll
-        for (int u = 0; u < FIN_UNROLL; ++u) {
-          const int t = gq2 + u * G;
-          v1[u] = t < T ? args.bnb_part[(long)t * 2 * NC + col] : 0.f;
-          v2[u] = t < T ? args.bnb_part[(long)t * 2 * NC + NC + col] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < FIN_UNROLL; ++u) {
-          a1 += v1[u];
-          a2 += v2[u];
+      bool last;
+      float sg = 0.f, sgx = 0.f;
+      if (F.group == 0) {
+        last = last_arriver(F.counters + blockIdx.y, T, flag);
+        if (last) sum_combine<BN>(args.bnb_part, NC, n0, 0, T, red, red2, sg, sgx);
+      } else {
+        const int GS = F.group, ng = (T + GS - 1) / GS, gi = blockIdx.x / GS;
+        const int gsize = min(GS, T - gi * GS);
+        last = last_arriver(F.counters + gridDim.y + blockIdx.y * ng + gi, gsize, flag);
+        if (last) {
+          sum_combine<BN>(args.bnb_part, NC, n0, gi * GS, gsize, red, red2, sg, sgx);
+          if (tid < BN && n0 + tid < NC) {
+            publish_f32(F.gpart + (long)gi * 2 * NC + n0 + tid, sg);
+            publish_f32(F.gpart + (long)gi * 2 * NC + NC + n0 + tid, sgx);
+          }
+          reset_counter(F.counters + gridDim.y + blockIdx.y * ng + gi);
+          last = last_arriver(F.counters + blockIdx.y, ng, flag);
+          if (last) sum_combine<BN>(F.gpart, NC, n0, 0, ng, red, red2, sg, sgx);
         }
       }
-      red[gq2 * BN + c] = a1;
-      red2[gq2 * BN + c] = a2;
-      __syncthreads();
-      if (gq2 == 0 && col < NC) {
-        float sg = 0.f, sgx = 0.f;
-        for (int k = 0; k < G; ++k) {
-          sg += red[k * BN + c];
-          sgx += red2[k * BN + c];
+      if (last) {
+        const int col = n0 + tid;
+        if (tid < BN && col < NC) {
+          F.dbeta[col] = sg;
+          F.dgamma[col] = sgx;
+          const float a = F.gamma[col] * F.rstd[col];
+          F.coef[col] = a;
+          F.coef[NC + col] = a * sg / (float)M;
+          F.coef[2 * NC + col] = a * sgx / (float)M;
         }
-        F.dbeta[col] = sg;
-        F.dgamma[col] = sgx;
-        const float a = F.gamma[col] * F.rstd[col];
-        F.coef[col] = a;
-        F.coef[NC + col] = a * sg / (float)M;
-        F.coef[2 * NC + col] = a * sgx / (float)M;
+        reset_counter(F.counters + blockIdx.y);
       }
-      reset_counter(F.counters + blockIdx.y);
     }
   }
 }

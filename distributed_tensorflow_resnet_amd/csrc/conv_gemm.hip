@@ -64,12 +64,6 @@ conv_gemm_kernel(GemmArgs args) {
   // Input-channel count of the A operand's gather (C for fwd, K for dgrad).
   const int Acin = (MODE == MODE_FWD) ? g.C : g.K;
 
-  if constexpr (PRE) {
-    for (int i = tid; i < Acin; i += 256) {
-      pre_s[i] = args.pre_scale[i];
-      pre_s[Acin + i] = args.pre_shift[i];
-    }
-  }
 
   // ---- per-thread loader state (row decomposition is K-invariant) ----
   const int kg = tid & 7;  // fixed 16-B k-group of every chunk this thread stages
@@ -104,7 +98,9 @@ conv_gemm_kernel(GemmArgs args) {
   bf16x8 ra[A_PER_T], rb[B_PER_T];
   const bf16x8 zero8 = {};
 
+  unsigned amask = 0;   // PRE: which A chunks of the in-flight tile are real pixels
   auto load_tile = [&](int t) {
+    if constexpr (PRE) amask = 0;
     const int k = t * BK + kg * 8;
     const bool kvalid = k < KD;
     const int tap = kvalid ? k / Acin : 0;
@@ -118,7 +114,7 @@ conv_gemm_kernel(GemmArgs args) {
         if (kvalid && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
           const long off = ((long)(a_base[i] + hi * g.W + wi)) * g.C + ci;
           v = *reinterpret_cast<const bf16x8*>(args.a + off);
-          if constexpr (PRE) v = affine_relu8(v, pre_s + ci, pre_s + Acin + ci);
+          if constexpr (PRE) amask |= 1u << i;   // BN+ReLU applied at LDS store time
         }
       } else {
         int hp = a_h[i] - rr, wp = a_w[i] - cc;
@@ -153,15 +149,26 @@ conv_gemm_kernel(GemmArgs args) {
     }
   };
 
-  auto store_tile = [&](int buf) {
+  // PRE is applied here, after the MFMAs of the previous tile, so the prefetched
+  // loads stay in flight across them (applying it in load_tile forced the wait).
+  auto store_tile = [&](int buf, int t) {
     bf16* A = As + buf * BM * BK;
     bf16* B = Bs + buf * BN * BK;
+    int ci = 0;
+    if constexpr (PRE) {
+      const int k = t * BK + kg * 8;
+      ci = k - (k / Acin) * Acin;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int q = tid + i * 256;
       if (q < A_CHUNKS) {
         const int r = q >> 3;
-        *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = ra[i];
+        bf16x8 v = ra[i];
+        if constexpr (PRE) {
+          if ((amask >> i) & 1u) v = affine_relu8(v, pre_s + ci, pre_s + Acin + ci);
+        }
+        *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
       }
     }
 #pragma unroll
@@ -180,10 +187,20 @@ conv_gemm_kernel(GemmArgs args) {
 #pragma unroll
     for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (PRE) __syncthreads();
   const int KT = (KD + BK - 1) / BK;
   load_tile(0);
-  store_tile(0);
+  if constexpr (PRE) {   // BN scale/shift table (finalized here if this is the first consumer)
+    if (args.pfin.cnt > 0) {
+      bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
+    } else {
+      for (int i = tid; i < Acin; i += 256) {
+        pre_s[i] = args.pre_scale[i];
+        pre_s[Acin + i] = args.pre_shift[i];
+      }
+      __syncthreads();
+    }
+  }
+  store_tile(0, 0);
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -210,7 +227,7 @@ conv_gemm_kernel(GemmArgs args) {
 #pragma unroll
         for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
-    if (t + 1 < KT) store_tile((t + 1) & 1);
+    if (t + 1 < KT) store_tile((t + 1) & 1, t + 1);
     __syncthreads();
   }
 
@@ -256,6 +273,13 @@ int conv_gemm_bm(int M, int nc) {
   if (nc <= 32) return m >= 128L * 512 ? 128 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
   return (m >= 128L * 128 && nc % 128 == 0) ? 128 : 64;
+}
+
+int conv_gemm_bn(int M, int nc) {
+  if (nc <= 16) return 16;
+  if (nc <= 32) return 32;
+  if (nc <= 64) return 64;
+  return conv_gemm_bm(M, nc) == 128 ? 128 : 64;
 }
 
 template <int MODE>

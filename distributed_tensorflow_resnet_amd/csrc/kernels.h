@@ -20,7 +20,8 @@ struct ConvGeom {
 
 // Fused BatchNorm finalize in the producing kernel (last-arriver; see bn_fused.h).
 struct BnFwdFin {            // forward statistics -> mean/rstd/scale/shift + moving averages
-  unsigned* counters;        // one per column tile; nullptr = disabled
+  unsigned* counters;        // [col tiles] level-2 (or only) + [col tiles][groups] level-1;
+                             // nullptr = disabled
   const float* gamma;
   const float* beta;
   float* mmean;
@@ -31,6 +32,30 @@ struct BnFwdFin {            // forward statistics -> mean/rstd/scale/shift + mo
   float* shift;
   float momentum, eps;
   int update_moving;
+  float* gpart;              // two-level: [groups][2][NC] group partials (mean, M2)
+  int group;                 // tiles per level-1 group; 0 = single level
+  int groups_only;           // 1: stop after level 1 (a consumer's BnPreFin combines gpart)
+};
+// Consumer-side BN finalize: the FIRST kernel that applies a BN (the next conv's
+// fused BN+ReLU prologue) combines the producer's (mean, M2) partials itself --
+// every workgroup redundantly into its LDS scale/shift table, block (0,0) also
+// writing mean/rstd/scale/shift and the moving averages for later consumers --
+// so no separate finalize launch sits between producer and consumer.
+struct BnPreFin {
+  const float* part;         // [cnt][2][C] (mean, M2); cnt == 0 -> disabled
+  int cnt;
+  int rows_per;              // rows per partial (the last one holds the remainder)
+  int M;                     // rows in total
+  const float* gamma;
+  const float* beta;
+  float* mean;
+  float* rstd;
+  float* scale;
+  float* shift;
+  float* mmean;
+  float* mvar;
+  float momentum, eps;
+  int update_moving;
 };
 struct BnBwdFin {            // backward sums -> dgamma/dbeta/apply coefficients
   unsigned* counters;        // nullptr = disabled
@@ -39,6 +64,8 @@ struct BnBwdFin {            // backward sums -> dgamma/dbeta/apply coefficients
   float* dgamma;
   float* dbeta;
   float* coef;               // [3][C]
+  float* gpart;              // two-level: [groups][2][NC] group sums
+  int group;                 // tiles per level-1 group; 0 = single level
 };
 
 struct GemmArgs {
@@ -61,6 +88,7 @@ struct GemmArgs {
   float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
   BnFwdFin fin;             // with stat_part: finalize in-kernel
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
+  BnPreFin pfin;            // with pre_scale: finalize the PRE BatchNorm in the prologue
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;
@@ -71,6 +99,7 @@ void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 void set_conv_direct(int enabled);
 int conv_gemm_bm(int M, int Ncol);
+int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 
 struct WgradArgs {
   const bf16* dy;           // [N,Ho,Wo,K]

@@ -75,8 +75,15 @@ def stat_tiles(M: int, ncol: int) -> tuple[int, int]:
 
 
 def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residual=None,
-               stat_part=None, bias=None, out=None, out_f32: bool = False, accumulate=False):
-    """y = conv(relu(x*pre_scale+pre_shift) if pre else x, W) [+bias] [+residual]."""
+               stat_part=None, bias=None, out=None, out_f32: bool = False, accumulate=False,
+               fin=None, pfin=None):
+    """y = conv(relu(x*pre_scale+pre_shift) if pre else x, W) [+bias] [+residual].
+
+    ``fin=[counters, gamma, beta, mmean, mvar, mean, rstd, scale, shift, gpart, group,
+    groups_only]`` (tensors or ints) finalizes the output's BN statistics inside the
+    kernel (last arriver); ``pfin=[part, cnt, rows_per, M, gamma, beta, mean, rstd,
+    scale, shift, mmean, mvar]`` finalizes the PRE BatchNorm in the prologue (the
+    kernel is that BN's first consumer; pre_scale/pre_shift are then outputs)."""
     _check(x, BF16, 4, "x")
     _check(w_ohwi, BF16, 4, "w_ohwi")
     N, H, W, C = x.shape
@@ -102,11 +109,16 @@ def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residu
                        0 if out_f32 else out.data_ptr(), out.data_ptr() if out_f32 else 0,
                        _ptr(residual), _ptr(pre_scale), _ptr(pre_shift), _ptr(bias),
                        0 if bias is None else bias.numel(), _ptr(stat_part), int(accumulate),
-                       g.as_list(), [], [], [], 0.997, 1e-5, 1, _stream())
+                       g.as_list(), [], _ptrs(fin), [], _ptrs(pfin), 0.997, 1e-5, 1, _stream())
     return out
 
 
-def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False, bnb=None):
+def _ptrs(lst):
+    return [] if lst is None else [t.data_ptr() if torch.is_tensor(t) else int(t) for t in lst]
+
+
+def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False, bnb=None,
+                 bfin=None):
     """dx = conv2d_transpose(dy, W) with TF fixed padding; w_hwio [kh][kw][C][K].
 
     ``bnb=(x, mean, rstd, scale, shift, part)`` additionally emits the
@@ -122,7 +134,8 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
         out = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
     bl = [] if bnb is None else [t.data_ptr() for t in bnb]
     native().conv_gemm(1, dy.data_ptr(), w_hwio.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                       int(accumulate), g.as_list(), bl, [], [], 0.997, 1e-5, 1, _stream())
+                       int(accumulate), g.as_list(), bl, [], _ptrs(bfin), [], 0.997, 1e-5, 1,
+                       _stream())
     return out
 
 

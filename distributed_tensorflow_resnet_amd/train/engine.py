@@ -42,6 +42,8 @@ from ..parallel.buckets import assign_buckets, schedule_buckets
 
 BF16 = torch.bfloat16
 BN_DECAY = 0.997
+# Diagnostics: DTR_DIAG_SKIP=wgrad,dgrad,... drops those launches (wrong math; timing only)
+_DIAG_SKIP = set(filter(None, os.environ.get("DTR_DIAG_SKIP", "").split(",")))
 BN_EPS = 1e-5
 
 WGD_DTYPE = np.dtype([
@@ -110,9 +112,11 @@ class _BN:
     rstd: torch.Tensor = None
     scale: torch.Tensor = None
     shift: torch.Tensor = None
-    # stat source of the forward partials: (tiles, tile_rows, M)
-    src: tuple = None
+    # forward statistics not yet finalized: (partials ptr, count, rows per partial, M)
+    pending: tuple = None
     names: tuple = ()
+    part: torch.Tensor = None     # this BN's forward tile partials [T][2][C]
+    gpart: torch.Tensor = None    # level-1 group partials [groups][2][C]
 
 
 @dataclass
@@ -133,7 +137,7 @@ class Engine:
                  lr_schedule: LRSchedule, optimizer: str = "mom", momentum: float = 0.9,
                  device=None, dist_ctx=None, bucket_mb: float = 25.0, seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
-                 use_graph: bool = True, data_seed: int = 1234, fork_wgrad: bool | None = None):
+                 use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None):
         self.nat = native(required=True)
         self.spec = spec
         self.N = batch_size
@@ -151,6 +155,7 @@ class Engine:
             # measured: eager + forked wgrad stream beats hipGraph replay (which
             # handles the cross-stream event edges poorly); graphs stay single-stream
             fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
+        self.fork_every = max(1, int(os.environ.get("DTR_FORK_EVERY", "2")))
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
             input_mode = "cifar_u8" if spec.dataset.startswith("cifar") else "nhwc"
@@ -252,8 +257,11 @@ class Engine:
         bn_specs = [b for blk in spec.blocks for b in blk.bns] + [spec.final_bn]
         total_c = sum(b.channels for b in bn_specs)
         self.bnbuf = torch.zeros(4 * total_c, device=self.device)
-        # last-arriver counters for in-kernel BN finalize: per BN 2 x 128 column tiles
-        self.bn_counters = torch.zeros(len(bn_specs) * 256, dtype=torch.int32, device=self.device)
+        # last-arriver counters for the in-kernel BN finalize (bump-allocated per fused
+        # launch at plan build; the kernels leave them zeroed) + group-partial scratch
+        self.bn_counters = torch.zeros(1 << 18, dtype=torch.int32, device=self.device)
+        self._cnt_next = 0
+        self.bn_gpart = torch.empty(2, 128 * 2 * 2048, device=self.device)
         off = 0
         for b in bn_specs:
             g = ps.slot(f"{b.name}/gamma")
@@ -268,8 +276,6 @@ class Engine:
             e.rstd = self.bnbuf[total_c + off:total_c + off + C]
             e.scale = self.bnbuf[2 * total_c + off:2 * total_c + off + C]
             e.shift = self.bnbuf[3 * total_c + off:3 * total_c + off + C]
-            e.cnt_fwd = self.bn_counters.data_ptr() + 4 * (256 * len(self.bns))
-            e.cnt_bwd = e.cnt_fwd + 4 * 128
             e.fused_fwd = e.fused_bwd = False
             off += C
             self.bns[b.name] = e
@@ -326,6 +332,14 @@ class Engine:
             max_bwd = max(max_bwd, tl * 2 * C)
         self.stat_part = torch.empty(max_stat, device=dev)
         self.bwd_part = torch.empty(max_bwd, device=dev)
+        # per-BN forward partials: the BN's first consumer may combine them (BnPreFin)
+        # while the same kernel produces the next BN's partials, so no sharing
+        for b in self.bns.values():
+            C = b.spec.channels
+            M = N * b.spec.h * b.spec.w
+            bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
+            b.part = torch.empty(_ceil(M, bm) * 2 * C, device=dev)
+            b.gpart = torch.empty(max(_ceil(M, bm) // 2, 1) * 2 * C, device=dev)
         max_c = max(b.spec.channels for b in self.bns.values())
         self.coef = torch.empty(3 * max_c, device=dev)
         # per-conv split-K partial slabs (persist until the bucket's grouped reduce)
@@ -349,41 +363,106 @@ class Engine:
     def _dense_geom(self, N):
         return [N, 1, 1, self.spec.dense_in, 1, 1, self.kpad, 1, 1, 1, 0]
 
-    def _fuse_finalize(self, M: int, nc: int) -> bool:
-        """In-kernel (last-arriver) BN finalize pays when the combine is one round
-        trip: <= FIN_UNROLL (8) partial tiles per combining thread."""
+    def _fuse_finalize(self, M: int, nc: int):
+        """Plan for the in-kernel (last-arriver) BN finalize of a conv producing M x nc:
+        None (separate finalize kernel), 0 (one level: every tile partial combined by the
+        last workgroup) or GS (two levels: groups of GS tiles, then the groups).  Each
+        level must be one round of loads: items <= (256 / BN) * FIN_UNROLL(8)."""
         if os.environ.get("DTR_FUSED_BN_FINALIZE", "1") == "0":
-            return False
-        bm = self.nat.conv_gemm_bm(M, nc)
-        bn = 16 if nc <= 16 else 32 if nc <= 32 else 64 if nc <= 64 else (128 if bm == 128 else 64)
-        return _ceil(_ceil(M, bm), 256 // bn) <= 8 and _ceil(nc, bn) <= 128
+            return None
+        bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
+        T, cap = _ceil(M, bm), (256 // bn) * 8
+        if T <= cap:
+            return 0
+        gs = 16
+        if gs <= cap and _ceil(T, gs) <= cap:
+            return gs
+        return None
+
+    def _counters(self, M: int, nc: int, group: int) -> int:
+        """Device address of a fresh zeroed counter block for one fused launch."""
+        bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
+        ny = _ceil(nc, bn)
+        n = ny * (1 + (_ceil(_ceil(M, bm), group) if group else 0))
+        off = self._cnt_next
+        self._cnt_next += _ceil(n, 16) * 16
+        assert self._cnt_next <= self.bn_counters.numel(), "BN counter pool exhausted"
+        return self.bn_counters.data_ptr() + 4 * off
+
+    @staticmethod
+    def _consumer_cap(C: int) -> int:
+        """Max partials a consumer prologue combines in one round (bn_prefin_table)."""
+        return (256 // C) * 8 if C <= 256 and C & (C - 1) == 0 else 0
 
     def _conv_fwd(self, plan, c: _Conv, x, out, N, pre: _BN | None = None, residual=None,
                   stats_for: _BN | None = None):
+        """One conv launch.  BatchNorm statistics of the output (``stats_for``) are
+        finalized, in order of preference, by (a) the BN's first consumer's prologue
+        reading the tile partials (few tiles), (b) the same after this kernel's
+        last-arriving workgroups folded groups of tiles, (c) this kernel's last
+        arriver (full), (d) a separate bn_finalize launch."""
         geom = self._geom(c, N)
         stat_ptr = 0
-        fin = []
+        fin, pfin = [], []
+        if pre is not None and pre.pending is not None:
+            part, cnt, rows, M0 = pre.pending
+            pfin = [part, cnt, rows, M0, pre.gamma, pre.beta, pre.mean.data_ptr(),
+                    pre.rstd.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
+                    pre.mmean, pre.mvar]
+            pre.pending = None
         if stats_for is not None:
-            M = N * c.spec.ho * c.spec.wo
-            bm = self.nat.conv_gemm_bm(M, c.spec.cout)
-            stats_for.src = (_ceil(M, bm), bm, M)
-            stat_ptr = self.stat_part.data_ptr()
-            if self._fuse_finalize(M, c.spec.cout):
-                b = stats_for
-                b.fused_fwd = True
-                fin = [b.cnt_fwd, b.gamma, b.beta, b.mmean, b.mvar, b.mean.data_ptr(),
-                       b.rstd.data_ptr(), b.scale.data_ptr(), b.shift.data_ptr()]
+            b = stats_for
+            M, nc = N * c.spec.ho * c.spec.wo, c.spec.cout
+            bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
+            T = _ceil(M, bm)
+            stat_ptr = b.part.data_ptr()
+            b.pending, b.fused_fwd = (stat_ptr, T, bm, M), False
+            capc, capp = self._consumer_cap(nc), (256 // bn) * 8
+            mode = os.environ.get("DTR_FUSED_BN_FINALIZE", "1")
+            if mode == "0":
+                b.pending = ("separate", stat_ptr, T, bm, M)
+            elif T <= capc:
+                pass                                    # (a)
+            elif capc and mode != "2":
+                gs = 2
+                while _ceil(T, gs) > capc:
+                    gs *= 2
+                if gs <= capp:                          # (b)
+                    fin = [self._counters(M, nc, gs), b.gamma, b.beta, b.mmean, b.mvar,
+                           b.mean.data_ptr(), b.rstd.data_ptr(), b.scale.data_ptr(),
+                           b.shift.data_ptr(), b.gpart.data_ptr(), gs, 1]
+                    b.pending = (b.gpart.data_ptr(), _ceil(T, gs), gs * bm, M)
+                else:
+                    b.pending = ("separate", stat_ptr, T, bm, M)
+            else:
+                grp = self._fuse_finalize(M, nc)
+                if grp is not None:                     # (c)
+                    b.fused_fwd, b.pending = True, None
+                    fin = [self._counters(M, nc, grp), b.gamma, b.beta, b.mmean, b.mvar,
+                           b.mean.data_ptr(), b.rstd.data_ptr(), b.scale.data_ptr(),
+                           b.shift.data_ptr(), self.bn_gpart[0].data_ptr(), grp, 0]
+                else:
+                    b.pending = ("separate", stat_ptr, T, bm, M)
         plan.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                        0 if residual is None else residual.data_ptr(),
                        0 if pre is None else pre.scale.data_ptr(),
-                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [], fin, [],
-                       BN_DECAY, BN_EPS, 1)
+                       0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [],
+                       fin, [], pfin, BN_DECAY, BN_EPS, 1)
 
-    def _bn_finalize(self, plan, bn: _BN, train=True):
-        if bn.fused_fwd:
-            return  # finalized by the producing conv's last workgroup
-        tiles, rows, M = bn.src
-        plan.bn_finalize(self.stat_part.data_ptr(), tiles, rows, M, bn.spec.channels, bn.gamma,
+    def _bn_finalize(self, plan, bn: _BN, train=True, consumer_conv: bool = True):
+        """Called where the BN's statistics are next needed.  Deferred to the first
+        consumer conv when that conv can combine the partials itself (BnPreFin);
+        otherwise (or for a non-conv consumer) one bn_finalize launch (case (d))."""
+        if bn.pending is None:
+            return
+        if bn.pending[0] == "separate":
+            _, part, tiles, rows, M = bn.pending
+        elif consumer_conv:
+            return
+        else:
+            part, tiles, rows, M = bn.pending
+        bn.pending = None
+        plan.bn_finalize(part, tiles, rows, M, bn.spec.channels, bn.gamma,
                          bn.beta, bn.mmean, bn.mvar, BN_DECAY, BN_EPS, int(train),
                          bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
                          bn.shift.data_ptr())
@@ -402,17 +481,19 @@ class Engine:
         geom = self._geom(c, N)
         off, sp, pps = self.wg_off[c.spec.name]
         part = self.wg_part.data_ptr() + 4 * off
-        # fork: the weight gradient only feeds the bucket's grouped reduce, so it
-        # runs on the side stream, overlapping the dgrad -> BN-backward chain.
+        # The weight gradient only feeds the bucket's grouped reduce, so it runs on
+        # the side stream, overlapping the dgrad -> BN-backward chain.  Forks are
+        # batched per residual block (_flush_side): a cross-stream event pair costs
+        # ~6 us of device time on ROCm, about a third of a CIFAR wgrad.
+        def emit(plan=plan, dy=dy, x=x, pre=pre, part=part, geom=geom, sp=sp, pps=pps):
+            if "wgrad" not in _DIAG_SKIP:   # diagnostics only (scripts/diag_step.py)
+                plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
+                                0 if pre is None else pre.scale.data_ptr(),
+                                0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
         if self.fork_wgrad:
-            ev = plan.new_event()
-            plan.record(ev)
-            plan.use_stream(1)
-            plan.wait(ev)
-        plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
-                        0 if pre is None else pre.scale.data_ptr(),
-                        0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
-        plan.use_stream(0)
+            self._side_q.append(emit)
+        else:
+            emit()
         s = c.spec
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         self._produced.add(c.name)
@@ -424,12 +505,18 @@ class Engine:
                       bn.shift.data_ptr(), self.bwd_part.data_ptr()]
                 Mx = N * s.h * s.w
                 self._bnb_tiles = _ceil(Mx, self.nat.conv_gemm_bm(Mx, c.cin))
-                if self._fuse_finalize(Mx, c.cin):
+                grp = self._fuse_finalize(Mx, c.cin)
+                bmode = os.environ.get("DTR_FUSED_BN_BWD", "1")
+                if bmode == "0" or (bmode == "1" and grp):
+                    grp = None          # 1: single-level last arriver only
+                if grp is not None:
                     bn.fused_bwd = True
-                    bfl = [bn.cnt_bwd, bn.gamma, bn.rstd.data_ptr(), bn.dgamma, bn.dbeta,
-                           self.coef.data_ptr()]
-            plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                           int(accumulate), geom, bl, [], bfl, BN_DECAY, BN_EPS, 1)
+                    bfl = [self._counters(Mx, c.cin, grp), bn.gamma, bn.rstd.data_ptr(),
+                           bn.dgamma, bn.dbeta, self.coef.data_ptr(),
+                           self.bn_gpart[1].data_ptr(), grp]
+            if "dgrad" not in _DIAG_SKIP:
+                plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
+                               int(accumulate), geom, bl, [], bfl, [], BN_DECAY, BN_EPS, 1)
 
     def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None, reduced: bool = False):
         """BN+ReLU backward.  ``reduced``: the producing dgrad already wrote the
@@ -451,6 +538,23 @@ class Engine:
                           bn.scale.data_ptr(), bn.shift.data_ptr(), self.coef.data_ptr(),
                           0 if add is None else add.data_ptr(), dx.data_ptr(), M, C)
 
+    def _flush_side(self, plan, force: bool = False):
+        """Fork: emit the queued weight gradients on the side stream behind ONE event
+        (every `fork_every` residual blocks, or now if `force`)."""
+        if not self._side_q:
+            return
+        self._side_blocks += 1
+        if not force and self._side_blocks < self.fork_every:
+            return
+        ev = plan.new_event()
+        plan.record(ev)
+        plan.use_stream(1)
+        plan.wait(ev)
+        for emit in self._side_q:
+            emit()
+        plan.use_stream(0)
+        self._side_q, self._side_blocks = [], 0
+
     def _flush_buckets(self, plan, force: bool = False):
         """Emit one grouped split-K reduce for every bucket whose gradients are
         all produced (or all remaining buckets if `force`); marks them ready."""
@@ -459,6 +563,7 @@ class Engine:
                 continue
             if not force and not all(n in self._produced for n in names):
                 continue
+            self._flush_side(plan, force=True)   # the bucket's wgrads precede its reduce
             descs = [self._pending.pop(n) for n in names if n in self._pending]
             if descs:
                 arr = np.zeros(len(descs), dtype=WGD_DTYPE)
@@ -495,6 +600,8 @@ class Engine:
         self.seg = {}
         for e in self.bns.values():
             e.fused_fwd = e.fused_bwd = False
+            e.pending = None
+        self._cnt_next = 0
         b0 = plan.size()
         # ---- input
         if self.input_mode == "cifar_u8":
@@ -514,8 +621,12 @@ class Engine:
                              self.pool_arg.data_ptr(),
                              [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
             M = N * ph * ph
-            plan.bn_stats(self.pool_out.data_ptr(), M, st.cout, self.stat_part.data_ptr())
-            first_bn.src = (self.nat.bn_bwd_tiles(M, st.cout), self.nat.bn_stats_tile_rows(), M)
+            plan.bn_stats(self.pool_out.data_ptr(), M, st.cout, first_bn.part.data_ptr())
+            T = self.nat.bn_bwd_tiles(M, st.cout)
+            rows = self.nat.bn_stats_tile_rows()
+            first_bn.pending = (first_bn.part.data_ptr(), T, rows, M)
+            if T > self._consumer_cap(st.cout):
+                first_bn.pending = ("separate",) + first_bn.pending
         else:
             self._conv_fwd(plan, stem, self.x_in, self.stem_out, N, stats_for=first_bn)
         for i, b in enumerate(blocks):
@@ -545,13 +656,13 @@ class Engine:
                 self._conv_fwd(plan, convs[2], self.H2[i], Xn, N, pre=bns[2], residual=residual,
                                stats_for=nxt)
         fbn = self.bns[spec.final_bn.name]
-        self._bn_finalize(plan, fbn)
+        self._bn_finalize(plan, fbn, consumer_conv=False)   # consumer: bnrelu_avgpool
         XL = self.X[-1]
         HL, WL, F = XL.shape[1], XL.shape[2], XL.shape[3]
         plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                             self.pooled.data_ptr(), N, HL * WL, F)
         plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
-                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], BN_DECAY, BN_EPS, 1)
+                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
@@ -563,6 +674,7 @@ class Engine:
         # ---- backward
         b1 = plan.size()
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
+        self._side_q, self._side_blocks = [], 0
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
         dpart = self.wg_part.data_ptr() + 4 * off
@@ -571,7 +683,7 @@ class Engine:
                                           spec.num_classes, 1, F, F)
         self._produced.add(self.dense_name)
         plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
-                       0, 0, 0, 0, 0, 0, dg, [], [], [], BN_DECAY, BN_EPS, 1)
+                       0, 0, 0, 0, 0, 0, dg, [], [], [], [], BN_DECAY, BN_EPS, 1)
         dact = self._g(0, (N, HL, WL, F))
         plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
         d = 1
@@ -611,6 +723,7 @@ class Engine:
             dx = self._g(o2, tuple(X.shape))
             self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
+            self._flush_side(plan)
             self._flush_buckets(plan)
         # stem (no dgrad: the input needs no gradient)
         if spec.maxpool:
@@ -623,6 +736,7 @@ class Engine:
             self._conv_bwd(plan, stem, dstem, self.x_in, N, None)
         else:
             self._conv_bwd(plan, stem, dout, self.x_in, N, None)
+        self._flush_side(plan, force=True)
         self._flush_buckets(plan, force=True)
         self.seg["bwd"] = (b1, plan.size())
 
@@ -815,7 +929,7 @@ class _EvalPlan:
                       bn.scale.data_ptr(), bn.shift.data_ptr())
         y = buf((N, st.ho, st.wo, st.cout))
         p.conv_gemm(0, self.x_in.data_ptr(), stem.ohwi, y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
-                    eng._geom(stem, N), [], [], [], BN_DECAY, BN_EPS, 1)
+                    eng._geom(stem, N), [], [], [], [], BN_DECAY, BN_EPS, 1)
         if spec.maxpool:
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
@@ -845,7 +959,7 @@ class _EvalPlan:
         p.bnrelu_avgpool(x.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                          self.pooled.data_ptr(), N, x.shape[1] * x.shape[2], F)
         p.conv_gemm(0, self.pooled.data_ptr(), eng.dense_ohwi, 0, self.logits.data_ptr(), 0, 0, 0,
-                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], BN_DECAY, BN_EPS, 1)
+                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
                        spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
@@ -854,7 +968,7 @@ class _EvalPlan:
     def _conv(self, p, c, x, out, pre, residual=None):
         p.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                     0 if residual is None else residual.data_ptr(), pre.scale.data_ptr(),
-                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [], [], [], BN_DECAY, BN_EPS, 1)
+                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [], [], [], [], BN_DECAY, BN_EPS, 1)
 
     def run(self, images=None, labels=None, raw_u8: bool = True):
         """Returns (loss_sum, correct, probs[N, classes]) for one eval batch.

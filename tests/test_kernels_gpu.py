@@ -330,3 +330,98 @@ def test_direct_conv3x3_matches_reference_and_generic(gpu, generic_conv, N, H, C
     assert _rel(outs[0][2], outs[1][2]) < 1e-2
     sums_d, sums_g = outs[0][3].sum(0), outs[1][3].sum(0)
     assert _rel(sums_d, sums_g) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,C,group", [(8, 32, 16, 0), (128, 32, 16, 16), (64, 16, 32, 16),
+                                         (4, 14, 256, 0), (16, 14, 256, 16)])
+def test_fused_last_arriver_bn_finalize(gpu, N, H, C, group):
+    """In-kernel BN finalize (one- and two-level last arriver) == separate kernels,
+    run twice to check the counters are left zeroed for the next launch."""
+    torch.manual_seed(12)
+    nat = fn.native()
+    M = N * H * H
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(3, 3, C, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    w_ohwi = w.permute(3, 0, 1, 2).contiguous()
+    tiles, rows = fn.stat_tiles(M, C)
+    gamma = torch.rand(C, device=gpu) + 0.5
+    beta = torch.randn(C, device=gpu)
+    cnt = torch.zeros(4096, dtype=torch.int32, device=gpu)
+    gpart = torch.empty(128 * 2 * C, device=gpu)
+    for _ in range(2):
+        part = torch.empty(tiles * 2 * C, device=gpu)
+        mm, mv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+        mean, rstd, scale, shift = (torch.empty(C, device=gpu) for _ in range(4))
+        y = fn.conv2d_fwd(x, w_ohwi, 1, stat_part=part,
+                          fin=[cnt, gamma, beta, mm, mv, mean, rstd, scale, shift, gpart, group,
+                              0])
+        mm2, mv2 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+        r = fn.bn_finalize(part, tiles, rows, M, gamma, beta, mm2, mv2)
+        torch.testing.assert_close(mean, r[0], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(rstd, r[1], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(scale, r[2], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(shift, r[3], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(mm, mm2, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(mv, mv2, rtol=1e-5, atol=1e-7)
+        assert int(cnt.abs().sum()) == 0
+        # backward: dgrad + BN-backward sums finalized in-kernel
+        dy = torch.randn_like(y)
+        bpart = torch.empty(tiles * 2 * C, device=gpu)
+        dg, db, coef = torch.empty(C, device=gpu), torch.empty(C, device=gpu), \
+            torch.empty(3 * C, device=gpu)
+        fn.conv2d_dgrad(dy, w, tuple(x.shape), 1, bnb=(x, mean, rstd, scale, shift, bpart),
+                        bfin=[cnt, gamma, rstd, dg, db, coef, gpart, group])
+        p = bpart.view(tiles, 2, C).sum(0)
+        torch.testing.assert_close(db, p[0], rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(dg, p[1], rtol=1e-4, atol=1e-3)
+        a = gamma * rstd
+        torch.testing.assert_close(coef, torch.cat([a, a * db / M, a * dg / M]), rtol=1e-5,
+                                   atol=1e-6)
+        assert int(cnt.abs().sum()) == 0
+    assert nat.conv_gemm_bn(M, C) in (16, 32, 64, 128)
+
+
+@pytest.mark.parametrize("N,H,C,k,groups", [(8, 32, 16, 3, False), (128, 32, 16, 3, True),
+                                            (64, 16, 32, 3, True), (16, 8, 64, 3, False),
+                                            (4, 14, 128, 1, False), (8, 14, 128, 1, True)])
+def test_consumer_prologue_bn_finalize(gpu, N, H, C, k, groups):
+    """BnPreFin: the first consumer conv combines the producer's (mean, M2) partials
+    (tile partials, or group partials left by groups_only last arrivers) in its
+    prologue == bn_finalize + plain PRE; block 0 writes the BN outputs."""
+    torch.manual_seed(13)
+    nat = fn.native()
+    M = N * H * H
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w0 = (torch.randn(C, k, k, C, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    w1 = (torch.randn(C, k, k, C, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    bm = nat.conv_gemm_bm(M, C)
+    T = -(-M // bm)
+    part = torch.empty(T * 2 * C, device=gpu)
+    gamma = torch.rand(C, device=gpu) + 0.5
+    beta = torch.randn(C, device=gpu)
+    fin = None
+    src, cnt, rows = part, T, bm
+    if groups:
+        cap = (256 // C) * 8
+        gs = 2
+        while -(-T // gs) > cap:
+            gs *= 2
+        gpart = torch.empty(-(-T // gs) * 2 * C, device=gpu)
+        cntr = torch.zeros(4096, dtype=torch.int32, device=gpu)
+        fin = [cntr, gamma, beta, 0, 0, 0, 0, 0, 0, gpart, gs, 1]
+        src, cnt, rows = gpart, -(-T // gs), gs * bm
+    y0 = fn.conv2d_fwd(x, w0, 1, stat_part=part, fin=fin)
+    if groups:
+        assert int(cntr.abs().sum()) == 0
+    outs = [torch.empty(C, device=gpu) for _ in range(4)]
+    mm, mv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    y1 = fn.conv2d_fwd(y0, w1, 1, pre_scale=outs[2], pre_shift=outs[3],
+                       pfin=[src, cnt, rows, M, gamma, beta, *outs, mm, mv])
+    mm2, mv2 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    r = fn.bn_finalize(part, T, bm, M, gamma, beta, mm2, mv2)
+    for a, b in zip(outs, r):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mm, mm2, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(mv, mv2, rtol=1e-5, atol=1e-7)
+    y1_ref = fn.conv2d_fwd(y0, w1, 1, pre_scale=r[2], pre_shift=r[3])
+    assert _rel(y1, y1_ref) < 2e-3
