@@ -460,6 +460,9 @@ PYBIND11_MODULE(_C, m) {
   // host-side helpers that mirror the launchers' internal choices
   m.def("conv_gemm_bm", &conv_gemm_bm);
   m.def("conv_gemm_bn", &conv_gemm_bn);
+  m.def("set_wgrad_direct", &set_wgrad_direct,
+        "enable/disable the direct 3x3 small-C wgrad kernel (default: on unless "
+        "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");
   m.def("set_conv_direct", &set_conv_direct,
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);

@@ -214,6 +214,10 @@ static void wg_tile(const ConvGeom& g, int* bm, int* bn) {
 }
 
 int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
+  if (const int bmp = wgrad_direct_bmp(g)) {   // direct kernel: one split per pixel tile
+    *px_per_split = bmp;
+    return (int)((long)g.N * g.H * g.W / bmp);
+  }
   int bm, bn;
   wg_tile(g, &bm, &bn);
   const long NT = (long)g.kh * g.kw * g.C;
@@ -237,6 +241,7 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
 }
 
 void conv_wgrad(const WgradArgs& a, hipStream_t s) {
+  if (conv_wgrad_direct(a, s)) return;
   int bm, bn;
   wg_tile(a.g, &bm, &bn);
   if (bm == 16) wg_launch<16, 64, 1, 4>(a, s);

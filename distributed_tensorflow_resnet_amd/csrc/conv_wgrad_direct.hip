@@ -1,0 +1,226 @@
+// Direct (halo-tiled) weight gradient of the 3x3 / stride-1 / pad-1 small-C
+// convolutions (the CIFAR stages, C = K in {16, 32, 64}; the
+// generic split-K kernel is conv_wgrad.hip).
+//
+//   dW[co][t=(r,c)][ci] = sum_p DY[p][co] * A[p + off(t)][ci],  A = relu(bn(x)) (PRE)
+//
+// The generic kernel gathers an im2col tile per K step (9 reads of every input
+// element, one dependent global round trip per 64 pixels).  Here a workgroup owns
+// BMP whole-row pixels (R rows of one image, or whole images) and one group of
+// TJ taps:
+//   1. ONE round of global loads into VGPRs: the dy tile [BMP][K] and the x halo
+//      [(R+2)][(W+2)][C] (zero padding; the BatchNorm+ReLU of x applied once per
+//      element while staging);
+//   2. both to LDS, pixel-major as they come from HBM;
+//   3. MFMA 16x16x32 with the fragments gathered by the transposed LDS read
+//      ds_read_b64_tr_b16 (both operands are K(=pixel)-major): lane (q, pc) of a
+//      16-lane group points at pixel row q of a 4-row block -- for B at that
+//      pixel's halo position shifted by the tap -- and columns 4pc..4pc+3, and
+//      receives one column of the transposed 4 x 16 block.  Waves split M
+//      (16 output channels each) and, when K < 64, the pixels (WK slices);
+//   4. the WK slice results are summed in LDS in fixed order and the workgroup's
+//      [K][TJ*C] block is written into its split's fp32 partial slab -- the same
+//      [split][K][9C] layout the grouped deterministic reduce already consumes.
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+template <int C, int KO, int WI, int HI, int BMP, int TJ, bool PRE>
+__global__ void __launch_bounds__(256)
+conv_wgrad_direct_kernel(WgradArgs args) {
+  constexpr int HW = HI * WI;
+  constexpr int NIMG = BMP >= HW ? BMP / HW : 1;
+  constexpr int RH = BMP >= HW ? HI : BMP / WI;       // rows per image in the tile
+  constexpr int W2 = WI + 2;
+  constexpr int U = C / 8;                            // 16-B units per pixel
+  constexpr int HU = NIMG * (RH + 2) * W2 * U;        // halo units
+  constexpr int HPT = (HU + 255) / 256;
+  constexpr int DU = BMP * KO / 8;                    // dy units
+  constexpr int DPT = (DU + 255) / 256;
+  constexpr int WM = KO / 16, WK = 4 / WM;            // waves: M blocks x pixel slices
+  constexpr int NJ = TJ * C;                          // output columns per workgroup
+  constexpr int NT = NJ / 16;                         // n-tiles per wave
+  constexpr int PX = BMP / WK;                        // pixels per wave
+  constexpr int KS = PX / 32;                         // k-steps per wave
+  static_assert(WM * WK == 4 && PX % 32 == 0 && NJ % 16 == 0, "tile");
+  static_assert(BMP >= HW ? BMP % HW == 0 : (HW % BMP == 0 && BMP % WI == 0), "rows");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* dys = reinterpret_cast<bf16*>(smem);                  // [BMP][KO]
+  bf16* halo = dys + BMP * KO;                                // [NIMG][RH+2][W2][C]
+  float* pre_s = reinterpret_cast<float*>(halo + HU * 8);     // [2][C]
+
+  const int split = blockIdx.x, tj = blockIdx.y;
+  const int p0 = split * BMP;                                 // first pixel of the tile
+  const int img0 = p0 / HW, h0 = (p0 - img0 * HW) / WI;       // h0 = 0 for whole images
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wk = wave / WM;
+  const bf16x8 zero8 = {};
+
+  // ---- 1. one round of loads: dy tile + x halo ----
+  bf16x8 dv[DPT], hv[HPT];
+  unsigned hmask = 0;
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int q = tid + i * 256;
+    dv[i] = q < DU ? *reinterpret_cast<const bf16x8*>(args.dy + (long)p0 * KO + q * 8) : zero8;
+  }
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int q = tid + i * 256;
+    bf16x8 v = zero8;
+    if (q < HU) {
+      const int u = q % U, pix = q / U;
+      const int hc = pix % W2, rr = pix / W2;
+      const int im = rr / (RH + 2), hr = rr - im * (RH + 2);
+      const int h = h0 - 1 + hr, w = hc - 1;
+      if (h >= 0 && h < HI && w >= 0 && w < WI) {
+        v = *reinterpret_cast<const bf16x8*>(
+            args.x + (((long)(img0 + im) * HI + h) * WI + w) * C + u * 8);
+        if constexpr (PRE) hmask |= 1u << i;
+      }
+    }
+    hv[i] = v;
+  }
+  if constexpr (PRE) {
+    if (tid < C) {
+      pre_s[tid] = args.pre_scale[tid];
+      pre_s[C + tid] = args.pre_shift[tid];
+    }
+    __syncthreads();
+  }
+  // ---- 2. to LDS ----
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int q = tid + i * 256;
+    if (q < DU) *reinterpret_cast<bf16x8*>(dys + q * 8) = dv[i];
+  }
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) {
+    const int q = tid + i * 256;
+    if (q < HU) {
+      bf16x8 v = hv[i];
+      if constexpr (PRE) {
+        const int u = q % U;
+        if ((hmask >> i) & 1u) v = affine_relu8(v, pre_s + u * 8, pre_s + C + u * 8);
+      }
+      *reinterpret_cast<bf16x8*>(halo + q * 8) = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. MFMA: acc[n-tile] for output channels [16 wm, 16 wm + 16) ----
+  f32x4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, li = lane & 15;
+  const int qr = li >> 2, pc = li & 3;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    // the two 4-row blocks of this lane group: pixels r1 (elements 0..3), r2 (4..7)
+    const int r1 = wk * PX + ks * 32 + 4 * gq + qr;
+    const int r2 = r1 + 16;
+    const s16x4 alo = lds_read_tr16(dys + r1 * KO + wm * 16 + 4 * pc);
+    const s16x4 ahi = lds_read_tr16(dys + r2 * KO + wm * 16 + 4 * pc);
+    const s16x8 av = {alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+    const bf16x8 af = __builtin_bit_cast(bf16x8, av);
+    // halo pixel (top-left of the 3x3 window) of the two rows
+    int hb[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = e == 0 ? r1 : r2;
+      const int im = p / (RH * WI), rem = p - im * (RH * WI);
+      const int hl = rem / WI, w = rem - hl * WI;
+      hb[e] = (im * (RH + 2) + hl) * W2 + w;
+    }
+#pragma unroll
+    for (int t = 0; t < TJ; ++t) {
+      const int tap = tj * TJ + t;
+      const int toff = (tap / 3) * W2 + (tap % 3);
+#pragma unroll
+      for (int cb = 0; cb < C / 16; ++cb) {
+        const int col = cb * 16 + 4 * pc;
+        const s16x4 blo = lds_read_tr16(halo + (hb[0] + toff) * C + col);
+        const s16x4 bhi = lds_read_tr16(halo + (hb[1] + toff) * C + col);
+        const s16x8 bv = {blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]};
+        acc[t * (C / 16) + cb] = mfma16(af, __builtin_bit_cast(bf16x8, bv), acc[t * (C / 16) + cb]);
+      }
+    }
+  }
+  __syncthreads();   // operands dead: LDS becomes the [WK][KO][NJ] reduction tile
+
+  // ---- 4. fixed-order sum over the WK pixel slices, write the partial block ----
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      red[(wk * KO + wm * 16 + gq * 4 + i) * NJ + n * 16 + li] = acc[n][i];
+  __syncthreads();
+  float* out = args.part + (long)split * KO * (9 * C) + tj * NJ;
+  for (int e = tid; e < KO * NJ; e += 256) {
+    const int co = e / NJ, n = e - co * NJ;
+    float s = red[e];
+#pragma unroll
+    for (int k = 1; k < WK; ++k) s += red[k * KO * NJ + e];
+    out[(long)co * (9 * C) + n] = s;
+  }
+}
+
+// (C, W, H, BMP, TJ) variants; BMP pixels per split, TJ taps per workgroup.
+template <int C, int WI, int HI, int BMP, int TJ>
+static void wgd_launch(const WgradArgs& a, hipStream_t s) {
+  constexpr int NIMG = BMP >= HI * WI ? BMP / (HI * WI) : 1;
+  constexpr int RH = BMP >= HI * WI ? HI : BMP / WI;
+  constexpr size_t MAIN = (size_t)BMP * C * 2 + (size_t)NIMG * (RH + 2) * (WI + 2) * C * 2 +
+                          2 * C * sizeof(float);
+  constexpr int WK = 4 / (C / 16);
+  constexpr size_t RED = (size_t)WK * C * TJ * C * sizeof(float);
+  const size_t lds = ((MAIN > RED ? MAIN : RED) + 15) & ~(size_t)15;
+  dim3 grid(a.splits, 9 / TJ);
+  if (a.pre_scale)
+    hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, true>), grid, dim3(256),
+                       lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, false>), grid,
+                       dim3(256), lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+static int g_wgd_enabled = -1;
+
+void set_wgrad_direct(int enabled) { g_wgd_enabled = enabled ? 1 : 0; }
+
+// Pixels per split of the direct kernel for this conv, 0 if not covered.
+int wgrad_direct_bmp(const ConvGeom& g) {
+  if (g_wgd_enabled < 0) {
+    const char* e = std::getenv("DTR_DIRECT_WGRAD");
+    g_wgd_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_wgd_enabled) return 0;
+  if (g.kh != 3 || g.kw != 3 || g.stride != 1 || g.pad != 1 || g.C != g.K || g.H != g.W ||
+      g.Ho != g.H || g.Wo != g.W)
+    return 0;
+  int bmp = 0;
+  if (g.C == 16 && g.W == 32) bmp = 256;
+  else if (g.C == 32 && g.W == 16) bmp = 256;
+  else if (g.C == 64 && g.W == 8) bmp = 128;
+  const long P = (long)g.N * g.H * g.W;
+  if (bmp == 0 || P % bmp != 0) return 0;
+  return bmp;
+}
+
+bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) {
+  const int bmp = wgrad_direct_bmp(a.g);
+  if (bmp == 0 || a.px_per_split != bmp) return false;
+  const ConvGeom& g = a.g;
+  if (g.C == 16) wgd_launch<16, 32, 32, 256, 9>(a, s);
+  else if (g.C == 32) wgd_launch<32, 16, 16, 256, 3>(a, s);
+  else wgd_launch<64, 8, 8, 128, 3>(a, s);
+  return true;
+}
+
+}  // namespace dtr

@@ -112,6 +112,10 @@ struct WgradArgs {
   int px_per_split;         // multiple of 64
 };
 void conv_wgrad(const WgradArgs& a, hipStream_t s);
+// Direct halo-tiled wgrad for 3x3/s1 small C (conv_wgrad_direct.hip).
+bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s);
+int wgrad_direct_bmp(const ConvGeom& g);   // pixels per split, 0 = not covered
+void set_wgrad_direct(int enabled);
 // grad[tap][ci][co] (+)= scale * sum_s part[s][co][tap*C+ci] for co < K_valid, ci < C_valid
 // (output is the unpadded TF HWIO tensor [taps][C_valid][K_valid])
 void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_valid, int taps,

@@ -425,3 +425,27 @@ def test_consumer_prologue_bn_finalize(gpu, N, H, C, k, groups):
     torch.testing.assert_close(mv, mv2, rtol=1e-5, atol=1e-7)
     y1_ref = fn.conv2d_fwd(y0, w1, 1, pre_scale=r[2], pre_shift=r[3])
     assert _rel(y1, y1_ref) < 2e-3
+
+
+@pytest.mark.parametrize("N,H,C", [(8, 32, 16), (4, 16, 32), (6, 8, 64), (128, 32, 16)])
+def test_direct_wgrad_matches_reference_and_generic(gpu, N, H, C):
+    """Halo-tiled 3x3/s1 wgrad (conv_wgrad_direct.hip) with the fused BN+ReLU of x:
+    == fp32 autograd of conv(relu(x*scale+shift)) and == the generic split-K kernel."""
+    torch.manual_seed(14)
+    nat = fn.native()
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    sc = torch.rand(C, device=gpu) + 0.5
+    sh = torch.randn(C, device=gpu) * 0.3
+    dy = torch.randn(N, H, H, C, device=gpu).to(BF)
+    assert nat.wgrad_pick_splits([N, H, H, C, H, H, C, 3, 3, 1, 1])[1] in (128, 256)
+    dw = fn.conv2d_wgrad(dy, x, 3, 3, 1, pre_scale=sc, pre_shift=sh)
+    nat.set_wgrad_direct(0)
+    try:
+        dw_gen = fn.conv2d_wgrad(dy, x, 3, 3, 1, pre_scale=sc, pre_shift=sh)
+    finally:
+        nat.set_wgrad_direct(1)
+    a = torch.relu(x.float() * sc + sh).to(BF).float()
+    w = torch.zeros(3, 3, C, C, device=gpu, requires_grad=True)
+    ref.conv2d(a, w, 1).backward(dy.float())
+    assert _rel(dw, w.grad) < 1e-3
+    assert _rel(dw, dw_gen) < 1e-3
