@@ -47,8 +47,9 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                            ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
                            ptr_t stat_part, int accumulate, std::vector<int> geom,
                            std::vector<ptr_t> bnb, std::vector<ptr_t> fin,
-                           std::vector<ptr_t> bfin, std::vector<ptr_t> pfin, float momentum,
-                           float eps, int update_moving) {
+                           std::vector<ptr_t> bfin, std::vector<ptr_t> pfin,
+                           std::vector<ptr_t> abwd, float momentum, float eps,
+                           int update_moving) {
   GemmArgs g{};
   g.a = P<const bf16>(a);
   g.b = P<const bf16>(b);
@@ -80,12 +81,12 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                      P<float>(fin[7]), P<float>(fin[8]), momentum, eps, update_moving,
                      P<float>(fin[9]), (int)fin[10], (int)fin[11]};
   }
-  if (!bfin.empty()) {  // [counters, gamma, rstd, dgamma, dbeta, coef, gpart, group]
-    if (bfin.size() != 8) throw std::invalid_argument("bfin needs 8 entries");
+  if (!bfin.empty()) {  // [counters, gamma, rstd, dgamma, dbeta, coef, gpart, group, groups_only]
+    if (bfin.size() != 9) throw std::invalid_argument("bfin needs 9 entries");
     if (bnb.empty()) throw std::invalid_argument("bfin requires bnb");
     g.bfin = BnBwdFin{P<unsigned>(bfin[0]), P<const float>(bfin[1]), P<const float>(bfin[2]),
                       P<float>(bfin[3]), P<float>(bfin[4]), P<float>(bfin[5]),
-                      P<float>(bfin[6]), (int)bfin[7]};
+                      P<float>(bfin[6]), (int)bfin[7], (int)bfin[8]};
   }
   if (!pfin.empty()) {  // [part, cnt, rows_per, M, gamma, beta, mean, rstd, scale, shift, mmean, mvar]
     if (pfin.size() != 12) throw std::invalid_argument("pfin needs 12 entries");
@@ -94,6 +95,16 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                       P<const float>(pfin[4]), P<const float>(pfin[5]), P<float>(pfin[6]),
                       P<float>(pfin[7]), P<float>(pfin[8]), P<float>(pfin[9]),
                       P<float>(pfin[10]), P<float>(pfin[11]), momentum, eps, update_moving};
+  }
+  if (!abwd.empty()) {  // [x, add, mean, rstd, scale, shift, gamma, part, cnt, a_out, dgamma,
+                       //  dbeta, coef]
+    if (abwd.size() != 13) throw std::invalid_argument("abwd needs 13 entries");
+    if (mode != MODE_DGRAD) throw std::invalid_argument("abwd is dgrad-only");
+    g.abwd = BnBwdPre{P<const bf16>(abwd[0]), P<const bf16>(abwd[1]), P<const float>(abwd[2]),
+                      P<const float>(abwd[3]), P<const float>(abwd[4]), P<const float>(abwd[5]),
+                      P<const float>(abwd[6]), P<const float>(abwd[7]), (int)abwd[8],
+                      P<bf16>(abwd[9]), P<float>(abwd[10]), P<float>(abwd[11]),
+                      P<float>(abwd[12])};
   }
   g.g = geom_from(geom);
   const ConvGeom& c = g.g;
@@ -112,6 +123,13 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   if (g.Ncol % 16) throw std::invalid_argument("conv: output channels must be a multiple of 16");
   if ((pre_scale != 0) && mode != MODE_FWD)
     throw std::invalid_argument("fused BN+ReLU prologue is forward-only");
+  if (g.abwd.x != nullptr) {
+    if (!conv_direct_covers(g, mode))
+      throw std::invalid_argument("abwd: this dgrad is not covered by the direct 3x3 kernel");
+    const int C = c.K;   // A channels of the dgrad
+    if (g.abwd.cnt < 1 || g.abwd.cnt > (256 / C) * 8)
+      throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
+  }
   if (g.pfin.cnt > 0) {
     const int C = c.C;   // PRE is forward-only: the A channels
     if (C > 256 || (C & (C - 1)) != 0 || g.pfin.cnt > (256 / C) * 8)
@@ -460,6 +478,14 @@ PYBIND11_MODULE(_C, m) {
   // host-side helpers that mirror the launchers' internal choices
   m.def("conv_gemm_bm", &conv_gemm_bm);
   m.def("conv_gemm_bn", &conv_gemm_bn);
+  m.def("conv_direct_covers", [](int mode, std::vector<int> geom) {
+    GemmArgs g{};
+    g.g = geom_from(geom);
+    const ConvGeom& c = g.g;
+    g.M = mode == MODE_FWD ? c.N * c.Ho * c.Wo : c.N * c.H * c.W;
+    g.Ncol = mode == MODE_FWD ? c.K : c.C;
+    return conv_direct_covers(g, mode);
+  }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
   m.def("set_wgrad_direct", &set_wgrad_direct,
         "enable/disable the direct 3x3 small-C wgrad kernel (default: on unless "
         "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");

@@ -36,6 +36,7 @@ template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 __global__ void __launch_bounds__(256)
 conv3x3_direct_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
+  constexpr bool ABWD = (FLAGS & F_ABWD) != 0;
   constexpr int U = CA / 8;                 // 16-B units per pixel
   constexpr int R = BM / WI;                // output rows per tile
   constexpr int HW2 = WI + 2;               // halo row length (pixels)
@@ -50,7 +51,7 @@ conv3x3_direct_kernel(GemmArgs args) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = reinterpret_cast<bf16*>(smem);
   float* pre_s = reinterpret_cast<float*>(smem + HU * 16);   // PRE: [2][CA] scale, shift
-  float* fin_scratch = pre_s + 2 * CA;                        // 768 floats (BnPreFin)
+  float* fin_scratch = pre_s + 7 * CA;                        // 768 floats (prologue sums)
 
   const ConvGeom& g = args.g;
   const int NC = args.Ncol;
@@ -83,23 +84,36 @@ conv3x3_direct_kernel(GemmArgs args) {
     }
   }
   bf16x8 hv[HPT];
+  bf16x8 hx[ABWD ? HPT : 1], hadd[ABWD ? HPT : 1];   // ABWD: BN input and residual grad
   unsigned hmask = 0;
-  const bf16* abase = args.a + (long)img * HWp * CA;
+  const long ibase = (long)img * HWp * CA;
+  const bf16* abase = args.a + ibase;
 #pragma unroll
   for (int i = 0; i < HPT; ++i) {
     const int q = tid + i * 256;
     bf16x8 v = zero8;
+    if constexpr (ABWD) {
+      hx[i] = zero8;
+      hadd[i] = zero8;
+    }
     if (q < HU) {
       const int u = q % U, pix = q / U;
       const int hr = pix / HW2, hc = pix - hr * HW2;
       const int h = h0 - 1 + hr, w = hc - 1;
       if (h >= 0 && h < H && w >= 0 && w < WI) {
-        v = *reinterpret_cast<const bf16x8*>(abase + ((long)h * WI + w) * CA + u * 8);
-        if constexpr (PRE) hmask |= 1u << i;   // padding stays zero (TF pads after BN-ReLU)
+        const long o = ((long)h * WI + w) * CA + u * 8;
+        v = *reinterpret_cast<const bf16x8*>(abase + o);
+        if constexpr (PRE || ABWD) hmask |= 1u << i;   // padding stays zero
+        if constexpr (ABWD) {
+          hx[i] = *reinterpret_cast<const bf16x8*>(args.abwd.x + ibase + o);
+          if (args.abwd.add) hadd[i] = *reinterpret_cast<const bf16x8*>(args.abwd.add + ibase + o);
+        }
       }
     }
     hv[i] = v;
   }
+  EpiPre<BM, BN, WM> epre;                    // epilogue operands, loaded now
+  epi_prefetch<BM, BN, WM, FLAGS>(args, m0, n0, epre);
   // ---- BN scale/shift table for the fused BN+ReLU (finalized here when this is
   //      the BN's first consumer); its loads overlap the halo loads in flight ----
   if constexpr (PRE) {
@@ -113,6 +127,54 @@ conv3x3_direct_kernel(GemmArgs args) {
       __syncthreads();
     }
   }
+  // ---- ABWD: BN-backward coefficients from the producer's partial sums ----
+  float* bw_s = pre_s;   // [7][CA]: a, b, c, mean, rstd, scale, shift (ABWD never has PRE)
+  if constexpr (ABWD) {
+    const BnBwdPre& Q = args.abwd;
+    constexpr int G = 256 / CA;
+    const int c = tid % CA, qq = tid / CA;
+    float a1 = 0.f, a2 = 0.f;
+    float v1[FIN_UNROLL], v2[FIN_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const int t = qq + u * G;
+      v1[u] = t < Q.cnt ? Q.part[(long)t * 2 * CA + c] : 0.f;
+      v2[u] = t < Q.cnt ? Q.part[(long)t * 2 * CA + CA + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      a1 += v1[u];
+      a2 += v2[u];
+    }
+    fin_scratch[tid] = a1;
+    fin_scratch[256 + tid] = a2;
+    __syncthreads();
+    if (qq == 0) {
+      float sg = 0.f, sgx = 0.f;
+      for (int k = 0; k < G; ++k) {
+        sg += fin_scratch[k * CA + c];
+        sgx += fin_scratch[256 + k * CA + c];
+      }
+      const float rs = Q.rstd[c];
+      const float a = Q.gamma[c] * rs;
+      const float M = (float)args.M;
+      bw_s[c] = a;
+      bw_s[CA + c] = a * sg / M;
+      bw_s[2 * CA + c] = a * sgx / M;
+      bw_s[3 * CA + c] = Q.mean[c];
+      bw_s[4 * CA + c] = rs;
+      bw_s[5 * CA + c] = Q.scale[c];
+      bw_s[6 * CA + c] = Q.shift[c];
+      if (blockIdx.x == 0 && blockIdx.y == 0) {
+        Q.dbeta[c] = sg;
+        Q.dgamma[c] = sgx;
+        Q.coef[c] = a;
+        Q.coef[CA + c] = a * sg / M;
+        Q.coef[2 * CA + c] = a * sgx / M;
+      }
+    }
+    __syncthreads();
+  }
   // ---- 2. halo -> LDS (swizzled 16-B units) ----
 #pragma unroll
   for (int i = 0; i < HPT; ++i) {
@@ -123,6 +185,27 @@ conv3x3_direct_kernel(GemmArgs args) {
       bf16x8 v = hv[i];
       if constexpr (PRE) {
         if ((hmask >> i) & 1u) v = affine_relu8(v, pre_s + u * 8, pre_s + CA + u * 8);
+      }
+      if constexpr (ABWD) {
+        if ((hmask >> i) & 1u) {
+          // dh = a*g - b - c*xhat (+ add), exactly bn_bwd_apply's formula and rounding
+          const float* cb = bw_s + u * 8;
+          bf16x8 r;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xv = (float)hx[i][j];
+            const float gg = (xv * cb[5 * CA + j] + cb[6 * CA + j] > 0.f) ? (float)v[j] : 0.f;
+            const float xh = (xv - cb[3 * CA + j]) * cb[4 * CA + j];
+            float o2 = cb[j] * gg - cb[CA + j] - cb[2 * CA + j] * xh;
+            if (args.abwd.add) o2 += (float)hadd[i][j];
+            r[j] = (bf16)o2;
+          }
+          v = r;
+          const int hr = pix / HW2;
+          if (hr >= 1 && hr <= R && hc >= 1 && hc <= WI)   // interior: this tile's dh rows
+            *reinterpret_cast<bf16x8*>(args.abwd.a_out + ibase +
+                                       ((long)(h0 + hr - 1) * WI + hc - 1) * CA + u * 8) = v;
+        }
       }
       *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = v;
     }
@@ -164,13 +247,13 @@ conv3x3_direct_kernel(GemmArgs args) {
   __syncthreads();   // halo dead: the epilogue reuses the LDS
 
   // ---- 4. shared epilogue ----
-  conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
+  conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0, &epre);
 }
 
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_direct_cfg(const GemmArgs& a, hipStream_t s) {
   constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
-  constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(2 * CA + 768) * sizeof(float);
+  constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(7 * CA + 768) * sizeof(float);
   const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
   dim3 grid(a.M / BM, (a.Ncol + BN - 1) / BN);
   hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
@@ -187,8 +270,14 @@ static void launch_direct_flags(const GemmArgs& a, hipStream_t s) {
     else if (st) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_STATS>(a, s);
     else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, 0>(a, s);
   } else {
-    if (a.bnb_part != nullptr) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_BNB>(a, s);
-    else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, 0>(a, s);
+    const bool ab = a.abwd.x != nullptr;
+    if (a.bnb_part != nullptr) {
+      if (ab) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_BNB | F_ABWD>(a, s);
+      else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_BNB>(a, s);
+    } else {
+      if (ab) launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, F_ABWD>(a, s);
+      else launch_direct_cfg<CA, WI, BM, BN, WM, WN, MODE, 0>(a, s);
+    }
   }
 }
 
@@ -196,11 +285,10 @@ static int g_direct_enabled = -1;   // -1: read DTR_DIRECT_CONV once
 
 void set_conv_direct(int enabled) { g_direct_enabled = enabled ? 1 : 0; }
 
-// Returns true (and launches) when the direct kernel covers this conv: 3x3,
-// stride 1, pad 1, A channels == output channels == {16 @ W 32, 32 @ W 16,
-// 64 @ W 8}, and the tile height BM (= conv_gemm_bm, so the BN-stat partial
-// layout is unchanged) divides the image.
-bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
+// Whether the direct kernel covers this conv: 3x3, stride 1, pad 1, A channels ==
+// output channels == {16 @ W 32, 32 @ W 16, 64 @ W 8}, and the tile height BM
+// (= conv_gemm_bm, so the BN-stat partial layout is unchanged) divides the image.
+bool conv_direct_covers(const GemmArgs& a, int mode) {
   if (g_direct_enabled < 0) {
     const char* e = std::getenv("DTR_DIRECT_CONV");
     g_direct_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
@@ -211,11 +299,21 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
     return false;
   if (a.out_f32 != nullptr || a.bias != nullptr) return false;
   const int ca = (mode == MODE_FWD) ? g.C : g.K;
-  const int nc = a.Ncol;
-  if (ca != nc) return false;
-  const int bm = conv_gemm_bm(a.M, nc);
+  if (ca != a.Ncol) return false;
+  const int bm = conv_gemm_bm(a.M, a.Ncol);
   const int hw = g.H * g.W;
   if (bm % g.W != 0 || hw % bm != 0 || a.M % bm != 0) return false;
+  return (ca == 16 && g.W == 32 && (bm == 256 || bm == 64)) ||
+         (ca == 32 && g.W == 16 && (bm == 128 || bm == 64)) ||
+         (ca == 64 && g.W == 8 && bm == 64);
+}
+
+// Launches the direct kernel when it covers the conv (see above); false otherwise.
+bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
+  if (!conv_direct_covers(a, mode)) return false;
+  const ConvGeom& g = a.g;
+  const int ca = (mode == MODE_FWD) ? g.C : g.K;
+  const int bm = conv_gemm_bm(a.M, a.Ncol);
   const bool fwd = mode == MODE_FWD;
 #define DTR_DIRECT(CA_, W_, BM_, WM_, WN_)                                              \
   if (ca == CA_ && g.W == W_ && bm == BM_) {                                          \

@@ -6,7 +6,7 @@
 
 namespace dtr {
 
-enum { F_PRE = 1, F_STATS = 2, F_BNB = 4 };
+enum { F_PRE = 1, F_STATS = 2, F_BNB = 4, F_ABWD = 8 };
 
 // Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
 // it fits in 64 KiB (one phase), else one wave-row per phase (128x128 tiles).
@@ -116,6 +116,63 @@ __device__ __forceinline__ void sum_combine(const float* src, int NC, int n0, in
   }
 }
 
+// Column sums of the epilogue's 8-column row vectors: thread (r0 = tid / CPR,
+// cc = tid % CPR) holds v[j] for column cc*8+j.  Lanes with equal cc sit CPR apart
+// in a wave: xor-shuffles fold the wave, then lanes < CPR write the 4 wave totals
+// to wred[4][BN] (fixed order, deterministic).  Ends with a barrier; the caller
+// adds wred[0..3][col].  (A serial loop over the RPP rows by BN threads cost
+// 2.5-4 us per conv at 256-row tiles.)
+template <int CPR, int BN>
+__device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1) v[j] += __shfl_xor(v[j], off, 64);
+  if (lane < CPR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wred[wave * BN + lane * 8 + j] = v[j];
+  }
+  __syncthreads();
+}
+
+// Epilogue operand prefetch (single-phase tiles): the residual / accumulate-into /
+// BN-input row vectors each epilogue thread will combine are independent of the
+// GEMM, so kernels issue their loads at kernel start (epi_prefetch) and the
+// epilogue finds them in registers instead of paying a global round trip.
+template <int BM, int BN, int WM>
+struct EpiPre {
+  static constexpr bool ON = EpiLayout<BM, BN, WM>::PHASES == 1;
+  static constexpr int RIT = ON ? (EpiLayout<BM, BN, WM>::PR + EpiLayout<BM, BN, WM>::RPP - 1) /
+                                      EpiLayout<BM, BN, WM>::RPP
+                                : 1;
+  bf16x8 res[RIT], acc[RIT], x[RIT];
+};
+
+template <int BM, int BN, int WM, int FLAGS>
+__device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0, const int n0,
+                                             EpiPre<BM, BN, WM>& P) {
+  using EL = EpiLayout<BM, BN, WM>;
+  if constexpr (EpiPre<BM, BN, WM>::ON) {
+    const int tid = threadIdx.x;
+    const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
+    const int col0 = n0 + cc * 8;
+    const bf16x8 zero8 = {};
+#pragma unroll
+    for (int it = 0; it < EpiPre<BM, BN, WM>::RIT; ++it) {
+      const int row = m0 + r0 + it * EL::RPP;
+      const bool ok = col0 < args.Ncol && r0 + it * EL::RPP < EL::PR && row < args.M;
+      const long o = (long)row * args.Ncol + col0;
+      P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
+                                        : zero8;
+      P.acc[it] = (ok && args.accumulate && !args.out_f32)
+                      ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
+      if constexpr ((FLAGS & F_BNB) != 0)
+        P.x[it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
+    }
+  }
+}
+
 // Shared epilogue of every conv kernel (implicit-GEMM and direct): the wave
 // fragments acc[MR][NR] of the BM x BN tile at (m0, n0) -> LDS-staged 16-byte
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN
@@ -124,7 +181,8 @@ __device__ __forceinline__ void sum_combine(const float* src, int NC, int n0, in
 template <int BM, int BN, int WM, int WN, int FLAGS>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                              char* smem, const int m0, const int n0) {
+                                              char* smem, const int m0, const int n0,
+                                              const EpiPre<BM, BN, WM>* pre = nullptr) {
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -153,6 +211,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  float bnb_t1 = 0.f, bnb_t2 = 0.f;   // BNB column totals (thread tid < BN)
   float bsc[8], bsh[8], bmu[8], brs[8];
   if constexpr (BNB) {
 #pragma unroll
@@ -185,11 +244,20 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     __syncthreads();
+    // Pass 1: values of this thread's rows (residual / accumulate, ONE bf16
+    // rounding) kept in registers; BN sums accumulated.  Global stores are issued
+    // only AFTER the statistics' barriers: a __syncthreads() waits for every
+    // outstanding store of the wave (vmcnt(0)), so storing first put a full
+    // store round trip in the middle of the epilogue (~2 us per STATS/BNB conv).
+    constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
+    bf16x8 ob[RIT];
     float p1[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) p1[j] = 0.f;
-    for (int r = r0; r < nph; r += EL::RPP) {
-      if (!colok) break;
+#pragma unroll
+    for (int it = 0; it < RIT; ++it) {
+      const int r = r0 + it * EL::RPP;
+      if (!colok || r >= nph) continue;
       const int row = prow0 + r;
       float* cp = cs + r * EL::LDC + cc * 8;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(cp);
@@ -197,11 +265,13 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const long o = (long)row * NC + col0;
       if (args.residual) {
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(args.residual + o);
+        const bf16x8 rv = (EpiPre<BM, BN, WM>::ON && pre)
+                              ? pre->res[EpiPre<BM, BN, WM>::ON ? it : 0]
+                              : *reinterpret_cast<const bf16x8*>(args.residual + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
       }
-      if (args.out_f32) {
+      if (args.out_f32) {   // fp32 output (dense logits): no BN fusion on this path
         float* op = args.out_f32 + o;
         if (args.accumulate) {
           const f32x4 a0 = *reinterpret_cast<const f32x4*>(op);
@@ -214,28 +284,28 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         }
         *reinterpret_cast<f32x4*>(op) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(op + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else {
-        if (args.accumulate) {
-          const bf16x8 av = *reinterpret_cast<const bf16x8*>(args.out + o);
+        continue;
+      }
+      if (args.accumulate) {
+        const bf16x8 av = (EpiPre<BM, BN, WM>::ON && pre)
+                              ? pre->acc[EpiPre<BM, BN, WM>::ON ? it : 0]
+                              : *reinterpret_cast<const bf16x8*>(args.out + o);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
-        }
-        bf16x8 ob;
+        for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          ob[j] = (bf16)v[j];
-          v[j] = (float)ob[j];
-        }
-        *reinterpret_cast<bf16x8*>(args.out + o) = ob;
+      for (int j = 0; j < 8; ++j) {
+        ob[it][j] = (bf16)v[j];
+        v[j] = (float)ob[it][j];
       }
       if constexpr (STATS) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) p1[j] += v[j];
-        *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
       }
       if constexpr (BNB) {
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+        const bf16x8 xv = (EpiPre<BM, BN, WM>::ON && pre)
+                              ? pre->x[EpiPre<BM, BN, WM>::ON ? it : 0]
+                              : *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xv[j];
@@ -246,37 +316,33 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     if constexpr (STATS) {
-      // phase mean
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[r0 * BN + cc * 8 + j] = p1[j];
-      __syncthreads();
+      // phase mean, then M2 about it (two-pass, from the registers)
+      colsum8<EL::CPR, BN>(p1, red);
       if (tid < BN) {
-        float t = 0.f;
-        for (int k = 0; k < EL::RPP; ++k) t += red[k * BN + tid];
+        const float t = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
         mean_s[tid] = t / (float)nph;
       }
       __syncthreads();
-      float mu[8], q[8];
+      float q[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        mu[j] = mean_s[cc * 8 + j];
-        q[j] = 0.f;
-      }
-      for (int r = r0; r < nph; r += EL::RPP) {
-        if (!colok) break;
-        const float* cp = cs + r * EL::LDC + cc * 8;
+      for (int j = 0; j < 8; ++j) q[j] = 0.f;
+      if (colok) {
+        float mu[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = cp[j] - mu[j];
-          q[j] += d * d;
+        for (int j = 0; j < 8; ++j) mu[j] = mean_s[cc * 8 + j];
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) {
+          if (r0 + it * EL::RPP >= nph) continue;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (float)ob[it][j] - mu[j];
+            q[j] += d * d;
+          }
         }
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red2[r0 * BN + cc * 8 + j] = q[j];
-      __syncthreads();
+      colsum8<EL::CPR, BN>(q, red2);
       if (tid < BN) {
-        float m2 = 0.f;
-        for (int k = 0; k < EL::RPP; ++k) m2 += red2[k * BN + tid];
+        const float m2 = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];
         const float nb = (float)nph, mb = mean_s[tid];
         const float n = wn_run + nb;
         const float d = mb - wmean_run;
@@ -285,7 +351,26 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         wn_run = n;
       }
     }
-    __syncthreads();  // the next phase overwrites the staging tile
+    if constexpr (BNB) {
+      if (ph == EL::PHASES - 1 || prow0 + EL::PR >= M) {   // last phase: reduce before storing
+        colsum8<EL::CPR, BN>(s1, red);
+        colsum8<EL::CPR, BN>(s2, red2);
+        if (tid < BN) {
+          bnb_t1 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+          bnb_t2 = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];
+        }
+      }
+    }
+    // Pass 2: the stores
+    if (!args.out_f32) {
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int r = r0 + it * EL::RPP;
+        if (!colok || r >= nph) continue;
+        *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
+      }
+    }
+    if constexpr (EL::PHASES > 1) __syncthreads();  // the next phase overwrites the tile
   }
 
   if constexpr (STATS) {
@@ -351,18 +436,8 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     }
   }
   if constexpr (BNB) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[r0 * BN + cc * 8 + j] = s1[j];
-      red2[r0 * BN + cc * 8 + j] = s2[j];
-    }
-    __syncthreads();
     if (tid < BN && n0 + tid < NC) {
-      float t1 = 0.f, t2 = 0.f;
-      for (int k = 0; k < EL::RPP; ++k) {
-        t1 += red[k * BN + tid];
-        t2 += red2[k * BN + tid];
-      }
+      const float t1 = bnb_t1, t2 = bnb_t2;
       float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
       if (args.bfin.counters != nullptr) {
         publish_f32(tile_out + n0 + tid, t1);
@@ -392,8 +467,12 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
             publish_f32(F.gpart + (long)gi * 2 * NC + NC + n0 + tid, sgx);
           }
           reset_counter(F.counters + gridDim.y + blockIdx.y * ng + gi);
-          last = last_arriver(F.counters + blockIdx.y, ng, flag);
-          if (last) sum_combine<BN>(F.gpart, NC, n0, 0, ng, red, red2, sg, sgx);
+          if (F.groups_only) {
+            last = false;   // the consumer dgrad's BnBwdPre combines the group sums
+          } else {
+            last = last_arriver(F.counters + blockIdx.y, ng, flag);
+            if (last) sum_combine<BN>(F.gpart, NC, n0, 0, ng, red, red2, sg, sgx);
+          }
         }
       }
       if (last) {

@@ -27,6 +27,7 @@
 //           gradient g = d_a * [x*scale+shift > 0]:  per-tile sum(g) and
 //           sum(g * xhat), so no separate pass re-reads d_a and x.
 #include <algorithm>
+#include <stdexcept>
 
 #include "conv_epilogue.h"
 
@@ -303,6 +304,8 @@ static void launch_mode(const GemmArgs& a, hipStream_t s) {
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
   if (conv_direct(a, mode, s)) return;
+  if (a.abwd.x != nullptr)   // the generic kernel has no BN-backward prologue: never silently
+    throw std::runtime_error("conv_gemm: fused BN backward (abwd) needs the direct 3x3 kernel");
   if (mode == MODE_FWD) launch_mode<MODE_FWD>(a, s);
   else launch_mode<MODE_DGRAD>(a, s);
 }

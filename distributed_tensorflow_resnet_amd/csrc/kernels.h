@@ -66,6 +66,28 @@ struct BnBwdFin {            // backward sums -> dgamma/dbeta/apply coefficients
   float* coef;               // [3][C]
   float* gpart;              // two-level: [groups][2][NC] group sums
   int group;                 // tiles per level-1 group; 0 = single level
+  int groups_only;           // 1: stop after level 1 (a consumer's BnBwdPre combines gpart)
+};
+// Consumer-side BatchNorm+ReLU backward (direct dgrad only): the dgrad's A operand
+// is the BN-backward output dh = a*g - b - c*xhat (+ add), g = da*[x*scale+shift > 0],
+// computed while staging the halo from da (GemmArgs::a), x and add; the (sum g,
+// sum g*xhat) partials of the producer are combined in the prologue (coefficients a,
+// b, c); the interior of the halo (this tile's dh rows) is written to a_out for the
+// other consumers (wgrad, residual path); block (0,0) writes dgamma/dbeta/coef.
+struct BnBwdPre {
+  const bf16* x;             // BN input [M][C]; nullptr = disabled
+  const bf16* add;           // optional gradient added to dh (residual branch)
+  const float* mean;
+  const float* rstd;
+  const float* scale;
+  const float* shift;
+  const float* gamma;
+  const float* part;         // [cnt][2][C] (sum g, sum g*xhat)
+  int cnt;
+  bf16* a_out;               // dh [M][C]
+  float* dgamma;
+  float* dbeta;
+  float* coef;               // [3][C]
 };
 
 struct GemmArgs {
@@ -89,6 +111,7 @@ struct GemmArgs {
   BnFwdFin fin;             // with stat_part: finalize in-kernel
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
   BnPreFin pfin;            // with pre_scale: finalize the PRE BatchNorm in the prologue
+  BnBwdPre abwd;            // direct dgrad: BN backward on the A operand (see above)
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;
@@ -97,6 +120,7 @@ struct GemmArgs {
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
+bool conv_direct_covers(const GemmArgs& a, int mode);
 void set_conv_direct(int enabled);
 int conv_gemm_bm(int M, int Ncol);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks

@@ -109,7 +109,7 @@ def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residu
                        0 if out_f32 else out.data_ptr(), out.data_ptr() if out_f32 else 0,
                        _ptr(residual), _ptr(pre_scale), _ptr(pre_shift), _ptr(bias),
                        0 if bias is None else bias.numel(), _ptr(stat_part), int(accumulate),
-                       g.as_list(), [], _ptrs(fin), [], _ptrs(pfin), 0.997, 1e-5, 1, _stream())
+                       g.as_list(), [], _ptrs(fin), [], _ptrs(pfin), [], 0.997, 1e-5, 1, _stream())
     return out
 
 
@@ -118,11 +118,14 @@ def _ptrs(lst):
 
 
 def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False, bnb=None,
-                 bfin=None):
+                 bfin=None, abwd=None):
     """dx = conv2d_transpose(dy, W) with TF fixed padding; w_hwio [kh][kw][C][K].
 
     ``bnb=(x, mean, rstd, scale, shift, part)`` additionally emits the
-    BN+ReLU backward partials of dx (per tile: sum g, sum g*xhat, g = dx*[relu])."""
+    BN+ReLU backward partials of dx (per tile: sum g, sum g*xhat, g = dx*[relu]).
+    ``abwd=[x, add, mean, rstd, scale, shift, gamma, part, cnt, a_out, dgamma, dbeta,
+    coef]`` (direct 3x3 kernel only): ``dy`` is the gradient BEFORE its BatchNorm+ReLU
+    backward, which the kernel applies while staging (writing the result to a_out)."""
     _check(dy, BF16, 4, "dy")
     _check(w_hwio, BF16, 4, "w_hwio")
     N, H, W, C = x_shape
@@ -134,7 +137,7 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
         out = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
     bl = [] if bnb is None else [t.data_ptr() for t in bnb]
     native().conv_gemm(1, dy.data_ptr(), w_hwio.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                       int(accumulate), g.as_list(), bl, [], _ptrs(bfin), [], 0.997, 1e-5, 1,
+                       int(accumulate), g.as_list(), bl, [], _ptrs(bfin), [], _ptrs(abwd), 0.997, 1e-5, 1,
                        _stream())
     return out
 

@@ -117,6 +117,8 @@ class _BN:
     names: tuple = ()
     part: torch.Tensor = None     # this BN's forward tile partials [T][2][C]
     gpart: torch.Tensor = None    # level-1 group partials [groups][2][C]
+    bpart: torch.Tensor = None    # backward partial sums [T][2][C] and their groups
+    bgpart: torch.Tensor = None
 
 
 @dataclass
@@ -340,6 +342,9 @@ class Engine:
             bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
             b.part = torch.empty(_ceil(M, bm) * 2 * C, device=dev)
             b.gpart = torch.empty(max(_ceil(M, bm) // 2, 1) * 2 * C, device=dev)
+            tb = max(self.nat.bn_bwd_tiles(M, C), _ceil(M, self.nat.conv_gemm_bm(M, C)))
+            b.bpart = torch.empty(tb * 2 * C, device=dev)
+            b.bgpart = torch.empty(max(tb // 2, 1) * 2 * C, device=dev)
         max_c = max(b.spec.channels for b in self.bns.values())
         self.coef = torch.empty(3 * max_c, device=dev)
         # per-conv split-K partial slabs (persist until the bucket's grouped reduce)
@@ -447,7 +452,7 @@ class Engine:
                        0 if residual is None else residual.data_ptr(),
                        0 if pre is None else pre.scale.data_ptr(),
                        0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [],
-                       fin, [], pfin, BN_DECAY, BN_EPS, 1)
+                       fin, [], pfin, [], BN_DECAY, BN_EPS, 1)
 
     def _bn_finalize(self, plan, bn: _BN, train=True, consumer_conv: bool = True):
         """Called where the BN's statistics are next needed.  Deferred to the first
@@ -474,17 +479,64 @@ class Engine:
 
     def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False,
                   bnb: tuple | None = None):
-        """wgrad (+reduce into the flat gradient) and optionally dgrad into dx.
+        """dgrad into dx (optional), then wgrad (+ reduce into the flat gradient).
 
         ``bnb=(bn, bn_input)``: the dgrad epilogue also emits that BN's backward
-        partials (sum g, sum g*xhat of dx) into bwd_part."""
+        partial sums (sum g, sum g*xhat of dx).  If ``dy`` is the output of a
+        pending BN backward (_bn_bwd), the direct dgrad applies that BN backward
+        while staging dy (BnBwdPre) and materializes dy for the wgrad."""
         geom = self._geom(c, N)
-        off, sp, pps = self.wg_off[c.spec.name]
-        part = self.wg_part.data_ptr() + 4 * off
+        s = c.spec
+        abw = []
+        a_src = dy
+        pb = self._pending_bwd
+        if pb is not None:
+            if (pb["out"] is dy and dx is not None and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
+                    and self.nat.conv_direct_covers(1, geom)
+                    and pb["cnt"] <= self._consumer_cap(s.cout)):
+                bn = pb["bn"]
+                add = pb["add"]
+                abw = [pb["x"].data_ptr(), 0 if add is None else add.data_ptr(),
+                       bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
+                       bn.shift.data_ptr(), bn.gamma, pb["part"], pb["cnt"], dy.data_ptr(),
+                       bn.dgamma, bn.dbeta, self.coef.data_ptr()]
+                self._produced.update(bn.names)
+                self._pending_bwd = None
+                a_src = pb["da"]        # the dgrad stages BNbwd(da) and writes dy itself
+            else:
+                self._emit_bn_bwd(plan)
+        if dx is not None:
+            bl, bfl = [], []
+            if bnb is not None:
+                bn, bx = bnb
+                Mx = N * s.h * s.w
+                C = c.cin
+                bm, bnt = self.nat.conv_gemm_bm(Mx, C), self.nat.conv_gemm_bn(Mx, C)
+                T = _ceil(Mx, bm)
+                bl = [bx.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
+                      bn.shift.data_ptr(), bn.bpart.data_ptr()]
+                self._bnb_src = (bn.bpart.data_ptr(), T)
+                capc, capp = self._consumer_cap(C), (256 // bnt) * 8
+                if T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0":
+                    gs = 2
+                    while _ceil(T, gs) > capc:
+                        gs *= 2
+                    if gs <= capp:   # last arrivers fold groups of gs tiles for the consumer
+                        bfl = [self._counters(Mx, C, gs), bn.gamma, bn.rstd.data_ptr(),
+                               bn.dgamma, bn.dbeta, self.coef.data_ptr(),
+                               bn.bgpart.data_ptr(), gs, 1]
+                        self._bnb_src = (bn.bgpart.data_ptr(), _ceil(T, gs))
+            if "dgrad" not in _DIAG_SKIP:
+                plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0,
+                               0, int(accumulate), geom, bl, [], bfl, [], abw, BN_DECAY, BN_EPS,
+                               1)
         # The weight gradient only feeds the bucket's grouped reduce, so it runs on
         # the side stream, overlapping the dgrad -> BN-backward chain.  Forks are
         # batched per residual block (_flush_side): a cross-stream event pair costs
         # ~6 us of device time on ROCm, about a third of a CIFAR wgrad.
+        off, sp, pps = self.wg_off[s.name]
+        part = self.wg_part.data_ptr() + 4 * off
+
         def emit(plan=plan, dy=dy, x=x, pre=pre, part=part, geom=geom, sp=sp, pps=pps):
             if "wgrad" not in _DIAG_SKIP:   # diagnostics only (scripts/diag_step.py)
                 plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
@@ -494,49 +546,43 @@ class Engine:
             self._side_q.append(emit)
         else:
             emit()
-        s = c.spec
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         self._produced.add(c.name)
-        if dx is not None:
-            bl, bfl = [], []
-            if bnb is not None:
-                bn, bx = bnb
-                bl = [bx.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
-                      bn.shift.data_ptr(), self.bwd_part.data_ptr()]
-                Mx = N * s.h * s.w
-                self._bnb_tiles = _ceil(Mx, self.nat.conv_gemm_bm(Mx, c.cin))
-                grp = self._fuse_finalize(Mx, c.cin)
-                bmode = os.environ.get("DTR_FUSED_BN_BWD", "1")
-                if bmode == "0" or (bmode == "1" and grp):
-                    grp = None          # 1: single-level last arriver only
-                if grp is not None:
-                    bn.fused_bwd = True
-                    bfl = [self._counters(Mx, c.cin, grp), bn.gamma, bn.rstd.data_ptr(),
-                           bn.dgamma, bn.dbeta, self.coef.data_ptr(),
-                           self.bn_gpart[1].data_ptr(), grp]
-            if "dgrad" not in _DIAG_SKIP:
-                plan.conv_gemm(1, dy.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                               int(accumulate), geom, bl, [], bfl, [], BN_DECAY, BN_EPS, 1)
 
     def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None, reduced: bool = False):
-        """BN+ReLU backward.  ``reduced``: the producing dgrad already wrote the
-        partial sums (conv epilogue BNB), so only finalize + apply remain."""
+        """BN+ReLU backward dx = BNbwd(dy) (+ add).  ``reduced``: the producing dgrad
+        already wrote the partial sums (conv epilogue BNB).  The finalize + apply are
+        deferred: the next dgrad consuming dx applies them while staging its input
+        (_conv_bwd), else _emit_bn_bwd launches them."""
         C = bn.spec.channels
         M = x.numel() // C
+        if self._pending_bwd is not None:
+            self._emit_bn_bwd(plan)
         if reduced:
-            tiles = self._bnb_tiles
+            part, cnt = self._bnb_src
         else:
-            tiles = self.nat.bn_bwd_tiles(M, C)
+            cnt = self.nat.bn_bwd_tiles(M, C)
+            part = bn.bpart.data_ptr()
             plan.bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(),
                                bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(), M, C,
-                               self.bwd_part.data_ptr())
-        if not (reduced and bn.fused_bwd):
-            plan.bn_bwd_finalize(self.bwd_part.data_ptr(), tiles, M, C, bn.gamma,
-                                 bn.rstd.data_ptr(), bn.dgamma, bn.dbeta, self.coef.data_ptr())
+                               part)
+        self._pending_bwd = dict(bn=bn, da=dy, x=x, out=dx, add=add, part=part, cnt=cnt, M=M)
+
+    def _emit_bn_bwd(self, plan):
+        """Launch the pending BN backward's finalize + apply (no fusing consumer)."""
+        pb = self._pending_bwd
+        if pb is None:
+            return
+        self._pending_bwd = None
+        bn, M, C = pb["bn"], pb["M"], pb["bn"].spec.channels
+        plan.bn_bwd_finalize(pb["part"], pb["cnt"], M, C, bn.gamma, bn.rstd.data_ptr(),
+                             bn.dgamma, bn.dbeta, self.coef.data_ptr())
         self._produced.update(bn.names)
-        plan.bn_bwd_apply(dy.data_ptr(), x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(),
-                          bn.scale.data_ptr(), bn.shift.data_ptr(), self.coef.data_ptr(),
-                          0 if add is None else add.data_ptr(), dx.data_ptr(), M, C)
+        add = pb["add"]
+        plan.bn_bwd_apply(pb["da"].data_ptr(), pb["x"].data_ptr(), bn.mean.data_ptr(),
+                          bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(),
+                          self.coef.data_ptr(), 0 if add is None else add.data_ptr(),
+                          pb["out"].data_ptr(), M, C)
 
     def _flush_side(self, plan, force: bool = False):
         """Fork: emit the queued weight gradients on the side stream behind ONE event
@@ -662,7 +708,7 @@ class Engine:
         plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                             self.pooled.data_ptr(), N, HL * WL, F)
         plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
-                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], [], BN_DECAY, BN_EPS, 1)
+                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
@@ -675,6 +721,7 @@ class Engine:
         b1 = plan.size()
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
         self._side_q, self._side_blocks = [], 0
+        self._pending_bwd, self._bnb_src = None, None
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
         dpart = self.wg_part.data_ptr() + 4 * off
@@ -683,7 +730,7 @@ class Engine:
                                           spec.num_classes, 1, F, F)
         self._produced.add(self.dense_name)
         plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
-                       0, 0, 0, 0, 0, 0, dg, [], [], [], [], BN_DECAY, BN_EPS, 1)
+                       0, 0, 0, 0, 0, 0, dg, [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         dact = self._g(0, (N, HL, WL, F))
         plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
         d = 1
@@ -726,6 +773,7 @@ class Engine:
             self._flush_side(plan)
             self._flush_buckets(plan)
         # stem (no dgrad: the input needs no gradient)
+        self._emit_bn_bwd(plan)     # the stem's consumers (maxpool_bwd / wgrad) are not fusing
         if spec.maxpool:
             dstem = self._g((d + 1) % 3, tuple(self.stem_out.shape))
             st = spec.stem
@@ -929,7 +977,7 @@ class _EvalPlan:
                       bn.scale.data_ptr(), bn.shift.data_ptr())
         y = buf((N, st.ho, st.wo, st.cout))
         p.conv_gemm(0, self.x_in.data_ptr(), stem.ohwi, y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
-                    eng._geom(stem, N), [], [], [], [], BN_DECAY, BN_EPS, 1)
+                    eng._geom(stem, N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         if spec.maxpool:
             ph = _ceil(st.ho, 2)
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
@@ -959,7 +1007,7 @@ class _EvalPlan:
         p.bnrelu_avgpool(x.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
                          self.pooled.data_ptr(), N, x.shape[1] * x.shape[2], F)
         p.conv_gemm(0, self.pooled.data_ptr(), eng.dense_ohwi, 0, self.logits.data_ptr(), 0, 0, 0,
-                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], [], BN_DECAY, BN_EPS, 1)
+                    eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
                        spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
@@ -968,7 +1016,7 @@ class _EvalPlan:
     def _conv(self, p, c, x, out, pre, residual=None):
         p.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                     0 if residual is None else residual.data_ptr(), pre.scale.data_ptr(),
-                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [], [], [], [], BN_DECAY, BN_EPS, 1)
+                    pre.shift.data_ptr(), 0, 0, 0, 0, self.eng._geom(c, self.N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
 
     def run(self, images=None, labels=None, raw_u8: bool = True):
         """Returns (loss_sum, correct, probs[N, classes]) for one eval batch.

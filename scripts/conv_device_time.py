@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Device time per launch (incl. the ~1.5 us kernel boundary) of the CIFAR conv
+kernels, from a native Plan of 200 back-to-back launches timed with HIP events:
+direct fwd/dgrad/wgrad with each fusion toggled."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import distributed_tensorflow_resnet_amd as dtr  # noqa: E402
+from distributed_tensorflow_resnet_amd.ops import functional as fn  # noqa: E402
+
+BF = torch.bfloat16
+
+
+def dev_time(plan, reps=3):
+    st = torch.cuda.current_stream()
+    best = 1e9
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        plan.run(0, plan.size(), st.cuda_stream, st.cuda_stream)
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / plan.size())
+    return best
+
+
+def main():
+    nat = dtr.native()
+    dev = torch.device("cuda", 0)
+    n = 200
+    batch = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    for H, C in ((32, 16), (16, 32), (8, 64)):
+        N = batch
+        M = N * H * H
+        g = fn.ConvGeom(N, H, H, C, C, 3, 3, 1).as_list()
+        x = torch.randn(N, H, H, C, device=dev).to(BF)
+        w = torch.randn(C, 3, 3, C, device=dev).to(BF)
+        wh = w.permute(1, 2, 3, 0).contiguous()
+        y = torch.empty_like(x)
+        res = torch.randn_like(x)
+        sc, sh = torch.rand(C, device=dev), torch.rand(C, device=dev)
+        T = -(-M // nat.conv_gemm_bm(M, C))
+        part = torch.empty(T * 2 * C, device=dev)
+        bpart = torch.empty(T * 2 * C, device=dev)
+        sp, pps = nat.wgrad_pick_splits(g)
+        wpart = torch.empty(sp * 9 * C * C, device=dev)
+        res_line = []
+        variants = {
+            "fwd": dict(pre=False, stats=False, res=False),
+            "fwd+pre": dict(pre=True, stats=False, res=False),
+            "fwd+stats": dict(pre=False, stats=True, res=False),
+            "fwd+pre+stats+res": dict(pre=True, stats=True, res=True),
+        }
+        for name, v in variants.items():
+            p = nat.Plan()
+            for _ in range(n):
+                p.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0,
+                            res.data_ptr() if v["res"] else 0,
+                            sc.data_ptr() if v["pre"] else 0, sh.data_ptr() if v["pre"] else 0,
+                            0, 0, part.data_ptr() if v["stats"] else 0, 0, g, [], [], [], [], [],
+                            0.997, 1e-5, 1)
+            res_line.append(f"{name} {dev_time(p):.2f}")
+        for name, bnb in (("dgrad", False), ("dgrad+bnb", True)):
+            p = nat.Plan()
+            bl = [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                  bpart.data_ptr()] if bnb else []
+            for _ in range(n):
+                p.conv_gemm(1, res.data_ptr(), wh.data_ptr(), y.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
+                            0, g, bl, [], [], [], [], 0.997, 1e-5, 1)
+            res_line.append(f"{name} {dev_time(p):.2f}")
+        for name, pre in (("wgrad", False), ("wgrad+pre", True)):
+            p = nat.Plan()
+            for _ in range(n):
+                p.conv_wgrad(res.data_ptr(), x.data_ptr(), sc.data_ptr() if pre else 0,
+                             sh.data_ptr() if pre else 0, wpart.data_ptr(), g, sp, pps)
+            res_line.append(f"{name} {dev_time(p):.2f}")
+        p = nat.Plan()
+        for _ in range(n):
+            p.fill(sc.data_ptr(), C, 1.0)
+        res_line.append(f"fill {dev_time(p):.2f}")
+        print(f"N={N} H={H} C={C} (us/launch): " + " | ".join(res_line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

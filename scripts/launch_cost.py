@@ -45,7 +45,7 @@ def main():
     p = nat.Plan()
     for _ in range(n):
         p.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
-                    g.as_list(), [], [], [], [], 0.997, 1e-5, 1)
+                    g.as_list(), [], [], [], [], [], 0.997, 1e-5, 1)
     h, tot = host_time(p)
     print(f"conv launch: host {h / n * 1e6:.2f} us/launch (device+host {tot / n * 1e6:.2f})")
     # event record (main) + wait (side) pairs

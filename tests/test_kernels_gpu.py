@@ -370,7 +370,7 @@ def test_fused_last_arriver_bn_finalize(gpu, N, H, C, group):
         dg, db, coef = torch.empty(C, device=gpu), torch.empty(C, device=gpu), \
             torch.empty(3 * C, device=gpu)
         fn.conv2d_dgrad(dy, w, tuple(x.shape), 1, bnb=(x, mean, rstd, scale, shift, bpart),
-                        bfin=[cnt, gamma, rstd, dg, db, coef, gpart, group])
+                        bfin=[cnt, gamma, rstd, dg, db, coef, gpart, group, 0])
         p = bpart.view(tiles, 2, C).sum(0)
         torch.testing.assert_close(db, p[0], rtol=1e-4, atol=1e-3)
         torch.testing.assert_close(dg, p[1], rtol=1e-4, atol=1e-3)
@@ -449,3 +449,52 @@ def test_direct_wgrad_matches_reference_and_generic(gpu, N, H, C):
     ref.conv2d(a, w, 1).backward(dy.float())
     assert _rel(dw, w.grad) < 1e-3
     assert _rel(dw, dw_gen) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,C,with_add", [(8, 32, 16, True), (128, 32, 16, False),
+                                            (16, 16, 32, True), (16, 8, 64, False)])
+def test_direct_dgrad_fused_bn_backward(gpu, N, H, C, with_add):
+    """BnBwdPre: the direct dgrad applies the pending BN+ReLU backward to its input
+    while staging (dh = a*g - b - c*xhat + add, coefficients combined from the
+    producer's partial sums), writes dh, and == bn_bwd_finalize + bn_bwd_apply + dgrad."""
+    torch.manual_seed(15)
+    nat = fn.native()
+    M = N * H * H
+    da = torch.randn(N, H, H, C, device=gpu).to(BF)          # grad wrt relu(bn(x))
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)           # BN input
+    add = torch.randn(N, H, H, C, device=gpu).to(BF) if with_add else None
+    w = (torch.randn(3, 3, C, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    mean = torch.randn(C, device=gpu) * 0.1
+    rstd = torch.rand(C, device=gpu) + 0.5
+    gamma = torch.rand(C, device=gpu) + 0.5
+    scale = gamma * rstd
+    shift = torch.randn(C, device=gpu) * 0.2 - mean * scale
+    # partial sums (sum g, sum g*xhat) in 16 row blocks, as a producer epilogue would
+    xf, gf = x.float().reshape(-1, C), da.float().reshape(-1, C)
+    g = gf * ((xf * scale + shift) > 0).float()
+    xh = (xf - mean) * rstd
+    cnt = 16
+    part = torch.stack([torch.stack([gg.sum(0), (gg * hh).sum(0)])
+                        for gg, hh in zip(g.chunk(cnt), xh.chunk(cnt))]).contiguous()
+    dh = torch.empty_like(da)
+    dg, db, coef = (torch.empty(n, device=gpu) for n in (C, C, 3 * C))
+    dx = fn.conv2d_dgrad(da, w, tuple(x.shape), 1,
+                         abwd=[x, 0 if add is None else add, mean, rstd, scale, shift, gamma,
+                               part, cnt, dh, dg, db, coef])
+    assert nat.conv_direct_covers(1, [N, H, H, C, H, H, C, 3, 3, 1, 1])
+    # reference: separate finalize + apply, then the plain dgrad of the applied tensor
+    dg2, db2, coef2 = (torch.empty(n, device=gpu) for n in (C, C, 3 * C))
+    nat.bn_bwd_finalize(part.data_ptr(), cnt, M, C, gamma.data_ptr(), rstd.data_ptr(),
+                        dg2.data_ptr(), db2.data_ptr(), coef2.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    dh2 = torch.empty_like(da)
+    nat.bn_bwd_apply(da.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                     scale.data_ptr(), shift.data_ptr(), coef2.data_ptr(),
+                     0 if add is None else add.data_ptr(), dh2.data_ptr(), M, C,
+                     torch.cuda.current_stream().cuda_stream)
+    torch.testing.assert_close(dg, dg2, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db, db2, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(coef, coef2, rtol=1e-5, atol=1e-6)
+    assert (dh.float() - dh2.float()).abs().max().item() <= 2 * 2 ** -8 * dh2.float().abs().max().item()
+    dx2 = fn.conv2d_dgrad(dh2, w, tuple(x.shape), 1)
+    assert _rel(dx, dx2) < 5e-3
