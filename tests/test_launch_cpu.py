@@ -1,0 +1,58 @@
+"""The launch/ shell scripts (MI355X equivalents of the reference's docker /
+mpirun / SLURM launchers) on the CPU: syntax of every script, the localhost gloo
+pseudo-cluster, and start -> checkpoint -> stop of a background run with its
+side-car evaluator."""
+import glob
+import os
+import subprocess
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_scripts_parse():
+    files = glob.glob(os.path.join(ROOT, "launch", "*.sh")) + \
+        glob.glob(os.path.join(ROOT, "launch", "slurm", "*.sbatch"))
+    assert len(files) >= 9
+    for f in files:
+        r = subprocess.run(["bash", "-n", f], capture_output=True, text=True)
+        assert r.returncode == 0, (f, r.stderr)
+
+
+def test_local_cpu_pseudo_cluster(tmp_path):
+    env = dict(os.environ, NPROC="2", STEPS="3", RUN_DIR=str(tmp_path), MASTER_PORT="29643",
+               LOG_EVERY="1", SAVE_STEPS="3")
+    r = subprocess.run(["bash", os.path.join(ROOT, "launch", "run_local_cpu.sh")], env=env,
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert os.path.exists(tmp_path / "ckpt" / "checkpoint")
+
+
+def test_start_and_stop_background_run(tmp_path):
+    env = dict(os.environ, GPUS="2", GLOBAL_BATCH="8", RESNET_SIZE="8", TRAIN_STEPS="1000000",
+               DEVICE="cpu", RUN_DIR=str(tmp_path), MASTER_PORT="29644", SYNTHETIC="1",
+               EXTRA_ARGS="--dtype fp32 --save_checkpoint_steps 2 --log_every 1")
+    r = subprocess.run(["bash", os.path.join(ROOT, "launch", "start-resnet-cifar-main.sh")],
+                       env=env, capture_output=True, text=True, timeout=60, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    pids = {os.path.basename(f)[:-4]: int(open(f).read()) for f in
+            glob.glob(str(tmp_path / "*.pid"))}
+    assert set(pids) == {"train", "eval"}
+    try:
+        deadline = time.time() + 300
+        while time.time() < deadline and not os.path.exists(tmp_path / "ckpt" / "checkpoint"):
+            time.sleep(1)
+        assert os.path.exists(tmp_path / "ckpt" / "checkpoint"), \
+            open(tmp_path / "logs" / "train.log").read()[-3000:]
+    finally:
+        s = subprocess.run(["bash", os.path.join(ROOT, "launch", "stop.sh"), str(tmp_path)],
+                           capture_output=True, text=True, timeout=120)
+    assert s.returncode == 0, s.stderr
+    for pid in pids.values():
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive
+    assert not glob.glob(str(tmp_path / "*.pid"))
