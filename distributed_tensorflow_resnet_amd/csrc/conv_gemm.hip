@@ -155,10 +155,14 @@ conv_gemm_kernel(GemmArgs args) {
   auto store_tile = [&](int buf, int t) {
     bf16* A = As + buf * BM * BK;
     bf16* B = Bs + buf * BN * BK;
-    int ci = 0;
+    f32x4 s0, s1, b0, b1;   // this thread's 8 channels: one table read for all its chunks
     if constexpr (PRE) {
       const int k = t * BK + kg * 8;
-      ci = k - (k / Acin) * Acin;
+      const int ci = k < KD ? k - (k / Acin) * Acin : 0;
+      s0 = *reinterpret_cast<const f32x4*>(pre_s + ci);
+      s1 = *reinterpret_cast<const f32x4*>(pre_s + ci + 4);
+      b0 = *reinterpret_cast<const f32x4*>(pre_s + Acin + ci);
+      b1 = *reinterpret_cast<const f32x4*>(pre_s + Acin + ci + 4);
     }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
@@ -167,7 +171,7 @@ conv_gemm_kernel(GemmArgs args) {
         const int r = q >> 3;
         bf16x8 v = ra[i];
         if constexpr (PRE) {
-          if ((amask >> i) & 1u) v = affine_relu8(v, pre_s + ci, pre_s + Acin + ci);
+          if ((amask >> i) & 1u) v = affine_relu8_reg(v, s0, s1, b0, b1);
         }
         *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
       }

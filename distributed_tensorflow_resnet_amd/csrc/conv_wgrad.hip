@@ -70,7 +70,9 @@ conv_wgrad_kernel(WgradArgs args) {
   const bf16x8 zero8 = {};
   const int HoWo = g.Ho * g.Wo;
 
+  unsigned bmask = 0;   // PRE: which B chunks of the in-flight tile are real pixels
   auto load_tile = [&](int t) {
+    if constexpr (PRE) bmask = 0;
     const int pbase = p_begin + t * BK;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
@@ -98,7 +100,7 @@ conv_wgrad_kernel(WgradArgs args) {
         if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
           v = *reinterpret_cast<const bf16x8*>(
               args.x + ((long)(img * g.H + hi) * g.W + wi) * Cin + ci);
-          if constexpr (PRE) v = affine_relu8(v, pre_s + ci, pre_s + Cin + ci);
+          if constexpr (PRE) bmask |= 1u << i;   // BN+ReLU applied at LDS-store time
         }
       }
       rb[i] = v;
@@ -123,7 +125,18 @@ conv_wgrad_kernel(WgradArgs args) {
       if (q < B_CH) {
         const int row = q / B_CPR, cc = q % B_CPR;
         const int col = (((cc >> 1) ^ unit_swz<UB>(row)) << 4) + ((cc & 1) << 3);
-        *reinterpret_cast<bf16x8*>(B + row * BN + col) = rb[i];
+        bf16x8 v = rb[i];
+        if constexpr (PRE) {
+          if ((bmask >> i) & 1u) {
+            const int n = n0 + cc * 8;
+            const int ci = n - (n / Cin) * Cin;
+            v = affine_relu8_reg(v, *reinterpret_cast<const f32x4*>(pre_s + ci),
+                                 *reinterpret_cast<const f32x4*>(pre_s + ci + 4),
+                                 *reinterpret_cast<const f32x4*>(pre_s + Cin + ci),
+                                 *reinterpret_cast<const f32x4*>(pre_s + Cin + ci + 4));
+          }
+        }
+        *reinterpret_cast<bf16x8*>(B + row * BN + col) = v;
       }
     }
   };

@@ -32,21 +32,28 @@ def main():
     dev = torch.device("cuda", 0)
     n = 200
     batch = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-    for H, C in ((32, 16), (16, 32), (8, 64)):
+    shapes = [(32, 16, 16, 3), (16, 32, 32, 3), (8, 64, 64, 3)]   # (H, C, K, k)
+    if len(sys.argv) > 2 and sys.argv[2] == "imagenet":
+        n = 20
+        shapes = [(56, 64, 256, 1), (56, 64, 64, 3), (28, 128, 128, 3), (14, 256, 256, 3),
+                  (14, 1024, 256, 1), (7, 512, 2048, 1)]
+    for H, C, K, k in shapes:
         N = batch
         M = N * H * H
-        g = fn.ConvGeom(N, H, H, C, C, 3, 3, 1).as_list()
+        g = fn.ConvGeom(N, H, H, C, K, k, k, 1).as_list()
         x = torch.randn(N, H, H, C, device=dev).to(BF)
-        w = torch.randn(C, 3, 3, C, device=dev).to(BF)
+        w = torch.randn(K, k, k, C, device=dev).to(BF)
         wh = w.permute(1, 2, 3, 0).contiguous()
-        y = torch.empty_like(x)
-        res = torch.randn_like(x)
-        sc, sh = torch.rand(C, device=dev), torch.rand(C, device=dev)
-        T = -(-M // nat.conv_gemm_bm(M, C))
-        part = torch.empty(T * 2 * C, device=dev)
-        bpart = torch.empty(T * 2 * C, device=dev)
+        y = torch.empty(N, H, H, K, device=dev, dtype=BF)
+        res = torch.randn_like(y)
+        dxb = torch.empty_like(x)
+        sc, sh = torch.rand(max(C, K), device=dev), torch.rand(max(C, K), device=dev)
+        T = -(-M // nat.conv_gemm_bm(M, K))
+        part = torch.empty(T * 2 * K, device=dev)
+        Tb = -(-M // nat.conv_gemm_bm(M, C))
+        bpart = torch.empty(Tb * 2 * C, device=dev)
         sp, pps = nat.wgrad_pick_splits(g)
-        wpart = torch.empty(sp * 9 * C * C, device=dev)
+        wpart = torch.empty(sp * k * k * C * K, device=dev)
         res_line = []
         variants = {
             "fwd": dict(pre=False, stats=False, res=False),
@@ -68,7 +75,7 @@ def main():
             bl = [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(), sh.data_ptr(),
                   bpart.data_ptr()] if bnb else []
             for _ in range(n):
-                p.conv_gemm(1, res.data_ptr(), wh.data_ptr(), y.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
+                p.conv_gemm(1, res.data_ptr(), wh.data_ptr(), dxb.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
                             0, g, bl, [], [], [], [], 0.997, 1e-5, 1)
             res_line.append(f"{name} {dev_time(p):.2f}")
         for name, pre in (("wgrad", False), ("wgrad+pre", True)):
@@ -81,7 +88,9 @@ def main():
         for _ in range(n):
             p.fill(sc.data_ptr(), C, 1.0)
         res_line.append(f"fill {dev_time(p):.2f}")
-        print(f"N={N} H={H} C={C} (us/launch): " + " | ".join(res_line), flush=True)
+        flop = 2.0 * M * K * k * k * C
+        print(f"N={N} H={H} C={C} K={K} k={k} ({flop / 1e9:.1f} GF; us/launch): " +
+              " | ".join(res_line), flush=True)
 
 
 if __name__ == "__main__":
