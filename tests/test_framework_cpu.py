@@ -241,3 +241,31 @@ def test_resnet_model_api_and_mlp():
         lr.train_op()
         lr.build_graph()
     assert float(lr.cost) < c0
+
+
+def test_model_registry_template(tmp_path):
+    """models/basic_model.py: the reference's BasicAgent template + make_model registry."""
+    from distributed_tensorflow_resnet_amd.models.basic_model import (MLPModel, ResNetModel,
+                                                                      get_model_class, make_model)
+    cfg = {"model_name": "ResNetModel", "dataset": "cifar10", "resnet_size": 8, "batch_size": 4,
+           "max_iter": 2, "steps_per_epoch": 1, "result_dir": str(tmp_path / "r"),
+           "device": "cpu"}
+    m = make_model(cfg)
+    assert isinstance(m, ResNetModel) and get_model_class(cfg) is ResNetModel
+    m.train(save_every=1)
+    assert m.global_step() == 2
+    assert (tmp_path / "r" / "config.json").exists()
+    probs = m.infer(torch.randint(0, 256, (4, 3, 32, 32), dtype=torch.uint8))
+    assert probs.shape[0] == 4
+    m2 = make_model(cfg)                       # init() restores the latest checkpoint
+    assert m2.global_step() == 2
+    mlp = make_model({"model_name": "MLPModel", "max_iter": 1, "steps_per_epoch": 3,
+                      "result_dir": str(tmp_path / "m")})
+    assert isinstance(mlp, MLPModel)
+    mlp.train()
+    assert make_model({"model_name": "MLPModel", "result_dir": str(tmp_path / "m")}).global_step() == 3
+    import pytest
+    with pytest.raises(KeyError):
+        make_model({"model_name": "SomeOtherModel"})
+    import models  # reference package path
+    assert models.make_model is make_model and models.get_model_class(cfg) is ResNetModel
