@@ -229,6 +229,28 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     const int prow0 = m0 + ph * EL::PR;
     const int nph = min(EL::PR, M - prow0);   // block-uniform
     if (nph <= 0) break;
+    // Operand loads of this phase's rows, all issued before the staging writes and
+    // the barrier so they overlap them (one round trip, not one per row iteration);
+    // kernels that prefetched them at kernel start (EpiPre) skip this.
+    // (single-phase dgrad+BNB tiles only: elsewhere the extra registers cost more
+    // occupancy than the batching gains -- measured on the ImageNet shapes.)
+    constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
+    constexpr bool PREL = EpiPre<BM, BN, WM>::ON;
+    constexpr bool BATCH = EL::PHASES == 1 && BNB;
+    bf16x8 lres[BATCH ? RIT : 1], lacc[BATCH ? RIT : 1], lx[BATCH ? RIT : 1];
+    if (BATCH && !(PREL && pre)) {
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int r = r0 + it * EL::RPP;
+        if (!colok || r >= nph) continue;
+        const long o = (long)(prow0 + r) * NC + col0;
+        const int ii = BATCH ? it : 0;
+        if (args.residual) lres[ii] = *reinterpret_cast<const bf16x8*>(args.residual + o);
+        if (args.accumulate && !args.out_f32)
+          lacc[ii] = *reinterpret_cast<const bf16x8*>(args.out + o);
+        if constexpr (BNB) lx[ii] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+      }
+    }
     if ((wm * WTM) / EL::PR == ph) {
       const int rbase = wm * WTM - ph * EL::PR;
 #pragma unroll
@@ -249,7 +271,6 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // only AFTER the statistics' barriers: a __syncthreads() waits for every
     // outstanding store of the wave (vmcnt(0)), so storing first put a full
     // store round trip in the middle of the epilogue (~2 us per STATS/BNB conv).
-    constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
     bf16x8 ob[RIT];
     float p1[8];
 #pragma unroll
@@ -265,9 +286,9 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const long o = (long)row * NC + col0;
       if (args.residual) {
-        const bf16x8 rv = (EpiPre<BM, BN, WM>::ON && pre)
-                              ? pre->res[EpiPre<BM, BN, WM>::ON ? it : 0]
-                              : *reinterpret_cast<const bf16x8*>(args.residual + o);
+        const bf16x8 rv = (PREL && pre) ? pre->res[PREL ? it : 0]
+                          : BATCH ? lres[BATCH ? it : 0]
+                                  : *reinterpret_cast<const bf16x8*>(args.residual + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
       }
@@ -287,9 +308,9 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         continue;
       }
       if (args.accumulate) {
-        const bf16x8 av = (EpiPre<BM, BN, WM>::ON && pre)
-                              ? pre->acc[EpiPre<BM, BN, WM>::ON ? it : 0]
-                              : *reinterpret_cast<const bf16x8*>(args.out + o);
+        const bf16x8 av = (PREL && pre) ? pre->acc[PREL ? it : 0]
+                          : BATCH ? lacc[BATCH ? it : 0]
+                                  : *reinterpret_cast<const bf16x8*>(args.out + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
       }
@@ -303,9 +324,9 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         for (int j = 0; j < 8; ++j) p1[j] += v[j];
       }
       if constexpr (BNB) {
-        const bf16x8 xv = (EpiPre<BM, BN, WM>::ON && pre)
-                              ? pre->x[EpiPre<BM, BN, WM>::ON ? it : 0]
-                              : *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+        const bf16x8 xv = (PREL && pre) ? pre->x[PREL ? it : 0]
+                          : BATCH ? lx[BATCH ? it : 0]
+                                  : *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xv[j];
