@@ -100,7 +100,73 @@ conv_gemm_kernel(GemmArgs args) {
   const bf16x8 zero8 = {};
 
   unsigned amask = 0;   // PRE: which A chunks of the in-flight tile are real pixels
+
+  // Fast gather (every A channel count a multiple of BK: all ImageNet layers but
+  // the stem): a K tile then lies inside ONE filter tap, so (tap, r, c) are
+  // wave-uniform scalars per k-step and each chunk needs only two adds, two
+  // unsigned compares and one 32-bit multiply-add -- instead of the per-chunk
+  // runtime divisions and exec-mask branches of the general path (which cost as
+  // many VALU cycles as the MFMAs).  Loads are buffer loads with a hardware range
+  // check: an invalid (padding) chunk gets an out-of-range offset and reads 0.
+  const long a_elems = (MODE == MODE_FWD) ? (long)g.N * g.H * g.W * g.C
+                                          : (long)g.N * g.Ho * g.Wo * g.K;
+  const long b_elems = (long)g.kh * g.kw * g.C * g.K;
+  const bool fast = (Acin % BK) == 0 && a_elems < (1L << 30) && b_elems < (1L << 30);
+  const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.a), 0,
+                                                      (int)(fast ? a_elems * 2 : 0), 0x00020000);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.b), 0,
+                                                      (int)(fast ? b_elems * 2 : 0), 0x00020000);
+  constexpr int kOOB = 0x7ffffff0;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  auto bload = [&](const __amdgpu_buffer_rsrc_t& rs, int byte_off) -> bf16x8 {
+    return __builtin_bit_cast(bf16x8, (u32x4)__builtin_amdgcn_raw_buffer_load_b128(rs, byte_off,
+                                                                                   0, 0));
+  };
+  auto load_tile_fast = [&](int t) {
+    if constexpr (PRE) amask = 0;
+    const int kb = t * BK;                       // uniform
+    const bool kv = kb < KD;
+    const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
+    const int ci = kb - tap * Acin + kg * 8;
+    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      int off = kOOB;
+      if constexpr (MODE == MODE_FWD) {
+        const int hi = a_h[i] + rr, wi = a_w[i] + cc;
+        if (kv && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W) {
+          off = ((a_base[i] + hi * g.W + wi) * g.C + ci) * 2;
+          if constexpr (PRE) amask |= 1u << i;
+        }
+      } else {
+        int hp = a_h[i] - rr, wp = a_w[i] - cc;
+        bool ok = kv && hp >= 0 && wp >= 0;
+        if (g.stride == 2) {
+          ok = ok && ((hp | wp) & 1) == 0;
+          hp >>= 1;
+          wp >>= 1;
+        }
+        if (ok && hp < g.Ho && wp < g.Wo) off = ((a_base[i] + hp * g.Wo + wp) * g.K + ci) * 2;
+      }
+      ra[i] = bload(rs_a, off);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int nrow = q >> 3;
+      int off = kOOB;
+      if (q < B_CHUNKS && n0 + nrow < NC && kv) {
+        if constexpr (MODE == MODE_FWD) off = ((n0 + nrow) * KD + kb + kg * 8) * 2;
+        else off = ((tap * g.C + (n0 + nrow)) * g.K + ci) * 2;
+      }
+      rb[i] = bload(rs_b, off);
+    }
+  };
   auto load_tile = [&](int t) {
+    if (fast) {
+      load_tile_fast(t);
+      return;
+    }
     if constexpr (PRE) amask = 0;
     const int k = t * BK + kg * 8;
     const bool kvalid = k < KD;
