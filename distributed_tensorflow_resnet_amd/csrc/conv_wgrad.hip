@@ -71,7 +71,84 @@ conv_wgrad_kernel(WgradArgs args) {
   const int HoWo = g.Ho * g.Wo;
 
   unsigned bmask = 0;   // PRE: which B chunks of the in-flight tile are real pixels
+
+  // Incremental im2col state: a thread's B chunks keep their column n (so tap and
+  // ci are fixed for the whole K loop) and their pixel rows advance by BK each
+  // k-step, so (img, ho, wo) are stepped by the launch constants (BK / Wo, BK % Wo)
+  // instead of re-derived with 4 runtime divisions per chunk per k-step.  Loads are
+  // range-checked buffer loads (invalid chunk -> out-of-range offset -> 0), so there
+  // are no exec-mask branches around them.
+  const long x_elems = (long)g.N * g.H * g.W * Cin;
+  const long dy_elems = (long)P * Cout;
+  const bool fast = x_elems < (1L << 30) && dy_elems < (1L << 30);
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.x), 0,
+                                                      (int)(fast ? x_elems * 2 : 0), 0x00020000);
+  const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.dy), 0,
+                                                       (int)(fast ? dy_elems * 2 : 0), 0x00020000);
+  constexpr int kOOB = 0x7ffffff0;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  auto bload = [&](const __amdgpu_buffer_rsrc_t& rs, int byte_off) -> bf16x8 {
+    return __builtin_bit_cast(bf16x8, (u32x4)__builtin_amdgcn_raw_buffer_load_b128(rs, byte_off,
+                                                                                   0, 0));
+  };
+  // per-thread B-chunk state (all of a thread's chunks share the column: B_CPR | 256)
+  const int bcc = tid % B_CPR;
+  const int bn_ = n0 + bcc * 8;
+  const bool bcol_ok = bn_ < NT;
+  const int btap = bcol_ok ? bn_ / Cin : 0, bci = bn_ - btap * Cin;
+  const int bdr = btap / g.kw, bdc = btap - bdr * g.kw;
+  const int d_ho = BK / g.Wo, d_wo = BK - d_ho * g.Wo;
+  int b_img[B_PER_T], b_ho[B_PER_T], b_wo[B_PER_T];
+#pragma unroll
+  for (int i = 0; i < B_PER_T; ++i) {
+    const int p = p_begin + (tid + i * 256) / B_CPR;
+    b_img[i] = p / HoWo;
+    const int rem = p - b_img[i] * HoWo;
+    b_ho[i] = rem / g.Wo;
+    b_wo[i] = rem - b_ho[i] * g.Wo;
+  }
+  auto load_tile_fast = [&](int t) {
+    if constexpr (PRE) bmask = 0;
+    const int pbase = p_begin + t * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int row = q / A_CPR, cc = q % A_CPR;
+      const int p = pbase + row;
+      const int off = (q < A_CH && p < p_end && m0 + cc * 8 < Cout)
+                          ? (p * Cout + m0 + cc * 8) * 2 : kOOB;
+      ra[i] = bload(rs_dy, off);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int p = pbase + q / B_CPR;
+      const int hi = b_ho[i] * g.stride - g.pad + bdr, wi = b_wo[i] * g.stride - g.pad + bdc;
+      int off = kOOB;
+      if (q < B_CH && p < p_end && bcol_ok && (unsigned)hi < (unsigned)g.H &&
+          (unsigned)wi < (unsigned)g.W) {
+        off = (((b_img[i] * g.H + hi) * g.W + wi) * Cin + bci) * 2;
+        if constexpr (PRE) bmask |= 1u << i;
+      }
+      rb[i] = bload(rs_x, off);
+      // advance this chunk's pixel by BK for the next k-step
+      b_wo[i] += d_wo;
+      b_ho[i] += d_ho;
+      if (b_wo[i] >= g.Wo) {
+        b_wo[i] -= g.Wo;
+        b_ho[i] += 1;
+      }
+      if (b_ho[i] >= g.Ho) {
+        b_img[i] += b_ho[i] / g.Ho;
+        b_ho[i] -= (b_ho[i] / g.Ho) * g.Ho;
+      }
+    }
+  };
   auto load_tile = [&](int t) {
+    if (fast) {
+      load_tile_fast(t);
+      return;
+    }
     if constexpr (PRE) bmask = 0;
     const int pbase = p_begin + t * BK;
 #pragma unroll
