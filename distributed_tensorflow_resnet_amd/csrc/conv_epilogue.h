@@ -232,23 +232,19 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // Operand loads of this phase's rows, all issued before the staging writes and
     // the barrier so they overlap them (one round trip, not one per row iteration);
     // kernels that prefetched them at kernel start (EpiPre) skip this.
-    // (single-phase dgrad+BNB tiles only: elsewhere the extra registers cost more
-    // occupancy than the batching gains -- measured on the ImageNet shapes.)
+    // (the BN-input loads of dgrad+BNB only: batching the residual / accumulate
+    // loads cost more occupancy than it gained -- measured on the ImageNet shapes.)
     constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
     constexpr bool PREL = EpiPre<BM, BN, WM>::ON;
-    constexpr bool BATCH = EL::PHASES == 1 && BNB;
-    bf16x8 lres[BATCH ? RIT : 1], lacc[BATCH ? RIT : 1], lx[BATCH ? RIT : 1];
+    constexpr bool BATCH = BNB;
+    bf16x8 lx[BATCH ? RIT : 1];
     if (BATCH && !(PREL && pre)) {
 #pragma unroll
       for (int it = 0; it < RIT; ++it) {
         const int r = r0 + it * EL::RPP;
         if (!colok || r >= nph) continue;
         const long o = (long)(prow0 + r) * NC + col0;
-        const int ii = BATCH ? it : 0;
-        if (args.residual) lres[ii] = *reinterpret_cast<const bf16x8*>(args.residual + o);
-        if (args.accumulate && !args.out_f32)
-          lacc[ii] = *reinterpret_cast<const bf16x8*>(args.out + o);
-        if constexpr (BNB) lx[ii] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+        if constexpr (BNB) lx[BATCH ? it : 0] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
       }
     }
     if ((wm * WTM) / EL::PR == ph) {
@@ -287,8 +283,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       const long o = (long)row * NC + col0;
       if (args.residual) {
         const bf16x8 rv = (PREL && pre) ? pre->res[PREL ? it : 0]
-                          : BATCH ? lres[BATCH ? it : 0]
-                                  : *reinterpret_cast<const bf16x8*>(args.residual + o);
+                                        : *reinterpret_cast<const bf16x8*>(args.residual + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
       }
@@ -309,8 +304,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
       if (args.accumulate) {
         const bf16x8 av = (PREL && pre) ? pre->acc[PREL ? it : 0]
-                          : BATCH ? lacc[BATCH ? it : 0]
-                                  : *reinterpret_cast<const bf16x8*>(args.out + o);
+                                        : *reinterpret_cast<const bf16x8*>(args.out + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)av[j];
       }

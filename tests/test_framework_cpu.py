@@ -269,3 +269,42 @@ def test_model_registry_template(tmp_path):
         make_model({"model_name": "SomeOtherModel"})
     import models  # reference package path
     assert models.make_model is make_model and models.get_model_class(cfg) is ResNetModel
+
+
+def test_imagenet_predict_tool(tmp_path):
+    """resnet_imagenet_predict.py (reference resnet_imagenet_predict.ipynb): restore an
+    ImageNet checkpoint on the CPU path, print top-5 with the reference's label-file format."""
+    from distributed_tensorflow_resnet_amd.models.spec import build_spec
+    from distributed_tensorflow_resnet_amd.train.backends import make_backend
+    from distributed_tensorflow_resnet_amd.train.engine import constant_lr
+    from distributed_tensorflow_resnet_amd.utils.checkpoint import Saver
+    import resnet_imagenet_predict as rip
+
+    spec = build_spec("imagenet", 18)
+    be = make_backend(spec, 2, device="cpu", weight_decay=1e-4, lr_schedule=constant_lr(0.1))
+    Saver(str(tmp_path)).save(be.state_tensors(), 0)
+    lab = tmp_path / "labels.txt"
+    lab.write_text("{0: 'tench, Tinca tinca',\n" + "".join(f" {i}: 'class{i}',\n" for i in range(1, 999))
+                   + " 999: 'toilet tissue'}\n")
+    assert rip.read_labels(str(lab))[0] == "tench, Tinca tinca" and len(rip.read_labels(str(lab))) == 1000
+    buf = io.StringIO()
+    import contextlib
+    with contextlib.redirect_stdout(buf):
+        rc = rip.main(["--train_dir", str(tmp_path), "--resnet_size", "18", "--num_images", "2",
+                       "--device", "cpu", "--labels_file", str(lab)])
+    assert rc == 0
+    out = buf.getvalue()
+    assert out.count("top-5") == 2 and "top-1 precision" in out
+
+
+def test_notebooks_are_valid():
+    """notebooks/*.ipynb (the reference's predict notebooks): valid nbformat-4 JSON whose
+    code cells parse."""
+    import ast
+    import json
+    for path in glob.glob(os.path.join(ROOT, "notebooks", "*.ipynb")):
+        nb = json.load(open(path))
+        assert nb["nbformat"] == 4
+        for c in nb["cells"]:
+            if c["cell_type"] == "code":
+                ast.parse("".join(c["source"]))
