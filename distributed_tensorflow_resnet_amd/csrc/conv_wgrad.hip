@@ -17,6 +17,8 @@
 // sums the slabs in fixed order (deterministic; no float atomics), writing the
 // TF HWIO layout of the master gradient.  Optional fused BN+ReLU is applied to
 // X while staging (the pre-activation tensor is never stored).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -316,9 +318,16 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   // ~768 workgroups (3 per CU) hide the per-tile load latency; cap the fp32
   // partial slabs at ~32 MB so the split-K reduce stays cheap, and keep >= 256
   // pixels (4 K-tiles) per split.  (Measured sweep: scripts/sweep_wgrad.py.)
-  long splits = (768 + tiles / 2) / tiles;
+  static long target = -1, cap_mb = -1;   // DTR_WGRAD_TARGET_WG / DTR_WGRAD_SLAB_MB (sweeps)
+  if (target < 0) {
+    const char* t = std::getenv("DTR_WGRAD_TARGET_WG");
+    const char* c = std::getenv("DTR_WGRAD_SLAB_MB");
+    target = t ? std::atol(t) : 768;
+    cap_mb = c ? std::atol(c) : 32;
+  }
+  long splits = (target + tiles / 2) / tiles;
   const long slab = (long)g.K * NT * 4;
-  const long cap_bytes = (32L << 20) / (slab > 0 ? slab : 1);
+  const long cap_bytes = (cap_mb << 20) / (slab > 0 ? slab : 1);
   if (splits > cap_bytes) splits = cap_bytes;
   long maxs = P / 256;
   if (maxs < 1) maxs = 1;

@@ -278,7 +278,7 @@ class Engine:
             e.rstd = self.bnbuf[total_c + off:total_c + off + C]
             e.scale = self.bnbuf[2 * total_c + off:2 * total_c + off + C]
             e.shift = self.bnbuf[3 * total_c + off:3 * total_c + off + C]
-            e.fused_fwd = e.fused_bwd = False
+            e.fused_fwd = False
             off += C
             self.bns[b.name] = e
 
@@ -322,20 +322,9 @@ class Engine:
         self.dpooled = torch.empty((N, F), dtype=BF16, device=dev)
         self.logits = torch.empty((N, self.kpad), device=dev)
         self.dlogits = torch.empty((N, self.kpad), dtype=BF16, device=dev)
-        # scratch: BN forward partials, BN backward partials, wgrad split-K slabs
-        max_stat = 1
-        max_bwd = 1
-        for b in list(self.bns.values()):
-            C = b.spec.channels
-            M = N * b.spec.h * b.spec.w
-            bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
-            max_stat = max(max_stat, _ceil(M, bm) * 2 * C)
-            tl = max(self.nat.bn_bwd_tiles(M, C), _ceil(M, self.nat.conv_gemm_bm(M, C)))
-            max_bwd = max(max_bwd, tl * 2 * C)
-        self.stat_part = torch.empty(max_stat, device=dev)
-        self.bwd_part = torch.empty(max_bwd, device=dev)
-        # per-BN forward partials: the BN's first consumer may combine them (BnPreFin)
-        # while the same kernel produces the next BN's partials, so no sharing
+        # scratch: per-BN forward / backward partials (the BN's first consumer may combine
+        # them -- BnPreFin / BnBwdPre -- while the same kernel produces the next BN's
+        # partials, so no sharing), wgrad split-K slabs
         for b in self.bns.values():
             C = b.spec.channels
             M = N * b.spec.h * b.spec.w
@@ -645,7 +634,7 @@ class Engine:
         plan, spec, N = self.plan, self.spec, self.N
         self.seg = {}
         for e in self.bns.values():
-            e.fused_fwd = e.fused_bwd = False
+            e.fused_fwd = False
             e.pending = None
         self._cnt_next = 0
         b0 = plan.size()
