@@ -295,6 +295,14 @@ static LrSchedule make_sched(float init, long long warm_steps, float warm_from, 
   return sc;
 }
 
+static Launch mk_ohwi_pack(ptr_t master, ptr_t segs, ptr_t tile0, int nseg, long long tiles,
+                           ptr_t bf) {
+  return [=](hipStream_t s) {
+    ohwi_pack(P<const float>(master), P<const ParamSeg>(segs), P<const long long>(tile0), nseg,
+              tiles, P<bf16>(bf), s);
+  };
+}
+
 static Launch mk_sgd_update_pack(ptr_t master, ptr_t grad, ptr_t mom, long n, float init,
                                  long long warm_steps, float warm_from, float warm_to,
                                  std::vector<long long> bounds, std::vector<float> vals,
@@ -465,6 +473,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "maxpool_fwd", mk_maxpool_fwd);
   def_op(m, plan, "maxpool_bwd", mk_maxpool_bwd);
   def_op(m, plan, "sgd_update_pack", mk_sgd_update_pack);
+  def_op(m, plan, "ohwi_pack", mk_ohwi_pack);
   def_op(m, plan, "step_increment", mk_step_increment);
   def_op(m, plan, "l2_half_sum", mk_l2_half_sum);
   def_op(m, plan, "fill", mk_fill);

@@ -66,25 +66,32 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
   const int tid = threadIdx.x;
   const int G = 256 / C;
   const int c = tid % C, q = tid / C;
+  // Division-free parallel combine about a common centre (Chan et al.): for items
+  // (n_i, mean_i, M2_i): N = sum n_i, mean = sum n_i mean_i / N,
+  // M2 = sum M2_i + sum n_i (mean_i - mean)^2 -- two passes over the registers
+  // instead of one dependent division per item (sequential Welford).
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (q < G) {
-    float mv[FIN_UNROLL], qv[FIN_UNROLL];
+    float mv[FIN_UNROLL], qv[FIN_UNROLL], nv[FIN_UNROLL];
 #pragma unroll
     for (int u = 0; u < FIN_UNROLL; ++u) {
       const int t = q + u * G;
-      mv[u] = t < P.cnt ? P.part[(long)t * 2 * C + c] : 0.f;
-      qv[u] = t < P.cnt ? P.part[(long)t * 2 * C + C + c] : 0.f;
+      const bool ok = t < P.cnt;
+      mv[u] = ok ? P.part[(long)t * 2 * C + c] : 0.f;
+      qv[u] = ok ? P.part[(long)t * 2 * C + C + c] : 0.f;
+      nv[u] = ok ? (float)min(P.rows_per, P.M - t * P.rows_per) : 0.f;
     }
+    float s = 0.f;
 #pragma unroll
     for (int u = 0; u < FIN_UNROLL; ++u) {
-      const int t = q + u * G;
-      if (t < P.cnt) {
-        const float nb = (float)min(P.rows_per, P.M - t * P.rows_per);
-        const float nn = n + nb, d = mv[u] - mu;
-        mu += d * nb / nn;
-        m2 += qv[u] + d * d * n * nb / nn;
-        n = nn;
-      }
+      n += nv[u];
+      s += nv[u] * mv[u];
+    }
+    mu = n > 0.f ? s / n : 0.f;
+#pragma unroll
+    for (int u = 0; u < FIN_UNROLL; ++u) {
+      const float d = mv[u] - mu;
+      m2 += qv[u] + nv[u] * d * d;
     }
     scratch[tid] = n;
     scratch[256 + tid] = mu;
@@ -92,17 +99,16 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
   }
   __syncthreads();
   if (q == 0) {
-    float fn_ = scratch[c], fmu = scratch[256 + c], fm2 = scratch[512 + c];
-    for (int k = 1; k < G; ++k) {
-      const float nb = scratch[k * C + c], mb = scratch[256 + k * C + c];
-      const float qb = scratch[512 + k * C + c];
-      const float nn = fn_ + nb;
-      if (nn > 0.f) {
-        const float d = mb - fmu;
-        fmu += d * nb / nn;
-        fm2 += qb + d * d * fn_ * nb / nn;
-        fn_ = nn;
-      }
+    float fn_ = 0.f, s = 0.f;
+    for (int k = 0; k < G; ++k) {
+      fn_ += scratch[k * C + c];
+      s += scratch[k * C + c] * scratch[256 + k * C + c];
+    }
+    const float fmu = s / fn_;
+    float fm2 = 0.f;
+    for (int k = 0; k < G; ++k) {
+      const float d = scratch[256 + k * C + c] - fmu;
+      fm2 += scratch[512 + k * C + c] + scratch[k * C + c] * d * d;
     }
     const float rs = rsqrtf(fm2 / fn_ + P.eps);
     const float sc = P.gamma[c] * rs;

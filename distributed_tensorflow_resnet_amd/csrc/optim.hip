@@ -38,19 +38,23 @@ __device__ __forceinline__ int find_seg(const ParamSeg* segs, int nseg, long e) 
   return lo;
 }
 
-__device__ __forceinline__ void write_copies(const ParamSeg& sg, long e, float w, bf16* bf) {
-  if (sg.bf_ohwi < 0 && sg.bf_hwio < 0) return;
+
+// HWIO bf16 copy of element e (contiguous with e: the master IS HWIO order).
+__device__ __forceinline__ void write_hwio(const ParamSeg& sg, long e, float w, bf16* bf) {
+  if (sg.bf_hwio < 0) return;
   const long local = e - sg.offset;
-  const int CK = sg.C * sg.K;
-  const int tap = (int)(local / CK);
-  const int rem = (int)(local - (long)tap * CK);
-  const int ci = rem / sg.K, co = rem - ci * sg.K;
-  const int taps = sg.kh * sg.kw;
-  const bf16 v = (bf16)w;
-  if (sg.bf_ohwi >= 0) bf[sg.bf_ohwi + ((long)co * taps + tap) * sg.cpad + ci] = v;
-  if (sg.bf_hwio >= 0) bf[sg.bf_hwio + ((long)tap * sg.C + ci) * sg.kpad + co] = v;
+  if (sg.kpad == sg.K) {
+    bf[sg.bf_hwio + local] = (bf16)w;
+  } else {
+    const long row = local / sg.K, co = local - row * sg.K;
+    bf[sg.bf_hwio + row * sg.kpad + co] = (bf16)w;
+  }
 }
 
+// The update itself: 4 consecutive elements per thread (16-B loads / stores of
+// w, grad, momentum; an 8-B store of the HWIO bf16 copy) with the parameter
+// segment tracked incrementally per thread (elements only move forward) instead
+// of a binary search per element.  The OHWI copy (a transpose) is ohwi_pack's.
 __global__ void __launch_bounds__(256)
 sgd_pack_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
                 long n, LrSchedule sched, const long long* __restrict__ gstep, float momentum,
@@ -58,21 +62,57 @@ sgd_pack_kernel(float* __restrict__ w, const float* __restrict__ g, float* __res
                 int nseg, bf16* __restrict__ bf, float* __restrict__ lr_out, int update) {
   const float lr = update ? lr_at(sched, gstep ? (long)*gstep : 0L) : 0.f;
   if (update && lr_out && blockIdx.x == 0 && threadIdx.x == 0) *lr_out = lr;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n;
-       e += (long)gridDim.x * blockDim.x) {
-    float wv = w[e];
-    if (update) {
-      const float gv = g[e] * grad_scale + wd * wv;
-      if (use_momentum) {
-        const float a = momentum * mom[e] + gv;
-        mom[e] = a;
-        wv -= lr * a;
-      } else {
-        wv -= lr * gv;
+  const long nv = (n + 3) / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  long v = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (v >= nv) return;
+  int sgi = find_seg(segs, nseg, v * 4);
+  for (; v < nv; v += stride) {
+    const long e0 = v * 4;
+    while (sgi + 1 < nseg && segs[sgi + 1].offset <= e0) ++sgi;
+    const ParamSeg& sg = segs[sgi];
+    const bool whole = e0 + 4 <= n && e0 + 4 <= sg.offset + sg.numel;
+    if (whole) {
+      f32x4 wv = *reinterpret_cast<const f32x4*>(w + e0);
+      if (update) {
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(g + e0) * grad_scale + wd * wv;
+        if (use_momentum) {
+          const f32x4 acc = momentum * *reinterpret_cast<const f32x4*>(mom + e0) + gv;
+          *reinterpret_cast<f32x4*>(mom + e0) = acc;
+          wv -= lr * acc;
+        } else {
+          wv -= lr * gv;
+        }
+        *reinterpret_cast<f32x4*>(w + e0) = wv;
       }
-      w[e] = wv;
+      if (bf && sg.bf_hwio >= 0) {
+        if (sg.kpad == sg.K && ((e0 - sg.offset) & 3) == 0) {
+          bf16x4 h = {(bf16)wv[0], (bf16)wv[1], (bf16)wv[2], (bf16)wv[3]};
+          *reinterpret_cast<bf16x4*>(bf + sg.bf_hwio + (e0 - sg.offset)) = h;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) write_hwio(sg, e0 + j, wv[j], bf);
+        }
+      }
+    } else {   // a vector straddling a segment end (e.g. a 10-class bias) or the tail
+      for (int j = 0; j < 4 && e0 + j < n; ++j) {
+        const long e = e0 + j;
+        const ParamSeg& sj = segs[find_seg(segs, nseg, e)];
+        float wj = w[e];
+        if (update) {
+          const float gj = g[e] * grad_scale + wd * wj;
+          if (use_momentum) {
+            const float acc = momentum * mom[e] + gj;
+            mom[e] = acc;
+            wj -= lr * acc;
+          } else {
+            wj -= lr * gj;
+          }
+          w[e] = wj;
+        }
+        if (bf) write_hwio(sj, e, wj, bf);
+      }
     }
-    if (bf) write_copies(segs[find_seg(segs, nseg, e)], e, wv, bf);
   }
 }
 
@@ -80,11 +120,59 @@ void sgd_update_pack(float* master, const float* grad, float* mom, long n, const
                      const long long* gstep, float momentum, float wd, float grad_scale,
                      int use_momentum, const ParamSeg* segs, int nseg, bf16* bf, float* lr_out,
                      int update, hipStream_t st) {
-  long blocks = (n + 255) / 256;
+  long blocks = ((n + 3) / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sgd_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, st, master, grad, mom,
                      n, s, gstep, momentum, wd, grad_scale, use_momentum, segs, nseg, bf, lr_out,
                      update);
+  DTR_CHECK_LAUNCH();
+}
+
+// OHWI bf16 copies of every weight: a tiled transpose of the fp32 master
+// ([tap*C + ci][co], HWIO) into [co][tap*cpad + ci] through LDS so both the
+// reads (along co) and the writes (along tap*C + ci) are coalesced -- the per-
+// element scattered 2-byte stores of the fused form were most of the optimizer
+// launch's time on ImageNet.  tile0[s] = first tile of segment s (prefix over
+// ceil(taps*C/64) x ceil(K/64) tiles; segments without an OHWI copy have 0 tiles).
+__global__ void __launch_bounds__(256)
+ohwi_pack_kernel(const float* __restrict__ w, const ParamSeg* __restrict__ segs,
+                 const long long* __restrict__ tile0, int nseg, bf16* __restrict__ bf) {
+  __shared__ bf16 tile[64][66];
+  const long long b = blockIdx.x;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tile0[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const ParamSeg& sg = segs[lo];
+  const int taps = sg.kh * sg.kw;
+  const int R = taps * sg.C;                 // HWIO rows (tap, ci)
+  const int tc_n = (sg.K + 63) / 64;
+  const int t = (int)(b - tile0[lo]);
+  const int tr = t / tc_n, tcol = t - tr * tc_n;
+  const int r0 = tr * 64, c0 = tcol * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {         // read rows r0+i, cols c0+tx (coalesced)
+    const int r = r0 + i, co = c0 + tx;
+    tile[i][tx] = (r < R && co < sg.K) ? (bf16)w[sg.offset + (long)r * sg.K + co] : (bf16)0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {         // write rows co = c0+i, cols r0+tx (coalesced)
+    const int co = c0 + i, r = r0 + tx;
+    if (co < sg.K && r < R) {
+      const int tap = r / sg.C, ci = r - tap * sg.C;
+      bf[sg.bf_ohwi + ((long)co * taps + tap) * sg.cpad + ci] = tile[tx][i];
+    }
+  }
+}
+
+void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0, int nseg,
+               long long total_tiles, bf16* bf, hipStream_t s) {
+  if (total_tiles <= 0) return;
+  hipLaunchKernelGGL(ohwi_pack_kernel, dim3((unsigned)total_tiles), dim3(256), 0, s, master,
+                     segs, tile0, nseg, bf);
   DTR_CHECK_LAUNCH();
 }
 

@@ -234,6 +234,12 @@ class Engine:
         assert SEG_DTYPE.itemsize == self.nat.param_seg_bytes()
         self.segs = torch.from_numpy(seg_arr.view(np.uint8).copy()).to(self.device)
         self.nseg = len(segs)
+        # OHWI transpose tiles (ohwi_pack): ceil(taps*C/64) x ceil(K/64) per weight
+        tiles = [(_ceil(int(r["kh"] * r["kw"] * r["C"]), 64) * _ceil(int(r["K"]), 64)
+                  if r["bf_ohwi"] >= 0 else 0) for r in seg_arr]
+        self.ohwi_tiles = int(sum(tiles))
+        self.ohwi_tile0 = torch.tensor(np.concatenate([[0], np.cumsum(tiles)[:-1]]).astype(np.int64),
+                                       device=self.device)
         self.wbf = torch.zeros(max(bf_total, 1), dtype=BF16, device=self.device)
         bptr = self.wbf.data_ptr()
         for rec, s in zip(seg_arr, ps.train_slots):
@@ -786,6 +792,8 @@ class Engine:
                              self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
                              int(self.use_momentum), self.segs.data_ptr(), self.nseg,
                              self.wbf.data_ptr(), sp + 8, 1)
+        plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
+                       self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr())
         plan.step_increment(self.gstep.data_ptr())
         self.seg["opt"] = (b2, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
@@ -799,6 +807,9 @@ class Engine:
                                  self.mom.data_ptr(), self.params.n_train, s.init, 0, 0.0, 0.0, [],
                                  [s.init], 0, 0.0, 0.0, 1.0, 0, self.segs.data_ptr(), self.nseg,
                                  self.wbf.data_ptr(), 0, 0, torch.cuda.current_stream().cuda_stream)
+        self.nat.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
+                           self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
+                           self.wbf.data_ptr(), torch.cuda.current_stream().cuda_stream)
 
     def _run(self, name, stream):
         a, b = self.seg[name]

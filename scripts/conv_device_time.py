@@ -70,6 +70,20 @@ def main():
                             0, 0, part.data_ptr() if v["stats"] else 0, 0, g, [], [], [], [], [],
                             0.997, 1e-5, 1)
             res_line.append(f"{name} {dev_time(p):.2f}")
+        # consumer-side BN finalize in the prologue (BnPreFin) over `cnt` group partials
+        if k == 3 and C == K and C <= 64:
+            for cnt in (T // 4, 32, 8):
+                gp = torch.rand(cnt * 2 * C, device=dev) + 0.1
+                gam = torch.rand(C, device=dev)
+                outs = [torch.empty(C, device=dev) for _ in range(6)]
+                p = nat.Plan()
+                for _ in range(n):
+                    p.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, res.data_ptr(),
+                                outs[2].data_ptr(), outs[3].data_ptr(), 0, 0, part.data_ptr(), 0,
+                                g, [], [], [], [gp.data_ptr(), cnt, M // cnt, M, gam.data_ptr(),
+                                               gam.data_ptr()] + [o.data_ptr() for o in outs],
+                                [], 0.997, 1e-5, 1)
+                res_line.append(f"fwd+pfin{cnt} {dev_time(p):.2f}")
         for name, bnb in (("dgrad", False), ("dgrad+bnb", True)):
             p = nat.Plan()
             bl = [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(), sh.data_ptr(),
