@@ -108,7 +108,7 @@ def main(argv=None) -> int:
     sps = args.steps / elapsed
     if ctx.is_chief:
         out = {
-            "metric": "steps/sec (global_batch=128 CIFAR-10 / 1024 ImageNet) ResNet-50",
+            "metric": "steps/sec (global_batch=128 CIFAR-10 / 1024 ImageNet) ResNet-50 at 1/2/4/8 MI355X",
             "value": round(sps, 3),
             "unit": "steps/s",
             "n_gpus": world,

@@ -15,7 +15,10 @@ struct EpiLayout {
   static constexpr int LDC = BN + 4;              // fp32 staging row stride (floats)
   static constexpr int CPR = BN / 8;              // 8-channel chunks per row
   static constexpr int RPP = 256 / CPR;           // rows per pass
-  static constexpr int RED = 2 * RPP * BN + BN;   // floats (two reduction planes + means)
+  // reduction planes: colsum8's 4 wave totals per column, or the last-arriver /
+  // prologue combines' (256 / BN) slices per column -- whichever is larger
+  static constexpr int REDP = (4 * BN > 256) ? 4 * BN : 256;
+  static constexpr int RED = 2 * REDP + BN;       // floats (two reduction planes + means)
   static constexpr int PHASES = ((BM * LDC + RED) * 4 <= 64 * 1024) ? 1 : WM;
   static constexpr int PR = BM / PHASES;          // rows staged per phase
   static constexpr int TILE = PR * LDC;           // floats
@@ -203,8 +206,8 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   using EL = EpiLayout<BM, BN, WM>;
   float* cs = reinterpret_cast<float*>(smem);
   float* red = cs + EL::TILE;
-  float* red2 = red + EL::RPP * BN;
-  float* mean_s = red + 2 * EL::RPP * BN;
+  float* red2 = red + EL::REDP;
+  float* mean_s = red + 2 * EL::REDP;
   const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
   const int col0 = n0 + cc * 8;
   const bool colok = col0 < NC;  // NC % 16 == 0 -> a chunk is all-in or all-out
