@@ -127,7 +127,7 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     if (!conv_direct_covers(g, mode))
       throw std::invalid_argument("abwd: this dgrad is not covered by the direct 3x3 kernel");
     const int C = c.K;   // A channels of the dgrad
-    if (g.abwd.cnt < 1 || g.abwd.cnt > (256 / C) * 8)
+    if (g.abwd.cnt < 0 || g.abwd.cnt > (256 / C) * 8)   // 0: coefficients precomputed
       throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
   }
   if (g.pfin.cnt > 0) {

@@ -131,6 +131,21 @@ conv3x3_direct_kernel(GemmArgs args) {
   float* bw_s = pre_s;   // [7][CA]: a, b, c, mean, rstd, scale, shift (ABWD never has PRE)
   if constexpr (ABWD) {
     const BnBwdPre& Q = args.abwd;
+    if (Q.cnt == 0) {   // coefficients precomputed by bn_bwd_finalize
+      if (tid < CA) {
+        bw_s[tid] = Q.coef[tid];
+        bw_s[CA + tid] = Q.coef[CA + tid];
+        bw_s[2 * CA + tid] = Q.coef[2 * CA + tid];
+        bw_s[3 * CA + tid] = Q.mean[tid];
+        bw_s[4 * CA + tid] = Q.rstd[tid];
+        bw_s[5 * CA + tid] = Q.scale[tid];
+        bw_s[6 * CA + tid] = Q.shift[tid];
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (ABWD) if (args.abwd.cnt > 0) {
+    const BnBwdPre& Q = args.abwd;
     constexpr int G = 256 / CA;
     const int c = tid % CA, qq = tid / CA;
     float a1 = 0.f, a2 = 0.f;

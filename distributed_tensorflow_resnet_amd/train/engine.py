@@ -418,12 +418,14 @@ class Engine:
             stat_ptr = b.part.data_ptr()
             b.pending, b.fused_fwd = (stat_ptr, T, bm, M), False
             capc, capp = self._consumer_cap(nc), (256 // bn) * 8
-            mode = os.environ.get("DTR_FUSED_BN_FINALIZE", "1")
+            # measured (CIFAR bs 128 / 32): "3" (consumer prologue when the tiles are few,
+            # else a separate finalize) beats adding producer-side last arrivers ("1")
+            mode = os.environ.get("DTR_FUSED_BN_FINALIZE", "3")
             if mode == "0":
                 b.pending = ("separate", stat_ptr, T, bm, M)
             elif T <= capc:
                 pass                                    # (a)
-            elif capc and mode != "2":
+            elif capc and mode not in ("2", "3"):
                 gs = 2
                 while _ceil(T, gs) > capc:
                     gs *= 2
@@ -434,6 +436,8 @@ class Engine:
                     b.pending = (b.gpart.data_ptr(), _ceil(T, gs), gs * bm, M)
                 else:
                     b.pending = ("separate", stat_ptr, T, bm, M)
+            elif mode == "3":
+                b.pending = ("separate", stat_ptr, T, bm, M)
             else:
                 grp = self._fuse_finalize(M, nc)
                 if grp is not None:                     # (c)
@@ -487,13 +491,20 @@ class Engine:
         pb = self._pending_bwd
         if pb is not None:
             if (pb["out"] is dy and dx is not None and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
-                    and self.nat.conv_direct_covers(1, geom)
-                    and pb["cnt"] <= self._consumer_cap(s.cout)):
+                    and self.nat.conv_direct_covers(1, geom)):
                 bn = pb["bn"]
                 add = pb["add"]
+                part, cnt = pb["part"], pb["cnt"]
+                if cnt > self._consumer_cap(s.cout):
+                    # too many partials for the prologue: finalize separately, the
+                    # dgrad then reads the coefficients (cnt = 0)
+                    plan.bn_bwd_finalize(part, cnt, pb["M"], bn.spec.channels, bn.gamma,
+                                         bn.rstd.data_ptr(), bn.dgamma, bn.dbeta,
+                                         self.coef.data_ptr())
+                    part, cnt = 0, 0
                 abw = [pb["x"].data_ptr(), 0 if add is None else add.data_ptr(),
                        bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
-                       bn.shift.data_ptr(), bn.gamma, pb["part"], pb["cnt"], dy.data_ptr(),
+                       bn.shift.data_ptr(), bn.gamma, part, cnt, dy.data_ptr(),
                        bn.dgamma, bn.dbeta, self.coef.data_ptr()]
                 self._produced.update(bn.names)
                 self._pending_bwd = None
@@ -512,7 +523,8 @@ class Engine:
                       bn.shift.data_ptr(), bn.bpart.data_ptr()]
                 self._bnb_src = (bn.bpart.data_ptr(), T)
                 capc, capp = self._consumer_cap(C), (256 // bnt) * 8
-                if T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0":
+                if (T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
+                        and os.environ.get("DTR_BWD_GROUPS", "0") == "1"):
                     gs = 2
                     while _ceil(T, gs) > capc:
                         gs *= 2

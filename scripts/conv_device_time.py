@@ -84,6 +84,17 @@ def main():
                                                gam.data_ptr()] + [o.data_ptr() for o in outs],
                                 [], 0.997, 1e-5, 1)
                 res_line.append(f"fwd+pfin{cnt} {dev_time(p):.2f}")
+        # dependency chain: every conv reads the previous conv's output (ping-pong)
+        if C == K:
+            y2 = torch.empty_like(y)
+            p = nat.Plan()
+            for i in range(n):
+                src, dst = (y, y2) if i % 2 else (y2, y)
+                p.conv_gemm(0, src.data_ptr(), w.data_ptr(), dst.data_ptr(), 0, res.data_ptr(),
+                            sc.data_ptr(), sh.data_ptr(), 0, 0, part.data_ptr(), 0, g, [], [], [],
+                            [], [], 0.997, 1e-5, 1)
+            y2.copy_(x)
+            res_line.append(f"chain(fwd+pre+stats+res) {dev_time(p):.2f}")
         for name, bnb in (("dgrad", False), ("dgrad+bnb", True)):
             p = nat.Plan()
             bl = [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(), sh.data_ptr(),

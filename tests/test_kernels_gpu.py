@@ -498,3 +498,32 @@ def test_direct_dgrad_fused_bn_backward(gpu, N, H, C, with_add):
     assert (dh.float() - dh2.float()).abs().max().item() <= 2 * 2 ** -8 * dh2.float().abs().max().item()
     dx2 = fn.conv2d_dgrad(dh2, w, tuple(x.shape), 1)
     assert _rel(dx, dx2) < 5e-3
+
+
+def test_direct_dgrad_fused_bn_backward_precomputed_coef(gpu):
+    """BnBwdPre with cnt = 0: coefficients read from a prior bn_bwd_finalize."""
+    torch.manual_seed(16)
+    nat = fn.native()
+    N, H, C = 16, 16, 32
+    M = N * H * H
+    da = torch.randn(N, H, H, C, device=gpu).to(BF)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    add = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(3, 3, C, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    mean, rstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    gamma = torch.rand(C, device=gpu) + 0.5
+    scale, shift = gamma * rstd, torch.randn(C, device=gpu) * 0.2
+    part = torch.randn(4, 2, C, device=gpu).contiguous()
+    dg, db, coef = (torch.empty(n, device=gpu) for n in (C, C, 3 * C))
+    st = torch.cuda.current_stream().cuda_stream
+    nat.bn_bwd_finalize(part.data_ptr(), 4, M, C, gamma.data_ptr(), rstd.data_ptr(),
+                        dg.data_ptr(), db.data_ptr(), coef.data_ptr(), st)
+    dh = torch.empty_like(da)
+    dx = fn.conv2d_dgrad(da, w, tuple(x.shape), 1,
+                         abwd=[x, add, mean, rstd, scale, shift, gamma, 0, 0, dh, dg, db, coef])
+    dh2 = torch.empty_like(da)
+    nat.bn_bwd_apply(da.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                     scale.data_ptr(), shift.data_ptr(), coef.data_ptr(), add.data_ptr(),
+                     dh2.data_ptr(), M, C, st)
+    torch.testing.assert_close(dh.float(), dh2.float(), rtol=0, atol=0)
+    assert _rel(dx, fn.conv2d_dgrad(dh2, w, tuple(x.shape), 1)) < 5e-3
