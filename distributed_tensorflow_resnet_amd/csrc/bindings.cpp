@@ -16,6 +16,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -375,6 +376,8 @@ struct Plan {
   std::vector<PlanOp> ops;
   std::vector<std::string> names;
   std::vector<hipEvent_t> events;
+  std::vector<double> host_us;   // per-op host issue time (profile mode only)
+  bool profile = false;
   int cur = 0;
   ~Plan() {
     for (auto e : events) (void)hipEventDestroy(e);
@@ -405,9 +408,12 @@ struct Plan {
     if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
     hipStream_t st[2] = {S(main_stream), S(side_stream ? side_stream : main_stream)};
     py::gil_scoped_release nogil;
+    if (profile && host_us.size() != ops.size()) host_us.assign(ops.size(), 0.0);
     for (int i = begin; i < end; ++i) {
       const PlanOp& o = ops[i];
       hipStream_t s = st[o.stream];
+      const auto t0 = profile ? std::chrono::steady_clock::now()
+                              : std::chrono::steady_clock::time_point();
       if (o.kind == 0) {
         o.fn(s);
       } else if (o.kind == 1) {
@@ -416,6 +422,9 @@ struct Plan {
         if (hipStreamWaitEvent(s, events[o.ev], 0) != hipSuccess)
           fprintf(stderr, "hipStreamWaitEvent failed\n");
       }
+      if (profile)
+        host_us[i] += std::chrono::duration<double, std::micro>(
+                          std::chrono::steady_clock::now() - t0).count();
     }
   }
   int size() const { return (int)ops.size(); }
@@ -454,7 +463,14 @@ PYBIND11_MODULE(_C, m) {
         if (s != 0 && s != 1) throw std::invalid_argument("stream index must be 0 or 1");
         p.cur = s;
       })
-      .def("names", [](const Plan& p) { return p.names; });
+      .def("names", [](const Plan& p) { return p.names; })
+      .def("set_profile", [](Plan& p, bool on) { p.profile = on; p.host_us.clear(); })
+      .def("host_us", [](const Plan& p) { return p.host_us; })
+      .def("op_streams", [](const Plan& p) {
+        std::vector<int> v;
+        for (const auto& o : p.ops) v.push_back(o.stream);
+        return v;
+      });
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);
   def_op(m, plan, "conv_wgrad", mk_conv_wgrad);

@@ -95,6 +95,17 @@ def main():
                             [], [], 0.997, 1e-5, 1)
             y2.copy_(x)
             res_line.append(f"chain(fwd+pre+stats+res) {dev_time(p):.2f}")
+            # chain over 16 distinct activation / partial buffers (like the real forward)
+            bufs = [torch.randn_like(x) for _ in range(17)]
+            parts = [torch.empty_like(part) for _ in range(16)]
+            p = nat.Plan()
+            for i in range(n):
+                j = i % 16
+                p.conv_gemm(0, bufs[j].data_ptr(), w.data_ptr(), bufs[j + 1].data_ptr(), 0,
+                            bufs[(j + 5) % 17].data_ptr(), sc.data_ptr(), sh.data_ptr(), 0, 0,
+                            parts[j].data_ptr(), 0, g, [], [], [], [], [], 0.997, 1e-5, 1)
+            res_line.append(f"chain16bufs {dev_time(p):.2f}")
+            del bufs, parts
         for name, bnb in (("dgrad", False), ("dgrad+bnb", True)):
             p = nat.Plan()
             bl = [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(), sh.data_ptr(),
