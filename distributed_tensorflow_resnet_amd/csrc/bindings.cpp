@@ -464,7 +464,10 @@ PYBIND11_MODULE(_C, m) {
         p.cur = s;
       })
       .def("names", [](const Plan& p) { return p.names; })
-      .def("set_profile", [](Plan& p, bool on) { p.profile = on; p.host_us.clear(); })
+      .def("set_profile", [](Plan& p, bool on) {
+        p.profile = on;
+        if (on) p.host_us.clear();
+      })
       .def("host_us", [](const Plan& p) { return p.host_us; })
       .def("op_streams", [](const Plan& p) {
         std::vector<int> v;
@@ -516,6 +519,8 @@ PYBIND11_MODULE(_C, m) {
         "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");
   m.def("set_conv_direct", &set_conv_direct,
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
+  m.def("set_fin_version", &set_fin_version,
+        "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);

@@ -11,6 +11,8 @@
 //
 // Backward: g = dy * [x*scale+shift > 0];  dbeta = sum g;  dgamma = sum g*xhat;
 //   dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat))   (+ residual gradient).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -32,6 +34,149 @@ __device__ __forceinline__ Welford wcombine(Welford a, Welford b) {
   return r;
 }
 
+// Finalize launches sit on the critical path between two convolutions (one per
+// BatchNorm whose consumer cannot combine the partials itself), so they are
+// built for latency: per-channel parameters loaded up front, the partials in
+// ONE round of loads, division-free combines, bitwise-deterministic orders.
+constexpr int FIN_BATCH = 16;
+
+// Per-channel variant: one 256-thread block per channel; thread t holds tiles t + 256u
+// (u < FIN_BATCH, loads issued together; more tiles re-read in further rounds).
+// Two division-free block sums (Chan about the global mean): N and sum n*mean ->
+// mean; then sum M2 + n (mean_i - mean)^2.  The per-channel parameters are loaded
+// up front so their latency hides under the partial loads.
+__device__ __forceinline__ float block_sum4(float v, float* red, int slot) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[slot * 4 + (threadIdx.x >> 6)] = v;
+  __syncthreads();
+  return (red[slot * 4] + red[slot * 4 + 1]) + (red[slot * 4 + 2] + red[slot * 4 + 3]);
+}
+
+__global__ void __launch_bounds__(256)
+bn_finalize_chan_kernel(const float* __restrict__ part, int tiles, int tile_rows, int M, int C,
+                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                    float* moving_mean, float* moving_var, float momentum, float eps,
+                    int update_moving, float* mean_out, float* rstd_out, float* scale_out,
+                    float* shift_out) {
+  __shared__ float red[12];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  float g = 0.f, bt = 0.f, mm = 0.f, mvv = 0.f;
+  if (tid == 0) {
+    g = gamma[c];
+    bt = beta[c];
+    if (update_moving) {
+      mm = moving_mean[c];
+      mvv = moving_var[c];
+    }
+  }
+  float mv[FIN_BATCH], qv[FIN_BATCH], nv[FIN_BATCH];
+#pragma unroll
+  for (int u = 0; u < FIN_BATCH; ++u) {
+    const int t = tid + u * 256;
+    const bool ok = t < tiles;
+    mv[u] = ok ? part[(long)t * 2 * C + c] : 0.f;
+    qv[u] = ok ? part[(long)t * 2 * C + C + c] : 0.f;
+    nv[u] = ok ? (float)min(tile_rows, M - t * tile_rows) : 0.f;
+  }
+  float n = 0.f, sx = 0.f;
+#pragma unroll
+  for (int u = 0; u < FIN_BATCH; ++u) {
+    n += nv[u];
+    sx += nv[u] * mv[u];
+  }
+  for (int t = tid + FIN_BATCH * 256; t < tiles; t += 256) {   // beyond one round
+    const float nt = (float)min(tile_rows, M - t * tile_rows);
+    n += nt;
+    sx += nt * part[(long)t * 2 * C + c];
+  }
+  const float N = block_sum4(n, red, 0);
+  const float mean = block_sum4(sx, red, 1) / N;
+  float m2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < FIN_BATCH; ++u) {
+    const float d = mv[u] - mean;
+    m2 += qv[u] + nv[u] * d * d;
+  }
+  for (int t = tid + FIN_BATCH * 256; t < tiles; t += 256) {
+    const float nt = (float)min(tile_rows, M - t * tile_rows);
+    const float d = part[(long)t * 2 * C + c] - mean;
+    m2 += part[(long)t * 2 * C + C + c] + nt * d * d;
+  }
+  m2 = block_sum4(m2, red, 2);
+  if (tid == 0) {
+    const float rstd = rsqrtf(m2 / N + eps);
+    const float sc = g * rstd;
+    mean_out[c] = mean;
+    rstd_out[c] = rstd;
+    scale_out[c] = sc;
+    shift_out[c] = bt - mean * sc;
+    if (update_moving) {
+      const float uvar = N > 1.f ? m2 / (N - 1.f) : m2;
+      moving_mean[c] = mm - (1.f - momentum) * (mm - mean);
+      moving_var[c] = mvv - (1.f - momentum) * (mvv - uvar);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_finalize_chan_kernel(const float* __restrict__ part, int tiles, int M, int C,
+                        const float* __restrict__ gamma, const float* __restrict__ rstd,
+                        float* dgamma, float* dbeta, float* coef) {
+  __shared__ float s0[4], s1[4];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float a = tid == 0 ? gamma[c] * rstd[c] : 0.f;   // issued ahead of the partials
+  float sg = 0.f, sgx = 0.f;
+  for (int base = tid; base < tiles; base += FIN_BATCH * 256) {
+    float v1[FIN_BATCH], v2[FIN_BATCH];
+#pragma unroll
+    for (int u = 0; u < FIN_BATCH; ++u) {
+      const int t = base + u * 256;
+      v1[u] = t < tiles ? part[(long)t * 2 * C + c] : 0.f;
+      v2[u] = t < tiles ? part[(long)t * 2 * C + C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_BATCH; ++u) {
+      sg += v1[u];
+      sgx += v2[u];
+    }
+  }
+  sg = wave_sum(sg);
+  sgx = wave_sum(sgx);
+  const int wave = tid >> 6;
+  if ((tid & 63) == 0) {
+    s0[wave] = sg;
+    s1[wave] = sgx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float a0 = (s0[0] + s0[1]) + (s0[2] + s0[3]);
+    const float a1 = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+    dbeta[c] = a0;
+    dgamma[c] = a1;
+    coef[c] = a;
+    coef[C + c] = a * a0 / (float)M;
+    coef[2 * C + c] = a * a1 / (float)M;
+  }
+}
+
+// Variant choice (measured, scripts/fin_bench.py): the per-channel one-round
+// kernels win once there are many partials per channel; the LDS-tree kernels
+// below win for few partials or many channels.  DTR_FIN_V=0/2 forces one.
+static int g_fin_version = -1;
+static int fin_version() {
+  if (g_fin_version < 0) {
+    const char* e = std::getenv("DTR_FIN_V");
+    g_fin_version = e ? std::atoi(e) : 1;
+  }
+  return g_fin_version;
+}
+void set_fin_version(int v) { g_fin_version = v; }
+static bool fin_use_v2(int tiles, int C, bool bwd) {
+  const int v = fin_version();
+  if (v != 1) return v == 2;
+  return C <= 512 && tiles >= (bwd ? 256 : 1024);
+}
+
 // One block per channel: thread t folds tiles t, t+256, ... then a fixed-shape
 // LDS tree -- bitwise deterministic.
 __global__ void __launch_bounds__(256)
@@ -42,6 +187,15 @@ bn_finalize_kernel(const float* __restrict__ part, int tiles, int tile_rows, int
                    float* shift_out) {
   __shared__ float sn[256], sm[256], s2[256];
   const int c = blockIdx.x, tid = threadIdx.x;
+  float g = 0.f, bt = 0.f, mm = 0.f, mvv = 0.f;   // issued ahead of the partials
+  if (tid == 0) {
+    g = gamma[c];
+    bt = beta[c];
+    if (update_moving) {
+      mm = moving_mean[c];
+      mvv = moving_var[c];
+    }
+  }
   Welford w{0.f, 0.f, 0.f};
   for (int t = tid; t < tiles; t += 256) {
     Welford b;
@@ -68,15 +222,15 @@ bn_finalize_kernel(const float* __restrict__ part, int tiles, int tile_rows, int
     const float n = sn[0], mean = sm[0], m2 = s2[0];
     const float var = m2 / n;
     const float rstd = rsqrtf(var + eps);
-    const float sc = gamma[c] * rstd;
+    const float sc = g * rstd;
     mean_out[c] = mean;
     rstd_out[c] = rstd;
     scale_out[c] = sc;
-    shift_out[c] = beta[c] - mean * sc;
+    shift_out[c] = bt - mean * sc;
     if (update_moving) {
       const float uvar = n > 1.f ? m2 / (n - 1.f) : m2;
-      moving_mean[c] -= (1.f - momentum) * (moving_mean[c] - mean);
-      moving_var[c] -= (1.f - momentum) * (moving_var[c] - uvar);
+      moving_mean[c] = mm - (1.f - momentum) * (mm - mean);
+      moving_var[c] = mvv - (1.f - momentum) * (mvv - uvar);
     }
   }
 }
@@ -85,6 +239,13 @@ void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
                  const float* gamma, const float* beta, float* moving_mean, float* moving_var,
                  float momentum, float eps, int update_moving, float* mean, float* rstd,
                  float* scale, float* shift, hipStream_t s) {
+  if (fin_use_v2(tiles, C, false)) {
+    hipLaunchKernelGGL(bn_finalize_chan_kernel, dim3(C), dim3(256), 0, s, stat_part, tiles,
+                       tile_rows, M, C, gamma, beta, moving_mean, moving_var, momentum, eps,
+                       update_moving, mean, rstd, scale, shift);
+    DTR_CHECK_LAUNCH();
+    return;
+  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, s, stat_part, tiles, tile_rows,
                      M, C, gamma, beta, moving_mean, moving_var, momentum, eps, update_moving,
                      mean, rstd, scale, shift);
@@ -258,6 +419,7 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
   __shared__ float s0[16][64], s1[16][64];
   const int cx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cx;
+  const float a = (ty == 0 && c < C) ? gamma[c] * rstd[c] : 0.f;   // ahead of the partials
   float sg = 0.f, sgx = 0.f;
   if (c < C) {
 #pragma unroll 4
@@ -278,7 +440,6 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
     }
     dbeta[c] = a0;
     dgamma[c] = a1;
-    const float a = gamma[c] * rstd[c];
     coef[c] = a;
     coef[C + c] = a * a0 / (float)M;
     coef[2 * C + c] = a * a1 / (float)M;
@@ -288,6 +449,12 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int tiles, int M, int C,
 void bn_bwd_finalize(const float* part, int tiles, int M, int C, const float* gamma,
                      const float* rstd, float* dgamma, float* dbeta, float* coef,
                      hipStream_t s) {
+  if (fin_use_v2(tiles, C, true)) {
+    hipLaunchKernelGGL(bn_bwd_finalize_chan_kernel, dim3(C), dim3(256), 0, s, part, tiles, M, C,
+                       gamma, rstd, dgamma, dbeta, coef);
+    DTR_CHECK_LAUNCH();
+    return;
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, tiles,
                      M, C, gamma, rstd, dgamma, dbeta, coef);
   DTR_CHECK_LAUNCH();
