@@ -44,6 +44,13 @@ static ConvGeom geom_from(const std::vector<int>& v) {
 }
 
 // ---------------------------------------------------------------- op makers
+// Partials a consumer prologue (bn_prefin_table / bn_prefin_sums, bn_fused.h)
+// combines for C channels: C/4 float4 groups, PFIN_ROUNDS rounds of PFIN_ITEMS.
+static int pfin_cap(int C) {
+  if (C < 4 || C > 128 || (C & (C - 1)) != 0) return 0;
+  return 8 * 2 * 1024 / C;
+}
+
 static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32, ptr_t residual,
                            ptr_t pre_scale, ptr_t pre_shift, ptr_t bias, int nbias,
                            ptr_t stat_part, int accumulate, std::vector<int> geom,
@@ -128,13 +135,14 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     if (!conv_direct_covers(g, mode))
       throw std::invalid_argument("abwd: this dgrad is not covered by the direct 3x3 kernel");
     const int C = c.K;   // A channels of the dgrad
-    if (g.abwd.cnt < 0 || g.abwd.cnt > (256 / C) * 8)   // 0: coefficients precomputed
+    if (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C))   // 0: coefficients precomputed
       throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
   }
   if (g.pfin.cnt > 0) {
     const int C = c.C;   // PRE is forward-only: the A channels
-    if (C > 256 || (C & (C - 1)) != 0 || g.pfin.cnt > (256 / C) * 8)
-      throw std::invalid_argument("pfin: C must be a power of two <= 256 and cnt <= 8*256/C");
+    if (g.pfin.cnt > pfin_cap(C))
+      throw std::invalid_argument("pfin: C must be a power of two in [4, 128] and cnt <= "
+                                  "PFIN_ITEMS*PFIN_ROUNDS*1024/C");
   }
   // In-kernel finalize bounds (conv_epilogue.h combines): every level's item count
   // must fit one round of loads, cnt <= (256 / BN) * FIN_UNROLL.
@@ -521,6 +529,7 @@ PYBIND11_MODULE(_C, m) {
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
   m.def("set_fin_version", &set_fin_version,
         "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
+  m.def("pfin_cap", &pfin_cap, "max partials a consumer prologue combines for C channels");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);

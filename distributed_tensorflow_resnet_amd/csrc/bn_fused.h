@@ -54,65 +54,107 @@ __device__ __forceinline__ void reset_counter(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Consumer-side finalize (BnPreFin, kernels.h): all 256 threads combine the
-// producer's partials for C channels (C a power of two <= 256; thread = (channel
-// c = tid % C, slice q = tid / C), items q, q + G, ... with G = 256 / C, at most
-// FIN_UNROLL each -- one round of loads), fold the G slices in fixed order and
-// write the BN scale/shift table sc_s/sh_s (LDS).  Block (0,0) also writes the
-// global mean/rstd/scale/shift and the moving averages.  `scratch` = 768 LDS
-// floats.  Ends with a barrier (the table is ready for every thread).
+// Consumer-side finalize (BnPreFin, kernels.h): the 256 threads of the BN's first
+// consuming conv combine the producer's per-tile partials [cnt][2][C] (mean, M2)
+// themselves -- no finalize launch between the two convs.  Thread = (channel
+// group of 4 = one 16-B load, tile slice q); slice q holds tiles q, q + G, ...
+// (G = 1024 / C), PFIN_ITEMS per round with all loads of a round in flight.
+// Per round a division-free Chan fold about the round mean, then pairwise Chan
+// combines: xor-shuffles across the slices inside a wave, one fixed-order LDS
+// pass across the 4 waves -- bitwise deterministic.  Writes the BN scale/shift
+// table sc_s/sh_s (LDS); block (0,0) also writes the global mean/rstd/scale/
+// shift and the moving averages.  `scratch` >= 12*C LDS floats (>= 768 for
+// C <= 64).  C: multiple of 4 with C/4 a power of two <= 64.  Ends with a barrier.
+constexpr int PFIN_ITEMS = 8;
+constexpr int PFIN_ROUNDS = 2;   // the host keeps cnt <= PFIN_ITEMS*PFIN_ROUNDS*1024/C
+
+__device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float nb, float mub,
+                                           float m2b) {
+  const float nn = n + nb;
+  if (nn <= 0.f) return;
+  const float d = mub - mu, fb = nb / nn;
+  mu += d * fb;
+  m2 += m2b + d * d * n * fb;
+  n = nn;
+}
+
 __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float* sc_s,
                                                 float* sh_s, float* scratch) {
   const int tid = threadIdx.x;
-  const int G = 256 / C;
-  const int c = tid % C, q = tid / C;
-  // Division-free parallel combine about a common centre (Chan et al.): for items
-  // (n_i, mean_i, M2_i): N = sum n_i, mean = sum n_i mean_i / N,
-  // M2 = sum M2_i + sum n_i (mean_i - mean)^2 -- two passes over the registers
-  // instead of one dependent division per item (sequential Welford).
-  float n = 0.f, mu = 0.f, m2 = 0.f;
-  if (q < G) {
-    float mv[FIN_UNROLL], qv[FIN_UNROLL], nv[FIN_UNROLL];
+  const int CG = C >> 2, cg = tid & (CG - 1), q = tid / CG, G = 256 / CG;
+  float gam = 0.f, bet = 0.f, mmv = 0.f, mvv = 0.f;   // issued ahead of the partials
+  if (tid < C) {
+    gam = P.gamma[tid];
+    bet = P.beta[tid];
+    if (P.update_moving && blockIdx.x == 0 && blockIdx.y == 0) {
+      mmv = P.mmean[tid];
+      mvv = P.mvar[tid];
+    }
+  }
+  float n = 0.f, mu[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int base = q; base < P.cnt; base += PFIN_ITEMS * G) {
+    f32x4 mv[PFIN_ITEMS], qv[PFIN_ITEMS];
+    float nv[PFIN_ITEMS];
 #pragma unroll
-    for (int u = 0; u < FIN_UNROLL; ++u) {
-      const int t = q + u * G;
+    for (int u = 0; u < PFIN_ITEMS; ++u) {
+      const int t = base + u * G;
       const bool ok = t < P.cnt;
-      mv[u] = ok ? P.part[(long)t * 2 * C + c] : 0.f;
-      qv[u] = ok ? P.part[(long)t * 2 * C + C + c] : 0.f;
+      const float* row = P.part + (long)t * 2 * C + 4 * cg;
+      mv[u] = ok ? *reinterpret_cast<const f32x4*>(row) : f32x4{0.f, 0.f, 0.f, 0.f};
+      qv[u] = ok ? *reinterpret_cast<const f32x4*>(row + C) : f32x4{0.f, 0.f, 0.f, 0.f};
       nv[u] = ok ? (float)min(P.rows_per, P.M - t * P.rows_per) : 0.f;
     }
-    float s = 0.f;
+    float nr = 0.f;
 #pragma unroll
-    for (int u = 0; u < FIN_UNROLL; ++u) {
-      n += nv[u];
-      s += nv[u] * mv[u];
-    }
-    mu = n > 0.f ? s / n : 0.f;
+    for (int u = 0; u < PFIN_ITEMS; ++u) nr += nv[u];
+    const float inv = nr > 0.f ? 1.f / nr : 0.f;
 #pragma unroll
-    for (int u = 0; u < FIN_UNROLL; ++u) {
-      const float d = mv[u] - mu;
-      m2 += qv[u] + nv[u] * d * d;
+    for (int j = 0; j < 4; ++j) {
+      float sx = 0.f;
+#pragma unroll
+      for (int u = 0; u < PFIN_ITEMS; ++u) sx += nv[u] * mv[u][j];
+      const float mr = sx * inv;
+      float q2 = 0.f;
+#pragma unroll
+      for (int u = 0; u < PFIN_ITEMS; ++u) {
+        const float d = mv[u][j] - mr;
+        q2 += qv[u][j] + nv[u] * d * d;
+      }
+      float nn = n;
+      chan_merge(nn, mu[j], m2[j], nr, mr, q2);
+      if (j == 3) n = nn;
     }
-    scratch[tid] = n;
-    scratch[256 + tid] = mu;
-    scratch[512 + tid] = m2;
+  }
+  // slices inside the wave (lanes cg + CG*k), then across the 4 waves
+  for (int o = CG; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(n, o, 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float mub = __shfl_xor(mu[j], o, 64), m2b = __shfl_xor(m2[j], o, 64);
+      float nn = n;
+      chan_merge(nn, mu[j], m2[j], nb, mub, m2b);
+      if (j == 3) n = nn;
+    }
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane < CG) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      scratch[(wave * 3 + 0) * C + 4 * lane + j] = n;
+      scratch[(wave * 3 + 1) * C + 4 * lane + j] = mu[j];
+      scratch[(wave * 3 + 2) * C + 4 * lane + j] = m2[j];
+    }
   }
   __syncthreads();
-  if (q == 0) {
-    float fn_ = 0.f, s = 0.f;
-    for (int k = 0; k < G; ++k) {
-      fn_ += scratch[k * C + c];
-      s += scratch[k * C + c] * scratch[256 + k * C + c];
-    }
-    const float fmu = s / fn_;
-    float fm2 = 0.f;
-    for (int k = 0; k < G; ++k) {
-      const float d = scratch[256 + k * C + c] - fmu;
-      fm2 += scratch[512 + k * C + c] + scratch[k * C + c] * d * d;
-    }
+  if (tid < C) {
+    const int c = tid;
+    float fn_ = scratch[c], fmu = scratch[C + c], fm2 = scratch[2 * C + c];
+    for (int k = 1; k < 4; ++k)
+      chan_merge(fn_, fmu, fm2, scratch[(k * 3) * C + c], scratch[(k * 3 + 1) * C + c],
+                 scratch[(k * 3 + 2) * C + c]);
     const float rs = rsqrtf(fm2 / fn_ + P.eps);
-    const float sc = P.gamma[c] * rs;
-    const float sh = P.beta[c] - fmu * sc;
+    const float sc = gam * rs;
+    const float sh = bet - fmu * sc;
     sc_s[c] = sc;
     sh_s[c] = sh;
     if (blockIdx.x == 0 && blockIdx.y == 0) {
@@ -122,12 +164,60 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
       P.shift[c] = sh;
       if (P.update_moving) {
         const float uvar = fn_ > 1.f ? fm2 / (fn_ - 1.f) : fm2;
-        P.mmean[c] -= (1.f - P.momentum) * (P.mmean[c] - fmu);
-        P.mvar[c] -= (1.f - P.momentum) * (P.mvar[c] - uvar);
+        P.mmean[c] = mmv - (1.f - P.momentum) * (mmv - fmu);
+        P.mvar[c] = mvv - (1.f - P.momentum) * (mvv - uvar);
       }
     }
   }
   __syncthreads();
+}
+
+// The BN-backward counterpart (BnBwdPre, the direct dgrad's ABWD prologue): sums
+// sum g, sum g*xhat over the producer's [cnt][2][C] partials with the same
+// thread layout, shuffles and fixed-order cross-wave pass.  Returns in out1/out2
+// (valid for tid < C).  `scratch` >= 8*C floats.
+__device__ __forceinline__ void bn_prefin_sums(const float* __restrict__ part, int cnt, int C,
+                                               float* scratch, float& out1, float& out2) {
+  const int tid = threadIdx.x;
+  const int CG = C >> 2, cg = tid & (CG - 1), q = tid / CG, G = 256 / CG;
+  f32x4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
+  for (int base = q; base < cnt; base += PFIN_ITEMS * G) {
+    f32x4 v1[PFIN_ITEMS], v2[PFIN_ITEMS];
+#pragma unroll
+    for (int u = 0; u < PFIN_ITEMS; ++u) {
+      const int t = base + u * G;
+      const bool ok = t < cnt;
+      const float* row = part + (long)t * 2 * C + 4 * cg;
+      v1[u] = ok ? *reinterpret_cast<const f32x4*>(row) : f32x4{0.f, 0.f, 0.f, 0.f};
+      v2[u] = ok ? *reinterpret_cast<const f32x4*>(row + C) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < PFIN_ITEMS; ++u) {
+      a1 += v1[u];
+      a2 += v2[u];
+    }
+  }
+  for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a1[j] += __shfl_xor(a1[j], o, 64);
+      a2[j] += __shfl_xor(a2[j], o, 64);
+    }
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane < CG) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      scratch[(wave * 2) * C + 4 * lane + j] = a1[j];
+      scratch[(wave * 2 + 1) * C + 4 * lane + j] = a2[j];
+    }
+  }
+  __syncthreads();
+  out1 = out2 = 0.f;
+  if (tid < C) {
+    out1 = (scratch[tid] + scratch[2 * C + tid]) + (scratch[4 * C + tid] + scratch[6 * C + tid]);
+    out2 = (scratch[C + tid] + scratch[3 * C + tid]) + (scratch[5 * C + tid] + scratch[7 * C + tid]);
+  }
 }
 
 }  // namespace dtr

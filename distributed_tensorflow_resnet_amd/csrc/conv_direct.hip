@@ -146,40 +146,27 @@ conv3x3_direct_kernel(GemmArgs args) {
   }
   if constexpr (ABWD) if (args.abwd.cnt > 0) {
     const BnBwdPre& Q = args.abwd;
-    constexpr int G = 256 / CA;
-    const int c = tid % CA, qq = tid / CA;
-    float a1 = 0.f, a2 = 0.f;
-    float v1[FIN_UNROLL], v2[FIN_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FIN_UNROLL; ++u) {
-      const int t = qq + u * G;
-      v1[u] = t < Q.cnt ? Q.part[(long)t * 2 * CA + c] : 0.f;
-      v2[u] = t < Q.cnt ? Q.part[(long)t * 2 * CA + CA + c] : 0.f;
+    const int c = tid;
+    float ga = 0.f, rs = 0.f, mn = 0.f, scl = 0.f, shf = 0.f;   // ahead of the partials
+    if (c < CA) {
+      ga = Q.gamma[c];
+      rs = Q.rstd[c];
+      mn = Q.mean[c];
+      scl = Q.scale[c];
+      shf = Q.shift[c];
     }
-#pragma unroll
-    for (int u = 0; u < FIN_UNROLL; ++u) {
-      a1 += v1[u];
-      a2 += v2[u];
-    }
-    fin_scratch[tid] = a1;
-    fin_scratch[256 + tid] = a2;
-    __syncthreads();
-    if (qq == 0) {
-      float sg = 0.f, sgx = 0.f;
-      for (int k = 0; k < G; ++k) {
-        sg += fin_scratch[k * CA + c];
-        sgx += fin_scratch[256 + k * CA + c];
-      }
-      const float rs = Q.rstd[c];
-      const float a = Q.gamma[c] * rs;
+    float sg, sgx;
+    bn_prefin_sums(Q.part, Q.cnt, CA, fin_scratch, sg, sgx);
+    if (c < CA) {
+      const float a = ga * rs;
       const float M = (float)args.M;
       bw_s[c] = a;
       bw_s[CA + c] = a * sg / M;
       bw_s[2 * CA + c] = a * sgx / M;
-      bw_s[3 * CA + c] = Q.mean[c];
+      bw_s[3 * CA + c] = mn;
       bw_s[4 * CA + c] = rs;
-      bw_s[5 * CA + c] = Q.scale[c];
-      bw_s[6 * CA + c] = Q.shift[c];
+      bw_s[5 * CA + c] = scl;
+      bw_s[6 * CA + c] = shf;
       if (blockIdx.x == 0 && blockIdx.y == 0) {
         Q.dbeta[c] = sg;
         Q.dgamma[c] = sgx;

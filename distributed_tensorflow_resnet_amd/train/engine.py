@@ -389,10 +389,9 @@ class Engine:
         assert self._cnt_next <= self.bn_counters.numel(), "BN counter pool exhausted"
         return self.bn_counters.data_ptr() + 4 * off
 
-    @staticmethod
-    def _consumer_cap(C: int) -> int:
-        """Max partials a consumer prologue combines in one round (bn_prefin_table)."""
-        return (256 // C) * 8 if C <= 256 and C & (C - 1) == 0 else 0
+    def _consumer_cap(self, C: int) -> int:
+        """Max partials a consumer prologue combines (bn_prefin_table / _sums)."""
+        return self.nat.pfin_cap(C)
 
     def _conv_fwd(self, plan, c: _Conv, x, out, N, pre: _BN | None = None, residual=None,
                   stats_for: _BN | None = None):

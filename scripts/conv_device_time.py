@@ -72,7 +72,7 @@ def main():
             res_line.append(f"{name} {dev_time(p):.2f}")
         # consumer-side BN finalize in the prologue (BnPreFin) over `cnt` group partials
         if k == 3 and C == K and C <= 64:
-            for cnt in (min(T // 4, (256 // C) * 8), 32, 8):
+            for cnt in (min(T, nat.pfin_cap(C)), 32, 8):
                 gp = torch.rand(cnt * 2 * C, device=dev) + 0.1
                 gam = torch.rand(C, device=dev)
                 outs = [torch.empty(C, device=dev) for _ in range(6)]

@@ -383,7 +383,9 @@ def test_fused_last_arriver_bn_finalize(gpu, N, H, C, group):
 
 @pytest.mark.parametrize("N,H,C,k,groups", [(8, 32, 16, 3, False), (128, 32, 16, 3, True),
                                             (64, 16, 32, 3, True), (16, 8, 64, 3, False),
-                                            (4, 14, 128, 1, False), (8, 14, 128, 1, True)])
+                                            (4, 14, 128, 1, False), (8, 14, 128, 1, True),
+                                            (128, 32, 16, 3, False), (128, 16, 32, 3, False),
+                                            (128, 8, 64, 3, False)])
 def test_consumer_prologue_bn_finalize(gpu, N, H, C, k, groups):
     """BnPreFin: the first consumer conv combines the producer's (mean, M2) partials
     (tile partials, or group partials left by groups_only last arrivers) in its
@@ -401,6 +403,8 @@ def test_consumer_prologue_bn_finalize(gpu, N, H, C, k, groups):
     beta = torch.randn(C, device=gpu)
     fin = None
     src, cnt, rows = part, T, bm
+    if not groups:
+        assert T <= nat.pfin_cap(C)
     if groups:
         cap = (256 // C) * 8
         gs = 2
@@ -451,9 +455,11 @@ def test_direct_wgrad_matches_reference_and_generic(gpu, N, H, C):
     assert _rel(dw, dw_gen) < 1e-3
 
 
-@pytest.mark.parametrize("N,H,C,with_add", [(8, 32, 16, True), (128, 32, 16, False),
-                                            (16, 16, 32, True), (16, 8, 64, False)])
-def test_direct_dgrad_fused_bn_backward(gpu, N, H, C, with_add):
+@pytest.mark.parametrize("N,H,C,with_add,cnt", [(8, 32, 16, True, 16), (128, 32, 16, False, 16),
+                                                (16, 16, 32, True, 16), (16, 8, 64, False, 16),
+                                                (128, 32, 16, True, 512), (128, 16, 32, False, 512),
+                                                (128, 8, 64, True, 128)])
+def test_direct_dgrad_fused_bn_backward(gpu, N, H, C, with_add, cnt):
     """BnBwdPre: the direct dgrad applies the pending BN+ReLU backward to its input
     while staging (dh = a*g - b - c*xhat + add, coefficients combined from the
     producer's partial sums), writes dh, and == bn_bwd_finalize + bn_bwd_apply + dgrad."""
@@ -473,7 +479,7 @@ def test_direct_dgrad_fused_bn_backward(gpu, N, H, C, with_add):
     xf, gf = x.float().reshape(-1, C), da.float().reshape(-1, C)
     g = gf * ((xf * scale + shift) > 0).float()
     xh = (xf - mean) * rstd
-    cnt = 16
+    assert cnt <= nat.pfin_cap(C)
     part = torch.stack([torch.stack([gg.sum(0), (gg * hh).sum(0)])
                         for gg, hh in zip(g.chunk(cnt), xh.chunk(cnt))]).contiguous()
     dh = torch.empty_like(da)
