@@ -69,12 +69,21 @@ def main():
         t_d = timeit(lambda: fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx)) if C >= 16 else 0
         gw = torch.empty(k, k, C, K, device=dev)
         t_w = timeit(lambda: fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, **pre))
+        # roofline floor: bf16 x, w read once, y written once (5 TB/s), 1.3 PF/s bf16 MFMA
+        nbytes = 2.0 * (x.numel() + w.numel() + out.numel())
+        floor = max(nbytes / 5e12, flops / 1.3e15) * 1e6
+        t_lib = 0.0
+        if k == 1 and s == 1:   # plain GEMM of the same shape through hipBLASLt (library reference)
+            x2, w2 = x.view(-1, C), w.view(K, C).t()
+            t_lib = timeit(lambda: torch.mm(x2, w2, out=out.view(-1, K)))
         r = {"name": name, "gflop": flops / 1e9, "fwd_us": t_f, "dgrad_us": t_d, "wgrad_us": t_w,
+             "floor_us": floor, "hipblaslt_us": t_lib,
              "fwd_tf": flops / t_f / 1e6, "dgrad_tf": flops / t_d / 1e6 if t_d else 0,
              "wgrad_tf": flops / t_w / 1e6}
         res.append(r)
         print(f"{name:22s} {flops/1e9:7.2f} GF | fwd {t_f:8.1f}us {r['fwd_tf']:6.1f}TF | "
-              f"dgrad {t_d:8.1f}us {r['dgrad_tf']:6.1f}TF | wgrad {t_w:8.1f}us {r['wgrad_tf']:6.1f}TF",
+              f"dgrad {t_d:8.1f}us {r['dgrad_tf']:6.1f}TF | wgrad {t_w:8.1f}us {r['wgrad_tf']:6.1f}TF"
+              f" | floor {floor:7.1f}us | hipblaslt-mm {t_lib:7.1f}us",
               flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/kernels.json", "w") as fh:
