@@ -527,6 +527,9 @@ PYBIND11_MODULE(_C, m) {
         "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");
   m.def("set_conv_direct", &set_conv_direct,
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
+  m.def("set_conv_pipeline", &set_conv_pipeline,
+        "enable/disable the 2-deep pipelined implicit-GEMM loop for C % 64 == 0 "
+        "(default: on unless DTR_CONV_PIPE=0)");
   m.def("set_fin_version", &set_fin_version,
         "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
   m.def("pfin_cap", &pfin_cap, "max partials a consumer prologue combines for C channels");

@@ -143,35 +143,54 @@ __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
 // BN-input row vectors each epilogue thread will combine are independent of the
 // GEMM, so kernels issue their loads at kernel start (epi_prefetch) and the
 // epilogue finds them in registers instead of paying a global round trip.
-template <int BM, int BN, int WM>
+// XO ("x only"): prefetch just the BN-backward operands (BN input rows + the
+// per-column scale/shift/mean/rstd) -- the implicit-GEMM dgrad, whose occupancy
+// cannot afford the residual / accumulate registers too.
+template <int BM, int BN, int WM, bool XO = false>
 struct EpiPre {
   static constexpr bool ON = EpiLayout<BM, BN, WM>::PHASES == 1;
+  static constexpr bool X_ONLY = XO;
   static constexpr int RIT = ON ? (EpiLayout<BM, BN, WM>::PR + EpiLayout<BM, BN, WM>::RPP - 1) /
                                       EpiLayout<BM, BN, WM>::RPP
                                 : 1;
-  bf16x8 res[RIT], acc[RIT], x[RIT];
+  static constexpr int RR = XO ? 1 : RIT;
+  bf16x8 res[RR], acc[RR], x[RIT];
+  f32x4 bsc[XO ? 2 : 1], bsh[XO ? 2 : 1], bmu[XO ? 2 : 1], brs[XO ? 2 : 1];
 };
 
-template <int BM, int BN, int WM, int FLAGS>
+template <int BM, int BN, int WM, int FLAGS, bool XO = false>
 __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0, const int n0,
-                                             EpiPre<BM, BN, WM>& P) {
+                                             EpiPre<BM, BN, WM, XO>& P) {
   using EL = EpiLayout<BM, BN, WM>;
-  if constexpr (EpiPre<BM, BN, WM>::ON) {
+  if constexpr (EpiPre<BM, BN, WM, XO>::ON) {
     const int tid = threadIdx.x;
     const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
     const int col0 = n0 + cc * 8;
     const bf16x8 zero8 = {};
 #pragma unroll
-    for (int it = 0; it < EpiPre<BM, BN, WM>::RIT; ++it) {
+    for (int it = 0; it < EpiPre<BM, BN, WM, XO>::RIT; ++it) {
       const int row = m0 + r0 + it * EL::RPP;
       const bool ok = col0 < args.Ncol && r0 + it * EL::RPP < EL::PR && row < args.M;
       const long o = (long)row * args.Ncol + col0;
-      P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
-                                        : zero8;
-      P.acc[it] = (ok && args.accumulate && !args.out_f32)
-                      ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
+      if constexpr (!XO) {
+        P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
+                                          : zero8;
+        P.acc[it] = (ok && args.accumulate && !args.out_f32)
+                        ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
+      }
       if constexpr ((FLAGS & F_BNB) != 0)
         P.x[it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
+    }
+    if constexpr (XO && (FLAGS & F_BNB) != 0) {
+      const bool colok = col0 < args.Ncol;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        P.bsc[h] = colok ? *reinterpret_cast<const f32x4*>(args.bnb_scale + col0 + 4 * h) : z;
+        P.bsh[h] = colok ? *reinterpret_cast<const f32x4*>(args.bnb_shift + col0 + 4 * h) : z;
+        P.bmu[h] = colok ? *reinterpret_cast<const f32x4*>(args.bnb_mean + col0 + 4 * h) : z;
+        P.brs[h] = colok ? *reinterpret_cast<const f32x4*>(args.bnb_rstd + col0 + 4 * h) : z;
+      }
     }
   }
 }
@@ -181,11 +200,11 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN
 // backward sums (BNB) and the optional last-arriver finalize.  Entered after a
 // workgroup barrier (the caller's LDS is dead).
-template <int BM, int BN, int WM, int WN, int FLAGS>
+template <int BM, int BN, int WM, int WN, int FLAGS, bool XO = false>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                               char* smem, const int m0, const int n0,
-                                              const EpiPre<BM, BN, WM>* pre = nullptr) {
+                                              const EpiPre<BM, BN, WM, XO>* pre = nullptr) {
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -217,12 +236,22 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   float bnb_t1 = 0.f, bnb_t2 = 0.f;   // BNB column totals (thread tid < BN)
   float bsc[8], bsh[8], bmu[8], brs[8];
   if constexpr (BNB) {
+    if (XO && EpiPre<BM, BN, WM, XO>::ON && pre) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bsc[j] = colok ? args.bnb_scale[col0 + j] : 0.f;
-      bsh[j] = colok ? args.bnb_shift[col0 + j] : 0.f;
-      bmu[j] = colok ? args.bnb_mean[col0 + j] : 0.f;
-      brs[j] = colok ? args.bnb_rstd[col0 + j] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        bsc[j] = pre->bsc[XO ? j / 4 : 0][j % 4];
+        bsh[j] = pre->bsh[XO ? j / 4 : 0][j % 4];
+        bmu[j] = pre->bmu[XO ? j / 4 : 0][j % 4];
+        brs[j] = pre->brs[XO ? j / 4 : 0][j % 4];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bsc[j] = colok ? args.bnb_scale[col0 + j] : 0.f;
+        bsh[j] = colok ? args.bnb_shift[col0 + j] : 0.f;
+        bmu[j] = colok ? args.bnb_mean[col0 + j] : 0.f;
+        brs[j] = colok ? args.bnb_rstd[col0 + j] : 0.f;
+      }
     }
   }
   float wn_run = 0.f, wmean_run = 0.f, wm2_run = 0.f;  // STATS, thread tid < BN owns column tid
@@ -238,7 +267,8 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // (the BN-input loads of dgrad+BNB only: batching the residual / accumulate
     // loads cost more occupancy than it gained -- measured on the ImageNet shapes.)
     constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
-    constexpr bool PREL = EpiPre<BM, BN, WM>::ON;
+    constexpr bool PREL = EpiPre<BM, BN, WM, XO>::ON;
+    constexpr bool PRER = PREL && !XO;   // residual / accumulate rows prefetched too
     constexpr bool BATCH = BNB;
     bf16x8 lx[BATCH ? RIT : 1];
     if (BATCH && !(PREL && pre)) {
@@ -285,7 +315,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const long o = (long)row * NC + col0;
       if (args.residual) {
-        const bf16x8 rv = (PREL && pre) ? pre->res[PREL ? it : 0]
+        const bf16x8 rv = (PRER && pre) ? pre->res[PRER ? it : 0]
                                         : *reinterpret_cast<const bf16x8*>(args.residual + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
@@ -306,7 +336,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         continue;
       }
       if (args.accumulate) {
-        const bf16x8 av = (PREL && pre) ? pre->acc[PREL ? it : 0]
+        const bf16x8 av = (PRER && pre) ? pre->acc[PRER ? it : 0]
                                         : *reinterpret_cast<const bf16x8*>(args.out + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)av[j];

@@ -27,7 +27,9 @@
 //           gradient g = d_a * [x*scale+shift > 0]:  per-tile sum(g) and
 //           sum(g * xhat), so no separate pass re-reads d_a and x.
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "conv_epilogue.h"
 
@@ -36,8 +38,23 @@ namespace dtr {
 // NBUF = LDS tile buffers: 2 = one barrier per K tile (register prefetch written
 // into the other buffer); 1 = two barriers per K tile but half the LDS, so more
 // workgroups per CU (the 128x128 ImageNet tiles).
-template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF = 2>
+//
+// FAST (every A channel count a multiple of BK, tensors < 2^30 elements: all
+// ImageNet layers but the stem) runs a 2-deep register pipeline: the loads of
+// K tile t+2 are issued while tile t is multiplied and tile t+1 (loaded one
+// iteration earlier) is written to LDS, so each global round trip is hidden
+// behind two MFMA blocks and a barrier instead of one.  The whole FAST loop is
+// branch-free (out-of-range chunks are buffer loads at an out-of-range offset,
+// the BN+ReLU padding mask is a select), so hipcc emits counted vmcnt(N) waits
+// instead of vmcnt(0) per chunk.  The 1-deep loop measured latency-bound on the
+// 7x7 / 14x14 layers: ~1 us per K tile whatever the tile's MFMA work.
+// Register budget of the FAST loop: at least 2 waves per SIMD (<= 256 VGPRs).
+// Without the hint hipcc spent 300+ VGPRs + 100 AGPRs on the 128x128 tiles (1
+// wave per SIMD: 2x slower on the 56x56 layers); a budget for the LDS-bound
+// occupancy of the smaller tiles (3-4 waves) spills the two register sets.
+template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, bool FAST, int NBUF = 2>
 __global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(FAST ? 2 : 1, 8)))
 conv_gemm_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
@@ -103,6 +120,19 @@ conv_gemm_kernel(GemmArgs args) {
   const bf16x8 zero8 = {};
 
   unsigned amask = 0;   // PRE: which A chunks of the in-flight tile are real pixels
+  // PRE: input channel of this thread's 8-channel group in the in-flight tile, and
+  // its BN scale/shift, read from the LDS table right after the tile's loads are
+  // issued so the table read overlaps the current tile's MFMAs (reading it at LDS
+  // store time put an LDS round trip + integer division on every K tile's
+  // critical path: +15..58 us per ImageNet conv).
+  int pre_ci = 0;
+  f32x4 s0, s1, b0, b1;
+  auto load_pre = [&]() {
+    s0 = *reinterpret_cast<const f32x4*>(pre_s + pre_ci);
+    s1 = *reinterpret_cast<const f32x4*>(pre_s + pre_ci + 4);
+    b0 = *reinterpret_cast<const f32x4*>(pre_s + Acin + pre_ci);
+    b1 = *reinterpret_cast<const f32x4*>(pre_s + Acin + pre_ci + 4);
+  };
 
   // Fast gather (every A channel count a multiple of BK: all ImageNet layers but
   // the stem): a K tile then lies inside ONE filter tap, so (tap, r, c) are
@@ -131,6 +161,7 @@ conv_gemm_kernel(GemmArgs args) {
     const bool kv = kb < KD;
     const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
     const int ci = kb - tap * Acin + kg * 8;
+    if constexpr (PRE) pre_ci = kv ? ci : 0;
     const int rr = tap / g.kw, cc = tap - rr * g.kw;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
@@ -175,6 +206,7 @@ conv_gemm_kernel(GemmArgs args) {
     const bool kvalid = k < KD;
     const int tap = kvalid ? k / Acin : 0;
     const int ci = k - tap * Acin;
+    if constexpr (PRE) pre_ci = kvalid ? ci : 0;
     const int rr = tap / g.kw, cc = tap - rr * g.kw;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
@@ -221,18 +253,9 @@ conv_gemm_kernel(GemmArgs args) {
 
   // PRE is applied here, after the MFMAs of the previous tile, so the prefetched
   // loads stay in flight across them (applying it in load_tile forced the wait).
-  auto store_tile = [&](int buf, int t) {
+  auto store_tile = [&](int buf) {
     bf16* A = As + buf * BM * BK;
     bf16* B = Bs + buf * BN * BK;
-    f32x4 s0, s1, b0, b1;   // this thread's 8 channels: one table read for all its chunks
-    if constexpr (PRE) {
-      const int k = t * BK + kg * 8;
-      const int ci = k < KD ? k - (k / Acin) * Acin : 0;
-      s0 = *reinterpret_cast<const f32x4*>(pre_s + ci);
-      s1 = *reinterpret_cast<const f32x4*>(pre_s + ci + 4);
-      b0 = *reinterpret_cast<const f32x4*>(pre_s + Acin + ci);
-      b1 = *reinterpret_cast<const f32x4*>(pre_s + Acin + ci + 4);
-    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int q = tid + i * 256;
@@ -255,33 +278,91 @@ conv_gemm_kernel(GemmArgs args) {
     }
   };
 
+  // ---- FAST path: two register sets (tile parity), everything branch-free ----
+  bf16x8 pa[2][A_PER_T], pb[2][B_PER_T];
+  unsigned pmask[2] = {0u, 0u};
+  int pci[2] = {0, 0};
+  auto issue = [&](int t, auto P) {   // loads of K tile t into set P (t >= KT: zeros)
+    constexpr int p = decltype(P)::value;
+    const int kb = t * BK;                       // uniform
+    const bool kv = kb < KD;
+    const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
+    const int ci = kb - tap * Acin + kg * 8;
+    if constexpr (PRE) pci[p] = kv ? ci : 0;
+    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+    unsigned msk = 0u;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      int off = kOOB;
+      if constexpr (MODE == MODE_FWD) {
+        const int hi = a_h[i] + rr, wi = a_w[i] + cc;
+        const bool ok = kv && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+        off = ok ? ((a_base[i] + hi * g.W + wi) * g.C + ci) * 2 : kOOB;
+        msk |= ok ? (1u << i) : 0u;
+      } else {
+        int hp = a_h[i] - rr, wp = a_w[i] - cc;
+        bool ok = kv && hp >= 0 && wp >= 0;
+        if (g.stride == 2) {
+          ok = ok && ((hp | wp) & 1) == 0;
+          hp >>= 1;
+          wp >>= 1;
+        }
+        ok = ok && hp < g.Ho && wp < g.Wo;
+        off = ok ? ((a_base[i] + hp * g.Wo + wp) * g.K + ci) * 2 : kOOB;
+      }
+      pa[p][i] = bload(rs_a, off);
+    }
+    if constexpr (PRE) pmask[p] = msk;
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      const int nrow = q >> 3;
+      const bool ok = (B_CHUNKS % 256 == 0 || q < B_CHUNKS) && n0 + nrow < NC && kv;
+      int off;
+      if constexpr (MODE == MODE_FWD) off = ((n0 + nrow) * KD + kb + kg * 8) * 2;
+      else off = ((tap * g.C + (n0 + nrow)) * g.K + ci) * 2;
+      pb[p][i] = bload(rs_b, ok ? off : kOOB);
+    }
+  };
+  auto stage = [&](int buf, auto P) {   // set P -> LDS buffer `buf` (BN+ReLU applied)
+    constexpr int p = decltype(P)::value;
+    bf16* A = As + buf * BM * BK;
+    bf16* B = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (A_CHUNKS % 256 == 0 || q < A_CHUNKS) {
+        const int r = q >> 3;
+        bf16x8 v = pa[p][i];
+        if constexpr (PRE) {
+          const u32x4 w = __builtin_bit_cast(u32x4, affine_relu8_reg(v, s0, s1, b0, b1));
+          const unsigned sel = 0u - ((pmask[p] >> i) & 1u);   // all-ones: real pixel
+          const u32x4 u = __builtin_bit_cast(u32x4, v);
+          v = __builtin_bit_cast(bf16x8, (w & sel) | (u & ~sel));
+        }
+        *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int q = tid + i * 256;
+      if (B_CHUNKS % 256 == 0 || q < B_CHUNKS) {
+        const int r = q >> 3;
+        *reinterpret_cast<bf16x8*>(B + r * BK + ((kg ^ (r & 7)) << 3)) = pb[p][i];
+      }
+    }
+  };
+
   f32x4 acc[MR][NR];
 #pragma unroll
   for (int a = 0; a < MR; ++a)
 #pragma unroll
     for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = (KD + BK - 1) / BK;
-  load_tile(0);
-  if constexpr (PRE) {   // BN scale/shift table (finalized here if this is the first consumer)
-    if (args.pfin.cnt > 0) {
-      bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
-    } else {
-      for (int i = tid; i < Acin; i += 256) {
-        pre_s[i] = args.pre_scale[i];
-        pre_s[Acin + i] = args.pre_shift[i];
-      }
-      __syncthreads();
-    }
-  }
-  store_tile(0, 0);
-  __syncthreads();
-
   const int fr = lane & 15, fq = lane >> 4;
-  for (int t = 0; t < KT; ++t) {
-    if (t + 1 < KT) load_tile(t + 1);
-    const bf16* A = As + (NBUF == 2 ? (t & 1) : 0) * BM * BK;
-    const bf16* B = Bs + (NBUF == 2 ? (t & 1) : 0) * BN * BK;
+  auto mma_tile = [&](int buf) {
+    const bf16* A = As + buf * BM * BK;
+    const bf16* B = Bs + buf * BN * BK;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fq;
@@ -301,17 +382,109 @@ conv_gemm_kernel(GemmArgs args) {
 #pragma unroll
         for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
+  };
+
+  const int KT = (KD + BK - 1) / BK;
+  // dgrad + BN-backward sums: the epilogue's BN-input rows and coefficients are
+  // GEMM-independent -> issue their loads now, off the epilogue's critical path.
+  EpiPre<BM, BN, WM, true> epre;
+  if constexpr (FAST) {
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    issue(0, I0{});
+    issue(1, I1{});
+    if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+    if constexpr (PRE) {
+      if (args.pfin.cnt > 0) {
+        bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
+      } else {
+        for (int i = tid; i < Acin; i += 256) {
+          pre_s[i] = args.pre_scale[i];
+          pre_s[Acin + i] = args.pre_shift[i];
+        }
+        __syncthreads();
+      }
+      pre_ci = pci[0];
+      load_pre();
+    }
+    stage(0, I0{});
+    __syncthreads();
+    // iteration t (parity P): loads of t+2 into set P (its tile t is already in
+    // LDS), MFMAs on buffer P, then set !P (tile t+1) -> buffer !P.
+    auto body = [&](int t, auto P) {
+      constexpr int p = decltype(P)::value;
+      issue(t + 2, P);
+      if constexpr (PRE) {
+        pre_ci = pci[p ^ 1];
+        load_pre();
+      }
+      mma_tile(p);
+      stage(p ^ 1, std::integral_constant<int, p ^ 1>{});
+      __syncthreads();
+    };
+    int t = 0;
+    for (; t + 1 < KT; t += 2) {
+      body(t, I0{});
+      body(t + 1, I1{});
+    }
+    if (t < KT) body(t, I0{});
+  } else {   // general gather (runtime `fast` only for the narrow-column tiles)
+  load_tile(0);
+  if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+  if constexpr (PRE) {   // BN scale/shift table (finalized here if this is the first consumer)
+    if (args.pfin.cnt > 0) {
+      bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
+    } else {
+      for (int i = tid; i < Acin; i += 256) {
+        pre_s[i] = args.pre_scale[i];
+        pre_s[Acin + i] = args.pre_shift[i];
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (PRE) load_pre();
+  store_tile(0);
+  __syncthreads();
+
+  for (int t = 0; t < KT; ++t) {
+    if (t + 1 < KT) {
+      load_tile(t + 1);
+      if constexpr (PRE) load_pre();
+    }
+    mma_tile(NBUF == 2 ? (t & 1) : 0);
     if constexpr (NBUF == 1) __syncthreads();   // every wave is done reading the tile
-    if (t + 1 < KT) store_tile(NBUF == 2 ? ((t + 1) & 1) : 0, t + 1);
+    if (t + 1 < KT) store_tile(NBUF == 2 ? ((t + 1) & 1) : 0);
     __syncthreads();
   }
+  }
 
-  conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
+  if constexpr (BNB && EpiPre<BM, BN, WM, true>::ON)
+    conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre);
+  else
+    conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
+static int g_pipe_enabled = -1;   // -1: read DTR_CONV_PIPE once (default on)
+void set_conv_pipeline(int enabled) { g_pipe_enabled = enabled ? 1 : 0; }
+
+// FAST-path eligibility (see the kernel): must match the kernel's own `fast` test.
+static bool conv_gemm_fast(const GemmArgs& a, int mode) {
+  if (g_pipe_enabled < 0) {
+    const char* e = std::getenv("DTR_CONV_PIPE");
+    g_pipe_enabled = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!g_pipe_enabled) return false;
+  const ConvGeom& g = a.g;
+  const int Acin = (mode == MODE_FWD) ? g.C : g.K;
+  const long a_elems = (mode == MODE_FWD) ? (long)g.N * g.H * g.W * g.C
+                                          : (long)g.N * g.Ho * g.Wo * g.K;
+  const long b_elems = (long)g.kh * g.kw * g.C * g.K;
+  return Acin % 64 == 0 && a_elems < (1L << 30) && b_elems < (1L << 30);
+}
+
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_cfg(const GemmArgs& a, hipStream_t s) {
   constexpr int NBUF = 2;   // 1 measured neutral on the ImageNet 128x128 tiles
@@ -321,8 +494,17 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
   lds = std::max(lds, EpiLayout<BM, BN, WM>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, NBUF>), grid, dim3(256), lds,
-                     s, a);
+  // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles
+  if constexpr (BN >= 64) {
+    if (conv_gemm_fast(a, MODE)) {
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
+                         dim3(256), lds, s, a);
+      DTR_CHECK_LAUNCH();
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, NBUF>), grid,
+                     dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
 }
 

@@ -36,6 +36,7 @@ def main():
     if len(sys.argv) > 2 and sys.argv[2] == "imagenet":
         n = 20
         shapes = [(56, 64, 256, 1), (56, 64, 64, 3), (28, 128, 128, 3), (14, 256, 256, 3),
+                  (28, 128, 512, 1), (7, 2048, 512, 1), (7, 512, 512, 3),
                   (14, 1024, 256, 1), (7, 512, 2048, 1)]
     for H, C, K, k in shapes:
         N = batch
