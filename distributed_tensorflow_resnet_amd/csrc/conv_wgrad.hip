@@ -18,6 +18,7 @@
 // TF HWIO layout of the master gradient.  Optional fused BN+ReLU is applied to
 // X while staging (the pre-activation tensor is never stored).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -30,8 +31,14 @@ __device__ __forceinline__ int unit_swz(int row) {
   else return (row / (8 / U)) & (U - 1);
 }
 
-template <int BM, int BN, int WM, int WN, bool PRE>
+// FAST (both tensors < 2^30 elements): 2-deep branch-free register pipeline, as in
+// conv_gemm.hip -- the loads of K tile t+2 are in flight while tile t is multiplied
+// and tile t+1 is written to LDS; a thread's B column (tap, ci) is fixed for the
+// whole loop, so its BN+ReLU scale/shift live in registers (no LDS table, no
+// per-chunk channel division at store time).
+template <int BM, int BN, int WM, int WN, bool PRE, bool FAST = false>
 __global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(FAST ? 2 : 1, 8)))
 conv_wgrad_kernel(WgradArgs args) {
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -60,7 +67,7 @@ conv_wgrad_kernel(WgradArgs args) {
   const int p_begin = split * args.px_per_split;
   const int p_end = min(P, p_begin + args.px_per_split);
 
-  if constexpr (PRE) {
+  if constexpr (PRE && !FAST) {
     for (int i = tid; i < Cin; i += 256) {
       pre_s[i] = args.pre_scale[i];
       pre_s[Cin + i] = args.pre_shift[i];
@@ -227,20 +234,13 @@ conv_wgrad_kernel(WgradArgs args) {
     for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int KT = (p_end - p_begin + BK - 1) / BK;
-  if (KT > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
 
   const int gq = lane >> 4;           // 16-lane group
   const int li = lane & 15;
   const int qr = li >> 2, pc = li & 3;  // row-in-block, 4-column piece
-
-  for (int t = 0; t < KT; ++t) {
-    if (t + 1 < KT) load_tile(t + 1);
-    const bf16* A = As + (t & 1) * BK * BM;
-    const bf16* B = Bs + (t & 1) * BK * BN;
+  auto mma_tile = [&](int buf) {
+    const bf16* A = As + buf * BK * BM;
+    const bf16* B = Bs + buf * BK * BN;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int r1 = ks * 32 + 4 * gq + qr;  // pixel row for elements 0..3
@@ -267,8 +267,117 @@ conv_wgrad_kernel(WgradArgs args) {
 #pragma unroll
         for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
     }
-    if (t + 1 < KT) store_tile((t + 1) & 1);
+  };
+
+  if constexpr (FAST) {
+    // ---- 2-deep pipeline: register set P holds K tile t with t % 2 == P ----
+    bf16x8 pa[2][A_PER_T], pb[2][B_PER_T];
+    unsigned pmask[2] = {0u, 0u};
+    f32x4 s0, s1, b0, b1;   // this thread's fixed 8 B channels (bci .. bci+7)
+    if constexpr (PRE) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      s0 = bcol_ok ? *reinterpret_cast<const f32x4*>(args.pre_scale + bci) : z;
+      s1 = bcol_ok ? *reinterpret_cast<const f32x4*>(args.pre_scale + bci + 4) : z;
+      b0 = bcol_ok ? *reinterpret_cast<const f32x4*>(args.pre_shift + bci) : z;
+      b1 = bcol_ok ? *reinterpret_cast<const f32x4*>(args.pre_shift + bci + 4) : z;
+    }
+    auto issue = [&](int t, auto P) {   // t >= KT: every chunk out of range -> zeros
+      constexpr int p = decltype(P)::value;
+      const int pbase = p_begin + t * BK;
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i) {
+        const int q = tid + i * 256;
+        const int row = q / A_CPR, cc = q % A_CPR;
+        const int px = pbase + row;
+        const bool ok = (A_CH % 256 == 0 || q < A_CH) && px < p_end && m0 + cc * 8 < Cout;
+        pa[p][i] = bload(rs_dy, ok ? (px * Cout + m0 + cc * 8) * 2 : kOOB);
+      }
+      unsigned msk = 0u;
+#pragma unroll
+      for (int i = 0; i < B_PER_T; ++i) {
+        const int q = tid + i * 256;
+        const int px = pbase + q / B_CPR;
+        const int hi = b_ho[i] * g.stride - g.pad + bdr, wi = b_wo[i] * g.stride - g.pad + bdc;
+        const bool ok = (B_CH % 256 == 0 || q < B_CH) && px < p_end && bcol_ok &&
+                        (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+        pb[p][i] = bload(rs_x, ok ? (((b_img[i] * g.H + hi) * g.W + wi) * Cin + bci) * 2 : kOOB);
+        msk |= ok ? (1u << i) : 0u;
+        // advance this chunk's pixel by BK for the next k-step
+        b_wo[i] += d_wo;
+        b_ho[i] += d_ho;
+        const bool wrap = b_wo[i] >= g.Wo;
+        b_wo[i] -= wrap ? g.Wo : 0;
+        b_ho[i] += wrap ? 1 : 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {   // host: BK / Wo + 1 <= 3 * Ho, so 3 rounds suffice
+          const bool nxt = b_ho[i] >= g.Ho;
+          b_ho[i] -= nxt ? g.Ho : 0;
+          b_img[i] += nxt ? 1 : 0;
+        }
+      }
+      if constexpr (PRE) pmask[p] = msk;
+    };
+    auto stage = [&](int buf, auto P) {
+      constexpr int p = decltype(P)::value;
+      bf16* A = As + buf * BK * BM;
+      bf16* B = Bs + buf * BK * BN;
+#pragma unroll
+      for (int i = 0; i < A_PER_T; ++i) {
+        const int q = tid + i * 256;
+        if (A_CH % 256 == 0 || q < A_CH) {
+          const int row = q / A_CPR, cc = q % A_CPR;
+          const int col = (((cc >> 1) ^ unit_swz<UA>(row)) << 4) + ((cc & 1) << 3);
+          *reinterpret_cast<bf16x8*>(A + row * BM + col) = pa[p][i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < B_PER_T; ++i) {
+        const int q = tid + i * 256;
+        if (B_CH % 256 == 0 || q < B_CH) {
+          const int row = q / B_CPR, cc = q % B_CPR;
+          const int col = (((cc >> 1) ^ unit_swz<UB>(row)) << 4) + ((cc & 1) << 3);
+          bf16x8 v = pb[p][i];
+          if constexpr (PRE) {
+            const u32x4 w = __builtin_bit_cast(u32x4, affine_relu8_reg(v, s0, s1, b0, b1));
+            const unsigned sel = 0u - ((pmask[p] >> i) & 1u);
+            const u32x4 u = __builtin_bit_cast(u32x4, v);
+            v = __builtin_bit_cast(bf16x8, (w & sel) | (u & ~sel));
+          }
+          *reinterpret_cast<bf16x8*>(B + row * BN + col) = v;
+        }
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    issue(0, I0{});
+    issue(1, I1{});
+    stage(0, I0{});
     __syncthreads();
+    auto body = [&](int t, auto P) {
+      constexpr int p = decltype(P)::value;
+      issue(t + 2, P);
+      mma_tile(p);
+      stage(p ^ 1, std::integral_constant<int, p ^ 1>{});
+      __syncthreads();
+    };
+    int t = 0;
+    for (; t + 1 < KT; t += 2) {
+      body(t, I0{});
+      body(t + 1, I1{});
+    }
+    if (t < KT) body(t, I0{});
+  } else {
+    if (KT > 0) {
+      load_tile(0);
+      store_tile(0);
+    }
+    __syncthreads();
+    for (int t = 0; t < KT; ++t) {
+      if (t + 1 < KT) load_tile(t + 1);
+      mma_tile(t & 1);
+      if (t + 1 < KT) store_tile((t + 1) & 1);
+      __syncthreads();
+    }
   }
 
   float* out = args.part + (long)split * Cout * NT;
@@ -285,12 +394,43 @@ conv_wgrad_kernel(WgradArgs args) {
   }
 }
 
+static int g_wpipe_enabled = -1;   // -1: read DTR_CONV_PIPE once (default on)
+void set_wgrad_pipeline(int enabled) { g_wpipe_enabled = enabled ? 1 : 0; }
+
+// FAST eligibility: 32-bit buffer offsets, C % 8 == 0 (16-B channel chunks), and the
+// branch-free pixel stepping's 3 image-wrap rounds cover BK = 64 pixels.
+static bool wgrad_fast(const WgradArgs& a) {
+  if (g_wpipe_enabled < 0) {
+    const char* e = std::getenv("DTR_CONV_PIPE");
+    g_wpipe_enabled = (e && e[0] == '0') ? 0 : 1;
+  }
+  const ConvGeom& g = a.g;
+  const long x_elems = (long)g.N * g.H * g.W * g.C;
+  const long dy_elems = (long)g.N * g.Ho * g.Wo * g.K;
+  // (A/B on the ImageNet shapes: 1.05-1.2x at 14x14 / 7x7 outputs, 0.91-1.04x at
+  // 56x56 / 28x28, where the occupancy of the one-set loop hides the latency)
+  return g_wpipe_enabled && x_elems < (1L << 30) && dy_elems < (1L << 30) &&
+         64 / g.Wo + 1 <= 3 * g.Ho && g.Ho <= 14;
+}
+
 template <int BM, int BN, int WM, int WN>
 static void wg_launch(const WgradArgs& a, hipStream_t s) {
   const int NT = a.g.kh * a.g.kw * a.g.C;
   size_t lds = (size_t)2 * 64 * (BM + BN) * sizeof(bf16);
-  if (a.pre_scale) lds += (size_t)2 * a.g.C * sizeof(float);
   dim3 grid((NT + BN - 1) / BN, (a.g.K + BM - 1) / BM, a.splits);
+  if constexpr (BM >= 64) {   // the pipelined loop: ImageNet-size tiles
+    if (wgrad_fast(a)) {
+      if (a.pre_scale)
+        hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), lds,
+                           s, a);
+      else
+        hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256),
+                           lds, s, a);
+      DTR_CHECK_LAUNCH();
+      return;
+    }
+  }
+  if (a.pre_scale) lds += (size_t)2 * a.g.C * sizeof(float);
   if (a.pre_scale)
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, a);
   else

@@ -122,7 +122,8 @@ void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
 void set_conv_direct(int enabled);
-void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loop (DTR_CONV_PIPE)
+void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loops (DTR_CONV_PIPE)
+void set_wgrad_pipeline(int enabled);  // (the wgrad half of it)
 void set_fin_version(int v);   // BN finalize kernel variant (DTR_FIN_V)
 int conv_gemm_bm(int M, int Ncol);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks

@@ -44,7 +44,7 @@ def main():
     batch = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = 10
-    tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0]}
+    tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
     for H, C, K, k, s in SHAPES:
         N = batch
         g = fn.ConvGeom(N, H, H, C, K, k, k, s)
@@ -59,23 +59,28 @@ def main():
         sc, sh = torch.rand(max(C, K), device=dev), torch.rand(max(C, K), device=dev)
         part = torch.empty(-(-Mf // nat.conv_gemm_bm(Mf, K)) * 2 * K, device=dev)
         bpart = torch.empty(-(-Md // nat.conv_gemm_bm(Md, C)) * 2 * C, device=dev)
-        pf, pd = nat.Plan(), nat.Plan()
+        sp, pps = nat.wgrad_pick_splits(gl)
+        wpart = torch.empty(sp * k * k * C * K, device=dev)
+        pf, pd, pw = nat.Plan(), nat.Plan(), nat.Plan()
         for _ in range(n):
+            pw.conv_wgrad(res.data_ptr(), x.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                          wpart.data_ptr(), gl, sp, pps)
             pf.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, res.data_ptr(),
                          sc.data_ptr(), sh.data_ptr(), 0, 0, part.data_ptr(), 0, gl, [], [], [],
                          [], [], 0.997, 1e-5, 1)
             pd.conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
                          gl, [x.data_ptr(), sc.data_ptr(), sh.data_ptr(), sc.data_ptr(),
                               sh.data_ptr(), bpart.data_ptr()], [], [], [], [], 0.997, 1e-5, 1)
-        ts = {(p, v): [] for p in ("fwd", "dgrad") for v in (0, 1)}
+        passes = (("fwd", pf), ("dgrad", pd), ("wgrad", pw))
+        ts = {(p, v): [] for p, _ in passes for v in (0, 1)}
         for _ in range(rounds):
             for v in (0, 1):
                 nat.set_conv_pipeline(v)
-                ts[("fwd", v)].append(dev_time(pf))
-                ts[("dgrad", v)].append(dev_time(pd))
+                for p, plan in passes:
+                    ts[(p, v)].append(dev_time(plan))
         nat.set_conv_pipeline(1)
         line = []
-        for p in ("fwd", "dgrad"):
+        for p, _ in passes:
             a, b = statistics.median(ts[(p, 0)]), statistics.median(ts[(p, 1)])
             tot[p][0] += a
             tot[p][1] += b
