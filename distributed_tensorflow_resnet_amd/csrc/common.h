@@ -41,6 +41,17 @@ __device__ __forceinline__ s16x4 lds_read_tr16(const void* p) {
       (__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// Workgroup barrier that orders LDS only: s_waitcnt lgkmcnt(0) + s_barrier.
+// __syncthreads() is a release on ALL address spaces, so with global stores in
+// flight it also waits vmcnt(0) -- in a multi-phase epilogue that put every
+// phase's store round trip on the critical path.  Use where the barrier only
+// protects LDS data (staging tiles, reduction planes).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

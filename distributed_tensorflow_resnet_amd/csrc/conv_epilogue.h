@@ -136,7 +136,7 @@ __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) wred[wave * BN + lane * 8 + j] = v[j];
   }
-  __syncthreads();
+  lds_barrier();   // LDS-only: the caller's global stores stay in flight
 }
 
 // Epilogue operand prefetch (single-phase tiles): the residual / accumulate-into /
@@ -264,13 +264,15 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // Operand loads of this phase's rows, all issued before the staging writes and
     // the barrier so they overlap them (one round trip, not one per row iteration);
     // kernels that prefetched them at kernel start (EpiPre) skip this.
-    // (the BN-input loads of dgrad+BNB only: batching the residual / accumulate
-    // loads cost more occupancy than it gained -- measured on the ImageNet shapes.)
+    // (the BN-input loads of dgrad+BNB; the residual rows too in the multi-phase
+    // 128x128 tiles, whose occupancy is LDS-bound anyway -- batching them in the
+    // single-phase tiles cost more occupancy than it gained on the ImageNet shapes.)
     constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
     constexpr bool PREL = EpiPre<BM, BN, WM, XO>::ON;
     constexpr bool PRER = PREL && !XO;   // residual / accumulate rows prefetched too
     constexpr bool BATCH = BNB;
-    bf16x8 lx[BATCH ? RIT : 1];
+    constexpr bool BATCHR = EL::PHASES > 1 && !BNB;   // (BNB: no residual; the registers spill)
+    bf16x8 lx[BATCH ? RIT : 1], lr[BATCHR ? RIT : 1];
     if (BATCH && !(PREL && pre)) {
 #pragma unroll
       for (int it = 0; it < RIT; ++it) {
@@ -278,6 +280,15 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         if (!colok || r >= nph) continue;
         const long o = (long)(prow0 + r) * NC + col0;
         if constexpr (BNB) lx[BATCH ? it : 0] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+      }
+    }
+    if (BATCHR && args.residual) {
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int r = r0 + it * EL::RPP;
+        const bool ok = colok && r < nph;
+        const long o = (long)(prow0 + (ok ? r : 0)) * NC + (ok ? col0 : 0);
+        lr[BATCHR ? it : 0] = *reinterpret_cast<const bf16x8*>(args.residual + o);
       }
     }
     if ((wm * WTM) / EL::PR == ph) {
@@ -294,7 +305,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
             cs[(rbase + a * 16 + fq * 4 + i) * EL::LDC + cl] = acc[a][b][i] + bias;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // Pass 1: values of this thread's rows (residual / accumulate, ONE bf16
     // rounding) kept in registers; BN sums accumulated.  Global stores are issued
     // only AFTER the statistics' barriers: a __syncthreads() waits for every
@@ -316,6 +327,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       const long o = (long)row * NC + col0;
       if (args.residual) {
         const bf16x8 rv = (PRER && pre) ? pre->res[PRER ? it : 0]
+                          : BATCHR      ? lr[BATCHR ? it : 0]
                                         : *reinterpret_cast<const bf16x8*>(args.residual + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
@@ -370,7 +382,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         const float t = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
         mean_s[tid] = t / (float)nph;
       }
-      __syncthreads();
+      lds_barrier();
       float q[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[j] = 0.f;
@@ -418,7 +430,8 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
       }
     }
-    if constexpr (EL::PHASES > 1) __syncthreads();  // the next phase overwrites the tile
+    // the next phase overwrites the tile (LDS-only: this phase's stores stay in flight)
+    if constexpr (EL::PHASES > 1) lds_barrier();
   }
 
   if constexpr (STATS) {

@@ -48,13 +48,14 @@ namespace dtr {
 // the BN+ReLU padding mask is a select), so hipcc emits counted vmcnt(N) waits
 // instead of vmcnt(0) per chunk.  The 1-deep loop measured latency-bound on the
 // 7x7 / 14x14 layers: ~1 us per K tile whatever the tile's MFMA work.
-// Register budget of the FAST loop: at least 2 waves per SIMD (<= 256 VGPRs).
-// Without the hint hipcc spent 300+ VGPRs + 100 AGPRs on the 128x128 tiles (1
-// wave per SIMD: 2x slower on the 56x56 layers); a budget for the LDS-bound
-// occupancy of the smaller tiles (3-4 waves) spills the two register sets.
+// Register budget: at least 2 waves per SIMD (<= 256 VGPRs+AGPRs), the LDS-bound
+// occupancy of the 128x128 tiles.  Without the hint hipcc spent 288-336 registers
+// on every 128x128 instantiation (1 wave per SIMD; the pipelined loop 2x slower
+// on the 56x56 layers); a budget for the higher LDS-bound occupancy of the smaller
+// tiles (3-4 waves) spills the two register sets of the FAST loop.
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, bool FAST, int NBUF = 2>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(FAST ? 2 : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(2, 8)))
 conv_gemm_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
@@ -485,9 +486,15 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   const long a_elems = (mode == MODE_FWD) ? (long)g.N * g.H * g.W * g.C
                                           : (long)g.N * g.Ho * g.Wo * g.K;
   const long b_elems = (long)g.kh * g.kw * g.C * g.K;
-  // K loops of 1-3 tiles gain nothing from the deeper pipeline and lose occupancy
-  // to its second register set (A/B: 0.93-0.95x on the 1x1 C=64/128 forwards).
-  return Acin % 64 == 0 && a.Kdim >= 256 && a_elems < (1L << 30) && b_elems < (1L << 30);
+  if (!(Acin % 64 == 0 && a_elems < (1L << 30) && b_elems < (1L << 30))) return false;
+  // Where the deeper pipeline pays (scripts/ab_conv_gemm.py, ImageNet RN50 shapes,
+  // both loops at 2 waves/SIMD): K loops of >= 4 tiles, and
+  //   forward: >= 128 output channels (1.02-1.24x; the 64-column 56x56 convs
+  //            run 0.81-0.83x: their single-set loop keeps more tiles per CU);
+  //   dgrad:   >= 16k rows (1.06-1.16x at 14x14..56x56; the 7x7 grids of <= 200
+  //            tiles run 0.88-0.95x).
+  if (a.Kdim < 256) return false;
+  return mode == MODE_FWD ? a.Ncol >= 128 : a.M >= 16384;
 }
 
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>

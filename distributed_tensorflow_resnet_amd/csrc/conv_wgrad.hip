@@ -38,7 +38,7 @@ __device__ __forceinline__ int unit_swz(int row) {
 // per-chunk channel division at store time).
 template <int BM, int BN, int WM, int WN, bool PRE, bool FAST = false>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(FAST ? 2 : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(2, 8)))
 conv_wgrad_kernel(WgradArgs args) {
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;

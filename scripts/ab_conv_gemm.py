@@ -45,7 +45,9 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = 10
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
-    for H, C, K, k, s in SHAPES:
+    only = os.environ.get("AB_SHAPES")   # e.g. "56,256,64,1,1;28,128,128,3,1"
+    shapes = [tuple(int(v) for v in t.split(",")) for t in only.split(";")] if only else SHAPES
+    for H, C, K, k, s in shapes:
         N = batch
         g = fn.ConvGeom(N, H, H, C, K, k, k, s)
         gl = g.as_list()
