@@ -263,11 +263,11 @@ static Launch mk_avgpool_bwd(ptr_t dp, ptr_t dx, int N, int HW, int C) {
 
 static Launch mk_softmax_xent(ptr_t logits, int ld, ptr_t labels, int N, int classes,
                               ptr_t loss_sum, ptr_t correct, ptr_t dlogits, ptr_t dbias,
-                              float grad_scale, ptr_t probs) {
+                              float grad_scale, ptr_t probs, ptr_t ws) {
   return [=](hipStream_t s) {
     softmax_xent(P<const float>(logits), ld, P<const int>(labels), N, classes, P<float>(loss_sum),
                  P<float>(correct), P<bf16>(dlogits), P<float>(dbias), grad_scale,
-                 P<float>(probs), s);
+                 P<float>(probs), P<float>(ws), s);
   };
 }
 
@@ -536,6 +536,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_tiles", &bn_bwd_tiles);
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);
+  m.def("softmax_xent_ws_floats", &softmax_xent_ws_floats);
   m.def("wgrad_pick_splits", [](std::vector<int> geom) {
     int pps = 0;
     const int sp = wgrad_pick_splits(geom_from(geom), &pps);

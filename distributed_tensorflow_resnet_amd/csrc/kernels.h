@@ -191,7 +191,8 @@ void bnrelu_avgpool(const bf16* x, const float* scale, const float* shift, bf16*
 void avgpool_bwd(const bf16* dpooled, bf16* dx, int N, int HW, int C, hipStream_t s);
 void softmax_xent(const float* logits, int ld, const int* labels, int N, int classes,
                   float* loss_sum, float* correct, bf16* dlogits, float* dbias,
-                  float grad_scale, float* probs, hipStream_t s);
+                  float grad_scale, float* probs, float* ws, hipStream_t s);
+long softmax_xent_ws_floats(int N, int ld);
 
 // ---- max pool (ImageNet stem) ----
 void maxpool_fwd(const bf16* x, bf16* y, uint8_t* argmax, int N, int H, int W, int C, int Ho,

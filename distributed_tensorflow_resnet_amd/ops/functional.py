@@ -249,9 +249,10 @@ def softmax_xent(logits, labels, classes, grad_scale, want_probs=False):
     db = torch.empty(classes, device=dev)
     probs = torch.zeros((N, ld), device=dev) if want_probs else None
     labels = labels.to(device=dev, dtype=torch.int32).contiguous()
+    ws = torch.empty(native().softmax_xent_ws_floats(N, ld), device=dev)
     native().softmax_xent(logits.data_ptr(), ld, labels.data_ptr(), N, classes, loss.data_ptr(),
                           corr.data_ptr(), dl.data_ptr(), db.data_ptr(), float(grad_scale),
-                          _ptr(probs), _stream())
+                          _ptr(probs), ws.data_ptr(), _stream())
     return loss, corr, dl, db, probs
 
 

@@ -137,7 +137,8 @@ class Engine:
 
     def __init__(self, spec: ModelSpec, batch_size: int, *, weight_decay: float,
                  lr_schedule: LRSchedule, optimizer: str = "mom", momentum: float = 0.9,
-                 device=None, dist_ctx=None, bucket_mb: float = 25.0, seed: int = 0,
+                 device=None, dist_ctx=None, bucket_mb: float = 25.0, reduce_mb: float = 4.0,
+                 seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
                  use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None):
         self.nat = native(required=True)
@@ -180,8 +181,19 @@ class Engine:
         self.ready_index: dict[str, int] = {}
         if self.dist is not None and self.world > 1:
             self.buckets = assign_buckets(self.params.train_slots, int(bucket_mb * 2 ** 20))
-        else:  # one group: a single grouped split-K reduce at the end of backward
+        else:  # one bucket: nothing to all-reduce, only the split-K reduces
             self.buckets = [(0, self.params.n_train, [s.name for s in self.params.train_slots])]
+        # Split-K reduce groups nest inside the buckets: each group's grouped reduce
+        # runs on the side stream as soon as its weight gradients are queued, so
+        # only the last group's reduce (stem + first stage) sits at the end of
+        # backward.  (One reduce of all of ResNet-50's slabs at the end was ~0.45 ms
+        # of tail; the group size trades that tail against launch count.)
+        reduce_mb = float(os.environ.get("DTR_REDUCE_MB", str(reduce_mb)))
+        slot_of = {s.name: s for s in self.params.train_slots}
+        self.reduce_groups = []
+        for lo, hi, names in self.buckets:
+            sub = assign_buckets([slot_of[n] for n in names], int(reduce_mb * 2 ** 20))
+            self.reduce_groups.append([g[2] for g in sub])
         self._build_train_plan()
         if self.dist is not None and self.world > 1:
             self.bucket_sched = schedule_buckets(self.buckets, self.ready_index)
@@ -354,6 +366,7 @@ class Engine:
         tot += sp * self.kpad * F
         self.wg_part = torch.empty(max(tot, 1), device=dev)
         self.l2_ws = torch.empty(self.nat.l2_workspace_floats(), device=dev)
+        self.xent_ws = torch.empty(self.nat.softmax_xent_ws_floats(N, self.kpad), device=dev)
 
     # ------------------------------------------------------------------ helpers
     def _geom(self, c: _Conv, N):
@@ -608,35 +621,48 @@ class Engine:
         self._side_q, self._side_blocks = [], 0
 
     def _flush_buckets(self, plan, force: bool = False):
-        """Emit one grouped split-K reduce for every bucket whose gradients are
-        all produced (or all remaining buckets if `force`); marks them ready."""
+        """Emit the grouped split-K reduce of every reduce group whose gradients are
+        all produced (all remaining ones if `force`); a bucket whose groups are all
+        reduced is joined to the main stream and marked ready for its all-reduce
+        (world > 1; with one process the only join is the final one)."""
         for bi, (lo, hi, names) in enumerate(self.buckets):
             if bi in self._flushed:
                 continue
-            if not force and not all(n in self._produced for n in names):
+            for gi, gnames in enumerate(self.reduce_groups[bi]):
+                if (bi, gi) in self._reduced:
+                    continue
+                if not force and not all(n in self._produced for n in gnames):
+                    continue
+                self._flush_side(plan, force=True)   # the group's wgrads precede its reduce
+                self._emit_reduce(plan, gnames)
+                self._reduced.add((bi, gi))
+            if not all((bi, gi) in self._reduced for gi in range(len(self.reduce_groups[bi]))):
                 continue
-            self._flush_side(plan, force=True)   # the bucket's wgrads precede its reduce
-            descs = [self._pending.pop(n) for n in names if n in self._pending]
-            if descs:
-                arr = np.zeros(len(descs), dtype=WGD_DTYPE)
-                chunk = 0
-                for i, (part, grad, sp, K, Kv, taps, C, Cv) in enumerate(descs):
-                    arr[i] = (part, grad, sp, K, Kv, taps, C, Cv, chunk)
-                    chunk += _ceil(K * taps * C, 256)   # WGR_COLS (conv_wgrad.hip)
-                t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
-                self._keep.append(t)
-                plan.use_stream(1 if self.fork_wgrad else 0)
-                plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
-                plan.use_stream(0)
-            if self.fork_wgrad:
-                # join: the main stream (and the bucket's all-reduce) waits for the side stream
-                ev = plan.new_event()
-                plan.use_stream(1)
-                plan.record(ev)
-                plan.use_stream(0)
-                plan.wait(ev)
-            self._mark(plan, *names)
-            self._flushed.add(bi)
+            if self.world > 1 or force:
+                if self.fork_wgrad:
+                    # join: the main stream (and the bucket's all-reduce) waits for the side stream
+                    ev = plan.new_event()
+                    plan.use_stream(1)
+                    plan.record(ev)
+                    plan.use_stream(0)
+                    plan.wait(ev)
+                self._mark(plan, *names)
+                self._flushed.add(bi)
+
+    def _emit_reduce(self, plan, names):
+        descs = [self._pending.pop(n) for n in names if n in self._pending]
+        if not descs:
+            return
+        arr = np.zeros(len(descs), dtype=WGD_DTYPE)
+        chunk = 0
+        for i, (part, grad, sp, K, Kv, taps, C, Cv) in enumerate(descs):
+            arr[i] = (part, grad, sp, K, Kv, taps, C, Cv, chunk)
+            chunk += _ceil(K * taps * C, 256)   # WGR_COLS (conv_wgrad.hip)
+        t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+        self._keep.append(t)
+        plan.use_stream(1 if self.fork_wgrad else 0)
+        plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
+        plan.use_stream(0)
 
     def _g(self, i, shape):
         """A fresh gradient buffer per backward tensor (the index is ignored):
@@ -718,15 +744,24 @@ class Engine:
         sp = self.scalars.data_ptr()
         plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
                           spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
-                          self.dense_bias_grad, 1.0 / self.global_batch, 0)
-        plan.l2_half_sum(self.params.master.data_ptr(), self.params.n_train,
-                         self.l2_ws.data_ptr(), sp + 12)
+                          self.dense_bias_grad, 1.0 / self.global_batch, 0,
+                          self.xent_ws.data_ptr())
         self.seg["fwd"] = (b0, plan.size())
 
         # ---- backward
         b1 = plan.size()
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
+        self._reduced = set()
         self._side_q, self._side_blocks = [], 0
+        # 1/2 sum v^2 of the (pre-update) weights for the reported `cost` only: it
+        # rides in the first side-stream batch, off the critical path (ImageNet:
+        # 25.5 M floats, ~80 us on the main stream).
+        l2 = lambda: plan.l2_half_sum(self.params.master.data_ptr(),  # noqa: E731
+                                      self.params.n_train, self.l2_ws.data_ptr(), sp + 12)
+        if self.fork_wgrad:
+            self._side_q.append(l2)
+        else:
+            l2()
         self._pending_bwd, self._bnb_src = None, None
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
@@ -967,6 +1002,7 @@ class _EvalPlan:
         self.x_in = torch.zeros((N, H, W, eng.cpad_in), dtype=BF16, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
         self.probs = torch.zeros((N, eng.kpad), device=dev)
+        self.xent_ws = torch.empty(eng.nat.softmax_xent_ws_floats(N, eng.kpad), device=dev)
         self.logits = torch.zeros((N, eng.kpad), device=dev)
         self.scalars = torch.zeros(4, device=dev)
         p = nat.Plan()
@@ -1021,7 +1057,8 @@ class _EvalPlan:
                     eng.dense_bias, spec.num_classes, 0, 0, eng._dense_geom(N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
         p.softmax_xent(self.logits.data_ptr(), eng.kpad, self.labels.data_ptr(), N,
-                       spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr())
+                       spec.num_classes, sp, sp + 4, 0, 0, 1.0, self.probs.data_ptr(),
+                       self.xent_ws.data_ptr())
         self._bufs = bufs
 
     def _conv(self, p, c, x, out, pre, residual=None):
