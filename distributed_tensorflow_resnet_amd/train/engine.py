@@ -489,7 +489,7 @@ class Engine:
             self.ready_index[n] = idx
 
     def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False,
-                  bnb: tuple | None = None):
+                  bnb: tuple | None = None, side: bool = True):
         """dgrad into dx (optional), then wgrad (+ reduce into the flat gradient).
 
         ``bnb=(bn, bn_input)``: the dgrad epilogue also emits that BN's backward
@@ -561,10 +561,12 @@ class Engine:
                 plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
                                 0 if pre is None else pre.scale.data_ptr(),
                                 0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
-        if self.fork_wgrad:
+        if self.fork_wgrad and side:
             self._side_q.append(emit)
         else:
             emit()
+            # a side-stream reduce of this slab must fork after it (_flush_side)
+            self._main_wgrad = self.fork_wgrad
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         self._produced.add(c.name)
 
@@ -606,11 +608,12 @@ class Engine:
     def _flush_side(self, plan, force: bool = False):
         """Fork: emit the queued weight gradients on the side stream behind ONE event
         (every `fork_every` residual blocks, or now if `force`)."""
-        if not self._side_q:
+        if not self._side_q and not (force and self._main_wgrad):
             return
         self._side_blocks += 1
         if not force and self._side_blocks < self.fork_every:
             return
+        self._main_wgrad = False   # the fork orders them before everything queued now
         ev = plan.new_event()
         plan.record(ev)
         plan.use_stream(1)
@@ -753,6 +756,7 @@ class Engine:
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
         self._reduced = set()
         self._side_q, self._side_blocks = [], 0
+        self._main_wgrad = self.fork_wgrad   # the dense wgrad below runs on the main stream
         # 1/2 sum v^2 of the (pre-update) weights for the reported `cost` only: it
         # rides in the first side-stream batch, off the critical path (ImageNet:
         # 25.5 M floats, ~80 us on the main stream).
@@ -811,7 +815,9 @@ class Engine:
             dx = self._g(o2, tuple(X.shape))
             self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
-            self._flush_side(plan)
+            # the last block's weight gradients go out now so they overlap the stem's
+            # backward (max-pool gather) instead of queueing behind it
+            self._flush_side(plan, force=i == 0)
             self._flush_buckets(plan)
         # stem (no dgrad: the input needs no gradient)
         self._emit_bn_bwd(plan)     # the stem's consumers (maxpool_bwd / wgrad) are not fusing
@@ -822,9 +828,12 @@ class Engine:
             pad = max((ph - 1) * 2 + 3 - st.ho, 0) // 2
             plan.maxpool_bwd(self.pool_arg.data_ptr(), dout.data_ptr(), dstem.data_ptr(),
                              [N, st.ho, st.wo, st.cout, ph, ph, st.cout, 3, 3, 2, pad], 3)
-            self._conv_bwd(plan, stem, dstem, self.x_in, N, None)
+            dstem_src = dstem
         else:
-            self._conv_bwd(plan, stem, dout, self.x_in, N, None)
+            dstem_src = dout
+        # The stem's weight gradient is the main stream's last op (nothing else is
+        # left for it), running alongside the side stream's last weight gradients.
+        self._conv_bwd(plan, stem, dstem_src, self.x_in, N, None, side=False)
         self._flush_side(plan, force=True)
         self._flush_buckets(plan, force=True)
         self.seg["bwd"] = (b1, plan.size())
