@@ -527,6 +527,8 @@ PYBIND11_MODULE(_C, m) {
         "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");
   m.def("set_conv_direct", &set_conv_direct,
         "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
+  m.def("set_conv_wide_tile", &set_conv_wide_tile,
+        "bit 0: forward, bit 1: dgrad -- 128x64 tiles for > 64 output columns (DTR_WIDE_128x64)");
   m.def("set_conv_pipeline", &set_conv_pipeline,
         "enable/disable the 2-deep pipelined implicit-GEMM loop for C % 64 == 0 "
         "(default: on unless DTR_CONV_PIPE=0)");

@@ -146,15 +146,19 @@ __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
 // XO ("x only"): prefetch just the BN-backward operands (BN input rows + the
 // per-column scale/shift/mean/rstd) -- the implicit-GEMM dgrad, whose occupancy
 // cannot afford the residual / accumulate registers too.
+// Multi-phase tiles (128x128) prefetch only in XO mode: the BN-input rows of every
+// phase (RIT * PHASES vectors).  Their occupancy is LDS-bound (2 workgroups per
+// CU), so the extra registers are free, while loading them per phase put a global
+// round trip into each phase of every tile (~0.1 ms per 56x56 dgrad).
 template <int BM, int BN, int WM, bool XO = false>
 struct EpiPre {
-  static constexpr bool ON = EpiLayout<BM, BN, WM>::PHASES == 1;
+  using EL = EpiLayout<BM, BN, WM>;
+  static constexpr bool ON = EL::PHASES == 1 || XO;
   static constexpr bool X_ONLY = XO;
-  static constexpr int RIT = ON ? (EpiLayout<BM, BN, WM>::PR + EpiLayout<BM, BN, WM>::RPP - 1) /
-                                      EpiLayout<BM, BN, WM>::RPP
-                                : 1;
-  static constexpr int RR = XO ? 1 : RIT;
-  bf16x8 res[RR], acc[RR], x[RIT];
+  static constexpr int RIT = ON ? (EL::PR + EL::RPP - 1) / EL::RPP : 1;   // per phase
+  static constexpr int NX = ON ? RIT * EL::PHASES : 1;
+  static constexpr int RR = (XO || EL::PHASES > 1) ? 1 : RIT;
+  bf16x8 res[RR], acc[RR], x[NX];
   f32x4 bsc[XO ? 2 : 1], bsh[XO ? 2 : 1], bmu[XO ? 2 : 1], brs[XO ? 2 : 1];
 };
 
@@ -162,25 +166,28 @@ template <int BM, int BN, int WM, int FLAGS, bool XO = false>
 __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0, const int n0,
                                              EpiPre<BM, BN, WM, XO>& P) {
   using EL = EpiLayout<BM, BN, WM>;
-  if constexpr (EpiPre<BM, BN, WM, XO>::ON) {
+  using PP = EpiPre<BM, BN, WM, XO>;
+  if constexpr (PP::ON) {
     const int tid = threadIdx.x;
     const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
     const int col0 = n0 + cc * 8;
     const bf16x8 zero8 = {};
 #pragma unroll
-    for (int it = 0; it < EpiPre<BM, BN, WM, XO>::RIT; ++it) {
-      const int row = m0 + r0 + it * EL::RPP;
-      const bool ok = col0 < args.Ncol && r0 + it * EL::RPP < EL::PR && row < args.M;
-      const long o = (long)row * args.Ncol + col0;
-      if constexpr (!XO) {
-        P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
-                                          : zero8;
-        P.acc[it] = (ok && args.accumulate && !args.out_f32)
-                        ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
+    for (int ph = 0; ph < EL::PHASES; ++ph)
+#pragma unroll
+      for (int it = 0; it < PP::RIT; ++it) {
+        const int row = m0 + ph * EL::PR + r0 + it * EL::RPP;
+        const bool ok = col0 < args.Ncol && r0 + it * EL::RPP < EL::PR && row < args.M;
+        const long o = (long)row * args.Ncol + col0;
+        if constexpr (!XO && EL::PHASES == 1) {
+          P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
+                                            : zero8;
+          P.acc[it] = (ok && args.accumulate && !args.out_f32)
+                          ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
+        }
+        if constexpr ((FLAGS & F_BNB) != 0)
+          P.x[ph * PP::RIT + it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
       }
-      if constexpr ((FLAGS & F_BNB) != 0)
-        P.x[it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
-    }
     if constexpr (XO && (FLAGS & F_BNB) != 0) {
       const bool colok = col0 < args.Ncol;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -269,10 +276,19 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // single-phase tiles cost more occupancy than it gained on the ImageNet shapes.)
     constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
     constexpr bool PREL = EpiPre<BM, BN, WM, XO>::ON;
-    constexpr bool PRER = PREL && !XO;   // residual / accumulate rows prefetched too
+    constexpr bool PRER = PREL && !XO;   // single-phase: residual / accumulate rows too
     constexpr bool BATCH = BNB;
     constexpr bool BATCHR = EL::PHASES > 1 && !BNB;   // (BNB: no residual; the registers spill)
     bf16x8 lx[BATCH ? RIT : 1], lr[BATCHR ? RIT : 1];
+    if (BATCH && PREL && pre) {   // this phase's prefetched BN-input rows (selects, no indexing)
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        lx[it] = pre->x[it];
+#pragma unroll
+        for (int q = 1; q < EL::PHASES; ++q)
+          if (ph == q) lx[it] = pre->x[q * RIT + it];
+      }
+    }
     if (BATCH && !(PREL && pre)) {
 #pragma unroll
       for (int it = 0; it < RIT; ++it) {
@@ -363,9 +379,8 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         for (int j = 0; j < 8; ++j) p1[j] += v[j];
       }
       if constexpr (BNB) {
-        const bf16x8 xv = (PREL && pre) ? pre->x[PREL ? it : 0]
-                          : BATCH ? lx[BATCH ? it : 0]
-                                  : *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+        const bf16x8 xv = BATCH ? lx[BATCH ? it : 0]
+                                : *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xv[j];

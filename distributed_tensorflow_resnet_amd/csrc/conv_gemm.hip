@@ -388,7 +388,9 @@ conv_gemm_kernel(GemmArgs args) {
   const int KT = (KD + BK - 1) / BK;
   // dgrad + BN-backward sums: the epilogue's BN-input rows and coefficients are
   // GEMM-independent -> issue their loads now, off the epilogue's critical path.
-  EpiPre<BM, BN, WM, true> epre;
+  // (prefetching the forward's residual rows the same way measured 1% slower)
+  using EP = EpiPre<BM, BN, WM, true>;
+  EP epre;
   if constexpr (FAST) {
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -459,7 +461,7 @@ conv_gemm_kernel(GemmArgs args) {
   }
   }
 
-  if constexpr (BNB && EpiPre<BM, BN, WM, true>::ON)
+  if constexpr (BNB && EP::ON)
     conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre);
   else
     conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
@@ -553,10 +555,26 @@ int conv_gemm_bn(int M, int nc) {
   return conv_gemm_bm(M, nc) == 128 ? 128 : 64;
 }
 
+// Wide-output tile experiment knob (>64 output columns): bit 0 = forward,
+// bit 1 = dgrad use 128x64 (4x1 waves, single-phase epilogue) instead of 128x128.
+static int g_wide_mask = -1;
+void set_conv_wide_tile(int mask) { g_wide_mask = mask; }
+static int wide_mask() {
+  if (g_wide_mask < 0) {
+    const char* e = std::getenv("DTR_WIDE_128x64");
+    g_wide_mask = e ? std::atoi(e) : 0;
+  }
+  return g_wide_mask;
+}
+
 template <int MODE>
 static void launch_mode(const GemmArgs& a, hipStream_t s) {
   const int nc = a.Ncol;
   const int bm = conv_gemm_bm(a.M, nc);
+  if (nc > 64 && bm == 128 && (wide_mask() & (MODE == MODE_FWD ? 1 : 2))) {
+    launch_flags<128, 64, 4, 1, MODE>(a, s);
+    return;
+  }
   if (nc <= 16) {
     if (bm == 256) launch_flags<256, 16, 4, 1, MODE>(a, s);
     else launch_flags<64, 16, 4, 1, MODE>(a, s);

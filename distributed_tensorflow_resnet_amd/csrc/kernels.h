@@ -122,6 +122,7 @@ void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
 void set_conv_direct(int enabled);
+void set_conv_wide_tile(int mask);     // 128x64 tiles for > 64 output columns (experiment)
 void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loops (DTR_CONV_PIPE)
 void set_wgrad_pipeline(int enabled);  // (the wgrad half of it)
 void set_fin_version(int v);   // BN finalize kernel variant (DTR_FIN_V)

@@ -45,6 +45,7 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = 10
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
+    knob = os.environ.get("AB_KNOB", "pipe")   # pipe: FAST loop off/on; wide: 128x128/128x64
     only = os.environ.get("AB_SHAPES")   # e.g. "56,256,64,1,1;28,128,128,3,1"
     shapes = [tuple(int(v) for v in t.split(",")) for t in only.split(";")] if only else SHAPES
     for H, C, K, k, s in shapes:
@@ -64,7 +65,12 @@ def main():
         sp, pps = nat.wgrad_pick_splits(gl)
         wpart = torch.empty(sp * k * k * C * K, device=dev)
         pf, pd, pw = nat.Plan(), nat.Plan(), nat.Plan()
+        pf0, pd0 = nat.Plan(), nat.Plan()   # AB_KNOB=fuse: no stats/residual/pre, no BNB
         for _ in range(n):
+            pf0.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0, gl,
+                          [], [], [], [], [], 0.997, 1e-5, 1)
+            pd0.conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
+                          gl, [], [], [], [], [], 0.997, 1e-5, 1)
             pw.conv_wgrad(res.data_ptr(), x.data_ptr(), sc.data_ptr(), sh.data_ptr(),
                           wpart.data_ptr(), gl, sp, pps)
             pf.conv_gemm(0, x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, res.data_ptr(),
@@ -77,10 +83,19 @@ def main():
         ts = {(p, v): [] for p, _ in passes for v in (0, 1)}
         for _ in range(rounds):
             for v in (0, 1):
-                nat.set_conv_pipeline(v)
+                if knob == "fuse":   # 0 = plain GEMM epilogue, 1 = the step's fusions
+                    for p, plan in (("fwd", pf if v else pf0), ("dgrad", pd if v else pd0),
+                                    ("wgrad", pw)):
+                        ts[(p, v)].append(dev_time(plan))
+                    continue
+                if knob == "wide":
+                    nat.set_conv_wide_tile(3 * v)
+                else:
+                    nat.set_conv_pipeline(v)
                 for p, plan in passes:
                     ts[(p, v)].append(dev_time(plan))
         nat.set_conv_pipeline(1)
+        nat.set_conv_wide_tile(0)
         line = []
         for p, _ in passes:
             a, b = statistics.median(ts[(p, 0)]), statistics.median(ts[(p, 1)])
