@@ -579,23 +579,23 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
 
 __global__ void bn_relu_apply_kernel(const bf16* __restrict__ x, const float* __restrict__ scale,
                                      const float* __restrict__ shift, bf16* __restrict__ y,
-                                     long nvec, int C) {
-  const int G = C / 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec;
-       i += (long)gridDim.x * blockDim.x) {
+                                     unsigned nvec, int C) {
+  const unsigned G = (unsigned)C / 8;   // 32-bit index math (host: nvec < 2^31)
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
     const int c0 = (int)(i % G) * 8;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
-    *reinterpret_cast<bf16x8*>(y + i * 8) = affine_relu8(v, scale + c0, shift + c0);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (size_t)i * 8);
+    *reinterpret_cast<bf16x8*>(y + (size_t)i * 8) = affine_relu8(v, scale + c0, shift + c0);
   }
 }
 
 void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M, int C,
                    hipStream_t s) {
   const long nvec = (long)M * C / 8;
+  if (nvec >= (1L << 31)) throw std::runtime_error("bn_relu_apply: tensor too large");
   long blocks = (nvec + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(bn_relu_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, scale,
-                     shift, y, nvec, C);
+                     shift, y, (unsigned)nvec, C);
   DTR_CHECK_LAUNCH();
 }
 

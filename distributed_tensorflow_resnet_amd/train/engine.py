@@ -319,14 +319,20 @@ class Engine:
         self.X.append(x0)
         max_act = x0.numel()
         sc_max = 0
+        self.Y1, self.Y2 = [], []   # materialized inner BN-ReLU outputs (_materialize_bn)
         for b in spec.blocks:
             f = b.convs[0].cout
             if b.kind == "building":
                 self.H1.append(torch.empty((N, b.ho, b.wo, f), dtype=BF16, device=dev))
                 self.H2.append(None)
+                self.Y1.append(None)
+                self.Y2.append(None)
             else:
                 self.H1.append(torch.empty((N, b.h, b.w, f), dtype=BF16, device=dev))
                 self.H2.append(torch.empty((N, b.ho, b.wo, f), dtype=BF16, device=dev))
+                for h, ys in ((self.H1[-1], self.Y1), (self.H2[-1], self.Y2)):
+                    ys.append(torch.empty_like(h) if self._materialize_bn(h.numel() // f, f)
+                              else None)
             self.X.append(torch.empty((N, b.ho, b.wo, b.cout), dtype=BF16, device=dev))
             if b.proj is not None:
                 sc_max = max(sc_max, N * b.ho * b.wo * b.cout)
@@ -464,6 +470,30 @@ class Engine:
                        0 if pre is None else pre.scale.data_ptr(),
                        0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [],
                        fin, [], pfin, [], BN_DECAY, BN_EPS, 1)
+
+    def _bn_input(self, plan, bn: _BN, x, y):
+        """Operand of the conv consuming BN(x): (y, None) after materializing
+        y = ReLU(BN(x)) when the plan gave the BN a buffer `y` (_alloc_activations),
+        else (x, bn) -- the conv applies BN+ReLU while staging (PRE)."""
+        if y is None:
+            self._bn_finalize(plan, bn)
+            return x, bn
+        self._bn_finalize(plan, bn, consumer_conv=False)
+        C = bn.spec.channels
+        plan.bn_relu_apply(x.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(), y.data_ptr(),
+                           x.numel() // C, C)
+        return y, None
+
+    def _materialize_bn(self, M: int, C: int) -> bool:
+        """Inner bottleneck BN: materialize ReLU(BN(x)) once instead of applying it in
+        the consumer conv's A staging (PRE), whose VALU work is repeated by every
+        output-column tile and, beside the MFMAs of the small 64x64 tiles of the 7x7
+        layers, cost more than the MFMAs (3x3 512->512: 66 -> 103 us).  Materializing
+        is one streaming pass: a win where the tensor is small and the consumers'
+        column tiles many (DTR_MAT_BN_ELEMS: M*C threshold, 0 = never; DTR_MAT_BN_MINC: min channels)."""
+        lim = int(os.environ.get("DTR_MAT_BN_ELEMS", "7000000"))
+        # measured (RN50 bs128): stages 3-4 (14x14 / 7x7) +1.3 %; adding stage 2 no gain
+        return C >= int(os.environ.get("DTR_MAT_BN_MINC", "256")) and M * C <= lim
 
     def _bn_finalize(self, plan, bn: _BN, train=True, consumer_conv: bool = True):
         """Called where the BN's statistics are next needed.  Deferred to the first
@@ -730,11 +760,10 @@ class Engine:
                                stats_for=nxt)
             else:
                 self._conv_fwd(plan, convs[0], X, self.H1[i], N, pre=bns[0], stats_for=bns[1])
-                self._bn_finalize(plan, bns[1])
-                self._conv_fwd(plan, convs[1], self.H1[i], self.H2[i], N, pre=bns[1],
-                               stats_for=bns[2])
-                self._bn_finalize(plan, bns[2])
-                self._conv_fwd(plan, convs[2], self.H2[i], Xn, N, pre=bns[2], residual=residual,
+                a1, p1 = self._bn_input(plan, bns[1], self.H1[i], self.Y1[i])
+                self._conv_fwd(plan, convs[1], a1, self.H2[i], N, pre=p1, stats_for=bns[2])
+                a2, p2 = self._bn_input(plan, bns[2], self.H2[i], self.Y2[i])
+                self._conv_fwd(plan, convs[2], a2, Xn, N, pre=p2, residual=residual,
                                stats_for=nxt)
         fbn = self.bns[spec.final_bn.name]
         self._bn_finalize(plan, fbn, consumer_conv=False)   # consumer: bnrelu_avgpool
@@ -796,12 +825,15 @@ class Engine:
                 dcur = dh
             else:
                 h1, h2 = self.H1[i], self.H2[i]
+                # wgrad inputs: the materialized BN-ReLU output, or the BN input + PRE
+                a1, p1 = (self.Y1[i], None) if self.Y1[i] is not None else (h1, bns[1])
+                a2, p2 = (self.Y2[i], None) if self.Y2[i] is not None else (h2, bns[2])
                 da = self._g(o1, tuple(h2.shape))
-                self._conv_bwd(plan, convs[2], dout, h2, N, bns[2], dx=da, bnb=(bns[2], h2))
+                self._conv_bwd(plan, convs[2], dout, a2, N, p2, dx=da, bnb=(bns[2], h2))
                 dh2 = self._g(o2, tuple(h2.shape))
                 self._bn_bwd(plan, bns[2], da, h2, dh2, reduced=True)
                 da = self._g(o1, tuple(h1.shape))
-                self._conv_bwd(plan, convs[1], dh2, h1, N, bns[1], dx=da, bnb=(bns[1], h1))
+                self._conv_bwd(plan, convs[1], dh2, a1, N, p1, dx=da, bnb=(bns[1], h1))
                 dh1 = self._g(o2, tuple(h1.shape))
                 self._bn_bwd(plan, bns[1], da, h1, dh1, reduced=True)
                 dcur = dh1
