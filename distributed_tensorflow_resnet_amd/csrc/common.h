@@ -99,6 +99,34 @@ __device__ __forceinline__ bf16x8 affine_relu8_reg(bf16x8 v, const f32x4& s0, co
   return r;
 }
 
+// The staging form used beside the MFMAs (FAST loops): scalar FMAs (a packed
+// v_pk_fma_f32 costs more than two v_fma_f32 in an MFMA gap, MI355X_MICROARCH
+// constants), the RNE pack first and the ReLU on the packed bf16 pair as a signed
+// 16-bit max against 0 (bf16 is sign-magnitude: every negative pattern, -0 too, is
+// a negative int16) -- one v_pk_max_i16 instead of two v_max_f32, bit-identical --
+// then `sel` (all-ones for a real pixel, 0 for padding; padding chunks were loaded
+// as zeros by the out-of-range buffer loads) as one AND per dword.
+__device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, const f32x4& s1,
+                                                   const f32x4& b0, const f32x4& b1,
+                                                   unsigned sel) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const u32x4 u = __builtin_bit_cast(u32x4, v);
+  const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+  const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  u32x4 r;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float lo = fmaf(__uint_as_float(u[p] << 16), sc[2 * p], sh[2 * p]);
+    const float hi = fmaf(__uint_as_float(u[p] & 0xffff0000u), sc[2 * p + 1], sh[2 * p + 1]);
+    const bf16x2 pk = {(bf16)lo, (bf16)hi};
+    const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pk), (s16x2){0, 0});
+    r[p] = __builtin_bit_cast(unsigned, m) & sel;
+  }
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 }  // namespace dtr
 
 #define DTR_CHECK_LAUNCH()                                                      \

@@ -139,6 +139,28 @@ __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
   lds_barrier();   // LDS-only: the caller's global stores stay in flight
 }
 
+// Two column sums (8 columns per thread each) behind ONE barrier.
+template <int CPR, int BN>
+__device__ __forceinline__ void colsum8x2(float (&v)[8], float (&w)[8], float* wred,
+                                          float* wred2) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1) {
+      v[j] += __shfl_xor(v[j], off, 64);
+      w[j] += __shfl_xor(w[j], off, 64);
+    }
+  if (lane < CPR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wred[wave * BN + lane * 8 + j] = v[j];
+      wred2[wave * BN + lane * 8 + j] = w[j];
+    }
+  }
+  lds_barrier();
+}
+
 // Epilogue operand prefetch (single-phase tiles): the residual / accumulate-into /
 // BN-input row vectors each epilogue thread will combine are independent of the
 // GEMM, so kernels issue their loads at kernel start (epi_prefetch) and the
@@ -328,9 +350,27 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // outstanding store of the wave (vmcnt(0)), so storing first put a full
     // store round trip in the middle of the epilogue (~2 us per STATS/BNB conv).
     bf16x8 ob[RIT];
-    float p1[8];
+    // STATS, one pass of shifted sums: d = y - K with K = the phase's row-0 value of
+    // the column (any per-column constant; close to the data, so sum d^2 - (sum d)^2/n
+    // does not cancel).  One reduction barrier per phase instead of the two-pass
+    // mean-then-M2 (two barriers and a second sweep).
+    float p1[8], p2[8], ksh[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) p1[j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      p1[j] = p2[j] = 0.f;
+      ksh[j] = 0.f;
+    }
+    if constexpr (STATS) {
+      if (colok) {
+        const f32x4 k0 = *reinterpret_cast<const f32x4*>(cs + cc * 8);
+        const f32x4 k1 = *reinterpret_cast<const f32x4*>(cs + cc * 8 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ksh[j] = k0[j];
+          ksh[4 + j] = k1[j];
+        }
+      }
+    }
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
       const int r = r0 + it * EL::RPP;
@@ -376,7 +416,11 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
       if constexpr (STATS) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p1[j] += v[j];
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[j] - ksh[j];
+          p1[j] += d;
+          p2[j] += d * d;
+        }
       }
       if constexpr (BNB) {
         const bf16x8 xv = BATCH ? lx[BATCH ? it : 0]
@@ -391,34 +435,13 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     if constexpr (STATS) {
-      // phase mean, then M2 about it (two-pass, from the registers)
-      colsum8<EL::CPR, BN>(p1, red);
+      colsum8x2<EL::CPR, BN>(p1, p2, red, red2);
       if (tid < BN) {
-        const float t = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
-        mean_s[tid] = t / (float)nph;
-      }
-      lds_barrier();
-      float q[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = 0.f;
-      if (colok) {
-        float mu[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) mu[j] = mean_s[cc * 8 + j];
-#pragma unroll
-        for (int it = 0; it < RIT; ++it) {
-          if (r0 + it * EL::RPP >= nph) continue;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = (float)ob[it][j] - mu[j];
-            q[j] += d * d;
-          }
-        }
-      }
-      colsum8<EL::CPR, BN>(q, red2);
-      if (tid < BN) {
-        const float m2 = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];
-        const float nb = (float)nph, mb = mean_s[tid];
+        const float sd = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+        const float sdd = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];
+        const float nb = (float)nph, dm = sd / nb;
+        const float mb = cs[tid] + dm;                 // K of column tid + mean of d
+        const float m2 = fmaxf(sdd - sd * dm, 0.f);
         const float n = wn_run + nb;
         const float d = mb - wmean_run;
         wmean_run += d * nb / n;

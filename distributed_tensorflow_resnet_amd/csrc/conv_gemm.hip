@@ -336,10 +336,8 @@ conv_gemm_kernel(GemmArgs args) {
         const int r = q >> 3;
         bf16x8 v = pa[p][i];
         if constexpr (PRE) {
-          const u32x4 w = __builtin_bit_cast(u32x4, affine_relu8_reg(v, s0, s1, b0, b1));
           const unsigned sel = 0u - ((pmask[p] >> i) & 1u);   // all-ones: real pixel
-          const u32x4 u = __builtin_bit_cast(u32x4, v);
-          v = __builtin_bit_cast(bf16x8, (w & sel) | (u & ~sel));
+          v = affine_relu8_sel(v, s0, s1, b0, b1, sel);
         }
         *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
       }

@@ -338,10 +338,8 @@ conv_wgrad_kernel(WgradArgs args) {
           const int col = (((cc >> 1) ^ unit_swz<UB>(row)) << 4) + ((cc & 1) << 3);
           bf16x8 v = pb[p][i];
           if constexpr (PRE) {
-            const u32x4 w = __builtin_bit_cast(u32x4, affine_relu8_reg(v, s0, s1, b0, b1));
-            const unsigned sel = 0u - ((pmask[p] >> i) & 1u);
-            const u32x4 u = __builtin_bit_cast(u32x4, v);
-            v = __builtin_bit_cast(bf16x8, (w & sel) | (u & ~sel));
+            const unsigned sel = 0u - ((pmask[p] >> i) & 1u);   // padding chunks loaded as 0
+            v = affine_relu8_sel(v, s0, s1, b0, b1, sel);
           }
           *reinterpret_cast<bf16x8*>(B + row * BN + col) = v;
         }
