@@ -80,6 +80,16 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     g.bnb_shift = P<const float>(bnb[4]);
     g.bnb_part = P<float>(bnb[5]);
   }
+  if (fin.size() == 1) {  // [acc]: STATS into the fp64 accumulator replicas (kernels.h)
+    if (stat_part == 0) throw std::invalid_argument("stat acc requires stat_part");
+    g.stat_acc = P<double>(fin[0]);
+    fin.clear();
+  }
+  if (bfin.size() == 1) {  // [acc]: BNB sums into the fp64 accumulator replicas
+    if (bnb.empty()) throw std::invalid_argument("bnb acc requires bnb");
+    g.bnb_acc = P<double>(bfin[0]);
+    bfin.clear();
+  }
   if (!fin.empty()) {  // [counters, gamma, beta, mmean, mvar, mean, rstd, scale, shift, gpart,
                        //  group, groups_only]
     if (fin.size() != 12) throw std::invalid_argument("fin needs 12 entries");
@@ -99,7 +109,10 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   if (!pfin.empty()) {  // [part, cnt, rows_per, M, gamma, beta, mean, rstd, scale, shift, mmean, mvar]
     if (pfin.size() != 12) throw std::invalid_argument("pfin needs 12 entries");
     if (pre_scale == 0) throw std::invalid_argument("pfin requires the PRE prologue");
-    g.pfin = BnPreFin{P<const float>(pfin[0]), (int)pfin[1], (int)pfin[2], (int)pfin[3],
+    // cnt == -1: part is a [BN_ACC_REP][2][C] fp64 accumulator (acc mode)
+    const bool acc = (int)pfin[1] == -1;
+    g.pfin = BnPreFin{acc ? nullptr : P<const float>(pfin[0]), acc ? 1 : (int)pfin[1],
+                      acc ? P<const double>(pfin[0]) : nullptr, (int)pfin[2], (int)pfin[3],
                       P<const float>(pfin[4]), P<const float>(pfin[5]), P<float>(pfin[6]),
                       P<float>(pfin[7]), P<float>(pfin[8]), P<float>(pfin[9]),
                       P<float>(pfin[10]), P<float>(pfin[11]), momentum, eps, update_moving};
@@ -108,9 +121,11 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                        //  dbeta, coef]
     if (abwd.size() != 13) throw std::invalid_argument("abwd needs 13 entries");
     if (mode != MODE_DGRAD) throw std::invalid_argument("abwd is dgrad-only");
+    const bool acc = (int)abwd[8] == -1;   // part is a fp64 accumulator (acc mode)
     g.abwd = BnBwdPre{P<const bf16>(abwd[0]), P<const bf16>(abwd[1]), P<const float>(abwd[2]),
                       P<const float>(abwd[3]), P<const float>(abwd[4]), P<const float>(abwd[5]),
-                      P<const float>(abwd[6]), P<const float>(abwd[7]), (int)abwd[8],
+                      P<const float>(abwd[6]), acc ? nullptr : P<const float>(abwd[7]),
+                      acc ? 1 : (int)abwd[8], acc ? P<const double>(abwd[7]) : nullptr,
                       P<bf16>(abwd[9]), P<float>(abwd[10]), P<float>(abwd[11]),
                       P<float>(abwd[12])};
   }
@@ -135,10 +150,10 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     if (!conv_direct_covers(g, mode))
       throw std::invalid_argument("abwd: this dgrad is not covered by the direct 3x3 kernel");
     const int C = c.K;   // A channels of the dgrad
-    if (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C))   // 0: coefficients precomputed
+    if (g.abwd.acc == nullptr && (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C)))   // 0: coef precomputed
       throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
   }
-  if (g.pfin.cnt > 0) {
+  if (g.pfin.cnt > 0 && g.pfin.acc == nullptr) {
     const int C = c.C;   // PRE is forward-only: the A channels
     if (g.pfin.cnt > pfin_cap(C))
       throw std::invalid_argument("pfin: C must be a power of two in [4, 128] and cnt <= "
@@ -193,6 +208,12 @@ static Launch mk_bn_finalize(ptr_t part, int tiles, int tile_rows, int M, int C,
                              ptr_t beta, ptr_t mmean, ptr_t mvar, float momentum, float eps,
                              int update_moving, ptr_t mean, ptr_t rstd, ptr_t scale,
                              ptr_t shift) {
+  if (tiles == -1)   // part is a [BN_ACC_REP][2][C] fp64 accumulator (acc mode)
+    return [=](hipStream_t s) {
+      bn_finalize_acc(P<const double>(part), M, C, P<const float>(gamma), P<const float>(beta),
+                      P<float>(mmean), P<float>(mvar), momentum, eps, update_moving,
+                      P<float>(mean), P<float>(rstd), P<float>(scale), P<float>(shift), s);
+    };
   return [=](hipStream_t s) {
     bn_finalize(P<const float>(part), tiles, tile_rows, M, C, P<const float>(gamma),
                 P<const float>(beta), P<float>(mmean), P<float>(mvar), momentum, eps,
@@ -226,6 +247,12 @@ static Launch mk_bn_bwd_reduce(ptr_t dy, ptr_t x, ptr_t mean, ptr_t rstd, ptr_t 
 
 static Launch mk_bn_bwd_finalize(ptr_t part, int tiles, int M, int C, ptr_t gamma, ptr_t rstd,
                                  ptr_t dgamma, ptr_t dbeta, ptr_t coef) {
+  if (tiles == -1)   // part is a [BN_ACC_REP][2][C] fp64 accumulator (acc mode)
+    return [=](hipStream_t s) {
+      bn_bwd_finalize_acc(P<const double>(part), M, C, P<const float>(gamma),
+                          P<const float>(rstd), P<float>(dgamma), P<float>(dbeta), P<float>(coef),
+                          s);
+    };
   return [=](hipStream_t s) {
     bn_bwd_finalize(P<const float>(part), tiles, M, C, P<const float>(gamma),
                     P<const float>(rstd), P<float>(dgamma), P<float>(dbeta), P<float>(coef), s);
@@ -534,6 +561,7 @@ PYBIND11_MODULE(_C, m) {
         "(default: on unless DTR_CONV_PIPE=0)");
   m.def("set_fin_version", &set_fin_version,
         "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
+  m.def("bn_acc_rep", []() { return BN_ACC_REP; }, "fp64 accumulator replicas per BatchNorm");
   m.def("pfin_cap", &pfin_cap, "max partials a consumer prologue combines for C channels");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);

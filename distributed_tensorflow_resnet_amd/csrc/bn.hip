@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "bn_fused.h"
 
 namespace dtr {
 
@@ -250,6 +251,69 @@ void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, s, stat_part, tiles, tile_rows,
                      M, C, gamma, beta, moving_mean, moving_var, momentum, eps, update_moving,
                      mean, rstd, scale, shift);
+  DTR_CHECK_LAUNCH();
+}
+
+// Accumulator mode (GemmArgs::stat_acc): the producer's workgroups added their
+// tile sums into BN_ACC_REP fp64 replicas; one thread per channel finalizes.
+__global__ void bn_finalize_acc_kernel(const double* __restrict__ acc, int M, int C,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float* moving_mean,
+                                       float* moving_var, float momentum, float eps,
+                                       int update_moving, float* mean_out, float* rstd_out,
+                                       float* scale_out, float* shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1, s2;
+  bn_acc_sums(acc, C, c, s1, s2);
+  const double dm = s1 / (double)M;
+  const double var = fmax(s2 / (double)M - dm * dm, 0.0);
+  const float mean = (float)dm, fvar = (float)var;
+  const float rstd = rsqrtf(fvar + eps);
+  const float sc = gamma[c] * rstd;
+  mean_out[c] = mean;
+  rstd_out[c] = rstd;
+  scale_out[c] = sc;
+  shift_out[c] = beta[c] - mean * sc;
+  if (update_moving) {
+    const float uvar = M > 1 ? (float)(var * M / (M - 1.0)) : fvar;
+    const float mm = moving_mean[c], mvv = moving_var[c];
+    moving_mean[c] = mm - (1.f - momentum) * (mm - mean);
+    moving_var[c] = mvv - (1.f - momentum) * (mvv - uvar);
+  }
+}
+
+void bn_finalize_acc(const double* acc, int M, int C, const float* gamma, const float* beta,
+                     float* moving_mean, float* moving_var, float momentum, float eps,
+                     int update_moving, float* mean, float* rstd, float* scale, float* shift,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_acc_kernel, dim3((C + 255) / 256), dim3(256), 0, s, acc, M, C,
+                     gamma, beta, moving_mean, moving_var, momentum, eps, update_moving, mean,
+                     rstd, scale, shift);
+  DTR_CHECK_LAUNCH();
+}
+
+__global__ void bn_bwd_finalize_acc_kernel(const double* __restrict__ acc, int M, int C,
+                                           const float* __restrict__ gamma,
+                                           const float* __restrict__ rstd, float* dgamma,
+                                           float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1, s2;
+  bn_acc_sums(acc, C, c, s1, s2);
+  const float sg = (float)s1, sgx = (float)s2;
+  const float a = gamma[c] * rstd[c];
+  dbeta[c] = sg;
+  dgamma[c] = sgx;
+  coef[c] = a;
+  coef[C + c] = a * sg / (float)M;
+  coef[2 * C + c] = a * sgx / (float)M;
+}
+
+void bn_bwd_finalize_acc(const double* acc, int M, int C, const float* gamma, const float* rstd,
+                         float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_acc_kernel, dim3((C + 255) / 256), dim3(256), 0, s, acc, M,
+                     C, gamma, rstd, dgamma, dbeta, coef);
   DTR_CHECK_LAUNCH();
 }
 

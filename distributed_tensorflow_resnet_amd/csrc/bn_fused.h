@@ -78,9 +78,65 @@ __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float
   n = nn;
 }
 
+// fp64 accumulator replicas [BN_ACC_REP][2][C] -> the channel's two sums, replicas
+// added in a fixed order (the per-replica atomic sums of fp32 tile partials are
+// exact in fp64 while the partials' magnitudes stay within ~2^20 of each other).
+__device__ __forceinline__ void bn_acc_sums(const double* __restrict__ acc, int C, int c,
+                                            double& s1, double& s2) {
+  double a[BN_ACC_REP], b[BN_ACC_REP];
+#pragma unroll
+  for (int r = 0; r < BN_ACC_REP; ++r) {
+    a[r] = acc[(long)r * 2 * C + c];
+    b[r] = acc[(long)r * 2 * C + C + c];
+  }
+  s1 = 0.0;
+  s2 = 0.0;
+#pragma unroll
+  for (int r = 0; r < BN_ACC_REP; ++r) {
+    s1 += a[r];
+    s2 += b[r];
+  }
+}
+
+// Adds one tile's per-column sums to its replica (memory-side fp64 atomics, no return).
+__device__ __forceinline__ void bn_acc_add(double* acc, int C, int col, double v1, double v2) {
+  double* p = acc + (long)(blockIdx.x % BN_ACC_REP) * 2 * C + col;
+  unsafeAtomicAdd(p, v1);
+  unsafeAtomicAdd(p + C, v2);
+}
+
 __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float* sc_s,
                                                 float* sh_s, float* scratch) {
   const int tid = threadIdx.x;
+  if (P.acc != nullptr) {   // accumulator mode: sum y, sum y^2 of all M rows (any C)
+    for (int c = tid; c < C; c += blockDim.x) {
+      const float gam = P.gamma[c], bet = P.beta[c];
+      double s1, s2;
+      bn_acc_sums(P.acc, C, c, s1, s2);
+      const double dm = s1 / (double)P.M;
+      const double var = fmax(s2 / (double)P.M - dm * dm, 0.0);
+      const float fmu = (float)dm, fvar = (float)var;
+      const float rs = rsqrtf(fvar + P.eps);
+      const float sc = gam * rs;
+      const float sh = bet - fmu * sc;
+      sc_s[c] = sc;
+      sh_s[c] = sh;
+      if (blockIdx.x == 0 && blockIdx.y == 0) {
+        P.mean[c] = fmu;
+        P.rstd[c] = rs;
+        P.scale[c] = sc;
+        P.shift[c] = sh;
+        if (P.update_moving) {
+          const float uvar = P.M > 1 ? (float)(var * P.M / (P.M - 1.0)) : fvar;
+          const float mmv = P.mmean[c], mvv = P.mvar[c];
+          P.mmean[c] = mmv - (1.f - P.momentum) * (mmv - fmu);
+          P.mvar[c] = mvv - (1.f - P.momentum) * (mvv - uvar);
+        }
+      }
+    }
+    __syncthreads();
+    return;
+  }
   const int CG = C >> 2, cg = tid & (CG - 1), q = tid / CG, G = 256 / CG;
   float gam = 0.f, bet = 0.f, mmv = 0.f, mvv = 0.f;   // issued ahead of the partials
   if (tid < C) {

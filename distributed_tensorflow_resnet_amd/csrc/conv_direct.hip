@@ -155,8 +155,17 @@ conv3x3_direct_kernel(GemmArgs args) {
       scl = Q.scale[c];
       shf = Q.shift[c];
     }
-    float sg, sgx;
-    bn_prefin_sums(Q.part, Q.cnt, CA, fin_scratch, sg, sgx);
+    float sg = 0.f, sgx = 0.f;
+    if (Q.acc != nullptr) {   // accumulator mode: the channel's two sums, no tile partials
+      if (c < CA) {
+        double s1, s2;
+        bn_acc_sums(Q.acc, CA, c, s1, s2);
+        sg = (float)s1;
+        sgx = (float)s2;
+      }
+    } else {
+      bn_prefin_sums(Q.part, Q.cnt, CA, fin_scratch, sg, sgx);
+    }
     if (c < CA) {
       const float a = ga * rs;
       const float M = (float)args.M;

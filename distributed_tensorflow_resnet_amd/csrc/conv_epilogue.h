@@ -475,7 +475,10 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   if constexpr (STATS) {
     if (tid < BN && n0 + tid < NC) {
       float* tile_out = args.stat_part + (long)blockIdx.x * 2 * NC;
-      if (args.fin.counters != nullptr) {   // handed to the last arriver: write-through (sc1)
+      if (args.stat_acc != nullptr) {       // accumulator mode: sum y, sum y^2 of the tile
+        const double n = wn_run, mu = wmean_run;
+        bn_acc_add(args.stat_acc, NC, n0 + tid, n * mu, (double)wm2_run + n * mu * mu);
+      } else if (args.fin.counters != nullptr) {   // handed to the last arriver: write-through (sc1)
         publish_f32(tile_out + n0 + tid, wmean_run);
         publish_f32(tile_out + NC + n0 + tid, wm2_run);
       } else {
@@ -538,7 +541,9 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     if (tid < BN && n0 + tid < NC) {
       const float t1 = bnb_t1, t2 = bnb_t2;
       float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
-      if (args.bfin.counters != nullptr) {
+      if (args.bnb_acc != nullptr) {        // accumulator mode
+        bn_acc_add(args.bnb_acc, NC, n0 + tid, (double)t1, (double)t2);
+      } else if (args.bfin.counters != nullptr) {
         publish_f32(tile_out + n0 + tid, t1);
         publish_f32(tile_out + NC + n0 + tid, t2);
       } else {

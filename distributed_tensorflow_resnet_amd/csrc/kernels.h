@@ -10,6 +10,8 @@ namespace dtr {
 
 typedef __bf16 bf16;
 
+constexpr int BN_ACC_REP = 8;   // fp64 accumulator replicas per BatchNorm (one per XCD)
+
 enum { MODE_FWD = 0, MODE_DGRAD = 1 };
 
 struct ConvGeom {
@@ -43,7 +45,8 @@ struct BnFwdFin {            // forward statistics -> mean/rstd/scale/shift + mo
 // so no separate finalize launch sits between producer and consumer.
 struct BnPreFin {
   const float* part;         // [cnt][2][C] (mean, M2); cnt == 0 -> disabled
-  int cnt;
+  int cnt;                   // acc mode: 1
+  const double* acc;         // optional [BN_ACC_REP][2][C] (sum y, sum y^2): replaces part
   int rows_per;              // rows per partial (the last one holds the remainder)
   int M;                     // rows in total
   const float* gamma;
@@ -83,7 +86,8 @@ struct BnBwdPre {
   const float* shift;
   const float* gamma;
   const float* part;         // [cnt][2][C] (sum g, sum g*xhat)
-  int cnt;
+  int cnt;                   // acc mode: 1
+  const double* acc;         // optional [BN_ACC_REP][2][C] (sum g, sum g*xhat): replaces part
   bf16* a_out;               // dh [M][C]
   float* dgamma;
   float* dbeta;
@@ -110,6 +114,13 @@ struct GemmArgs {
   float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
   BnFwdFin fin;             // with stat_part: finalize in-kernel
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
+  // Accumulator mode of STATS / BNB: instead of (or beside) the per-tile partials,
+  // every workgroup adds its tile's sums into [BN_ACC_REP][2][Ncol] fp64 replicas
+  // (replica = blockIdx.x % BN_ACC_REP, one per XCD) with memory-side atomics, so
+  // a consumer reads 2 x BN_ACC_REP values per channel instead of combining every
+  // tile partial.  The buffers are zeroed once per step.
+  double* stat_acc;         // STATS: sum y, sum y^2
+  double* bnb_acc;          // BNB: sum g, sum g*xhat
   BnPreFin pfin;            // with pre_scale: finalize the PRE BatchNorm in the prologue
   BnBwdPre abwd;            // direct dgrad: BN backward on the A operand (see above)
   int accumulate;           // out += result
@@ -164,6 +175,13 @@ void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,
                  const float* gamma, const float* beta, float* moving_mean,
                  float* moving_var, float momentum, float eps, int update_moving,
                  float* mean, float* rstd, float* scale, float* shift, hipStream_t s);
+// Accumulator-mode finalizers (acc = [BN_ACC_REP][2][C] fp64 sums, see GemmArgs).
+void bn_finalize_acc(const double* acc, int M, int C, const float* gamma, const float* beta,
+                     float* moving_mean, float* moving_var, float momentum, float eps,
+                     int update_moving, float* mean, float* rstd, float* scale, float* shift,
+                     hipStream_t s);
+void bn_bwd_finalize_acc(const double* acc, int M, int C, const float* gamma, const float* rstd,
+                         float* dgamma, float* dbeta, float* coef, hipStream_t s);
 void bn_scale_shift_eval(const float* gamma, const float* beta, const float* moving_mean,
                          const float* moving_var, float eps, int C, float* scale,
                          float* shift, hipStream_t s);

@@ -95,6 +95,11 @@ def constant_lr(lr: float) -> LRSchedule:
     return LRSchedule(lr, [], [lr])
 
 
+# partial count meaning "the pointer is a fp64 accumulator" in the pointer-vector
+# arguments of plan.conv_gemm (pfin / abwd; read back as int -1 by the bindings)
+_ACC_CNT = 0xFFFFFFFF
+
+
 def _ceil(a, b):
     return (a + b - 1) // b
 
@@ -119,6 +124,8 @@ class _BN:
     gpart: torch.Tensor = None    # level-1 group partials [groups][2][C]
     bpart: torch.Tensor = None    # backward partial sums [T][2][C] and their groups
     bgpart: torch.Tensor = None
+    acc: torch.Tensor = None      # accumulator mode: fp64 [REP][2][C] sum y, sum y^2
+    bacc: torch.Tensor = None     # ... and sum g, sum g*xhat (zeroed once per step)
 
 
 @dataclass
@@ -358,6 +365,24 @@ class Engine:
             tb = max(self.nat.bn_bwd_tiles(M, C), _ceil(M, self.nat.conv_gemm_bm(M, C)))
             b.bpart = torch.empty(tb * 2 * C, device=dev)
             b.bgpart = torch.empty(max(tb // 2, 1) * 2 * C, device=dev)
+        # Accumulator mode (DTR_BN_ACC, default on): the producing conv's workgroups add
+        # their tile sums into BN_ACC_REP fp64 replicas per BatchNorm with memory-side
+        # atomics, and the consumer reads 2 x REP values per channel instead of
+        # combining every tile partial in its prologue or a finalize launch (measured on
+        # the CIFAR direct convs: ~4 us per consumer prologue at 512 tiles).  All the
+        # replicas live in one buffer zeroed by one memset at the start of the step.
+        acc_mode = os.environ.get("DTR_BN_ACC", "1")   # 1 | 0 | fwd | bwd (diagnostics)
+        self.bn_acc_on = acc_mode in ("1", "fwd")
+        self.bn_bacc_on = acc_mode in ("1", "bwd")
+        rep = self.nat.bn_acc_rep()
+        tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
+        self.bn_acc = torch.zeros(max(tot, 1), dtype=torch.float64, device=dev)
+        off = 0
+        for b in self.bns.values():
+            n = 2 * rep * b.spec.channels
+            b.acc = self.bn_acc[off:off + n]
+            b.bacc = self.bn_acc[off + n:off + 2 * n]
+            off += 2 * n
         max_c = max(b.spec.channels for b in self.bns.values())
         self.coef = torch.empty(3 * max_c, device=dev)
         # per-conv split-K partial slabs (persist until the bucket's grouped reduce)
@@ -423,7 +448,11 @@ class Engine:
         stat_ptr = 0
         fin, pfin = [], []
         if pre is not None and pre.pending is not None:
-            part, cnt, rows, M0 = pre.pending
+            if pre.pending[0] == "acc":
+                _, part, M0 = pre.pending
+                cnt, rows = _ACC_CNT, 0
+            else:
+                part, cnt, rows, M0 = pre.pending
             pfin = [part, cnt, rows, M0, pre.gamma, pre.beta, pre.mean.data_ptr(),
                     pre.rstd.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
                     pre.mmean, pre.mvar]
@@ -439,7 +468,10 @@ class Engine:
             # measured (CIFAR bs 128 / 32): "3" (consumer prologue when the tiles are few,
             # else a separate finalize) beats adding producer-side last arrivers ("1")
             mode = os.environ.get("DTR_FUSED_BN_FINALIZE", "3")
-            if mode == "0":
+            if self.bn_acc_on:
+                fin = [b.acc.data_ptr()]
+                b.pending = ("acc", b.acc.data_ptr(), M)
+            elif mode == "0":
                 b.pending = ("separate", stat_ptr, T, bm, M)
             elif T <= capc:
                 pass                                    # (a)
@@ -501,7 +533,12 @@ class Engine:
         otherwise (or for a non-conv consumer) one bn_finalize launch (case (d))."""
         if bn.pending is None:
             return
-        if bn.pending[0] == "separate":
+        if bn.pending[0] == "acc":
+            if consumer_conv:
+                return
+            _, part, M = bn.pending
+            tiles, rows = -1, 0
+        elif bn.pending[0] == "separate":
             _, part, tiles, rows, M = bn.pending
         elif consumer_conv:
             return
@@ -537,7 +574,7 @@ class Engine:
                 bn = pb["bn"]
                 add = pb["add"]
                 part, cnt = pb["part"], pb["cnt"]
-                if cnt > self._consumer_cap(s.cout):
+                if cnt != -1 and cnt > self._consumer_cap(s.cout):
                     # too many partials for the prologue: finalize separately, the
                     # dgrad then reads the coefficients (cnt = 0)
                     plan.bn_bwd_finalize(part, cnt, pb["M"], bn.spec.channels, bn.gamma,
@@ -546,7 +583,8 @@ class Engine:
                     part, cnt = 0, 0
                 abw = [pb["x"].data_ptr(), 0 if add is None else add.data_ptr(),
                        bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
-                       bn.shift.data_ptr(), bn.gamma, part, cnt, dy.data_ptr(),
+                       bn.shift.data_ptr(), bn.gamma, part, _ACC_CNT if cnt == -1 else cnt,
+                       dy.data_ptr(),
                        bn.dgamma, bn.dbeta, self.coef.data_ptr()]
                 self._produced.update(bn.names)
                 self._pending_bwd = None
@@ -565,7 +603,10 @@ class Engine:
                       bn.shift.data_ptr(), bn.bpart.data_ptr()]
                 self._bnb_src = (bn.bpart.data_ptr(), T)
                 capc, capp = self._consumer_cap(C), (256 // bnt) * 8
-                if (T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
+                if self.bn_bacc_on:
+                    bfl = [bn.bacc.data_ptr()]
+                    self._bnb_src = (bn.bacc.data_ptr(), -1)
+                elif (T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
                         and os.environ.get("DTR_BWD_GROUPS", "0") == "1"):
                     gs = 2
                     while _ceil(T, gs) > capc:
@@ -714,6 +755,8 @@ class Engine:
             e.pending = None
         self._cnt_next = 0
         b0 = plan.size()
+        if self.bn_acc_on or self.bn_bacc_on:   # the step's BN accumulators start at zero
+            plan.memset(self.bn_acc.data_ptr(), self.bn_acc.numel() * 8)
         # ---- input
         if self.input_mode == "cifar_u8":
             plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,

@@ -168,3 +168,23 @@ def test_eval_plan_matches_autograd_eval(gpu):
         logits = model(imgs[:8], False)
     p_ref = torch.softmax(logits, 1)
     assert _rel(probs, p_ref) < 2e-2
+
+
+def test_bn_accumulator_mode_matches_partials(gpu, monkeypatch):
+    """DTR_BN_ACC=1 (fp64 atomic accumulators per BatchNorm) vs the per-tile partial
+    path: same loss, gradients and BN statistics up to rounding (shallow net; deep
+    nets are chaotic under bf16 and covered by the oracle tests above)."""
+    spec = cifar_spec(8)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DTR_BN_ACC", mode)
+        eng, _, _, _ = _make(spec, 64, gpu)
+        st = torch.cuda.current_stream().cuda_stream
+        eng._run("fwd", st)
+        eng._run("bwd", st)
+        torch.cuda.synchronize()
+        res[mode] = (eng.scalars[0].item(), eng.grad.clone(), eng.params.stats.clone())
+    (l0, g0, s0), (l1, g1, s1) = res["0"], res["1"]
+    assert abs(l1 - l0) <= 1e-4 * max(1.0, abs(l0))
+    assert _rel(g1, g0) < 1e-2
+    assert _rel(s1, s0) < 1e-5
