@@ -48,6 +48,8 @@ def main(argv=None) -> int:
                          "plan with weight gradients on a second stream (measured faster)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for compatibility)")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--allreduce-dtype", default="fp32", choices=("fp32", "bf16"),
+                    help="gradient all-reduce precision (bf16 halves the xGMI bytes)")
     args = ap.parse_args(argv)
 
     import torch
@@ -82,7 +84,8 @@ def main(argv=None) -> int:
     use_graph = bool(args.graph) and not args.no_graph
     eng = Engine(spec, per_rank, weight_decay=wd, lr_schedule=sched, device=device,
                  dist_ctx=ctx, global_batch=global_batch, bucket_mb=args.bucket_mb,
-                 seed=0, data_seed=1234 + ctx.rank, use_graph=use_graph)
+                 seed=0, data_seed=1234 + ctx.rank, use_graph=use_graph,
+                 allreduce_dtype=args.allreduce_dtype)
     eng.broadcast_parameters(0)
     eng.fill_synthetic(seed=ctx.rank)
 
@@ -129,6 +132,7 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{world}",
                 "graph": use_graph,
                 "wgrad_stream": eng.fork_wgrad,
+                "allreduce_dtype": args.allreduce_dtype,
             },
             "images_per_sec": round(sps * global_batch, 1),
             "final_loss": round(m["cross_entropy"], 4),

@@ -81,7 +81,8 @@ class CPUBackend:
 
     def __init__(self, spec: ModelSpec, batch_size: int, *, weight_decay: float, lr_schedule,
                  optimizer: str = "mom", momentum: float = 0.9, seed: int = 0, dist_ctx=None,
-                 global_batch: int | None = None, threads: int = 0):
+                 global_batch: int | None = None, threads: int = 0,
+                 allreduce_dtype: str = "fp32"):
         if threads:
             torch.set_num_threads(threads)
         self.spec = spec
@@ -104,6 +105,9 @@ class CPUBackend:
         self._last = {}
         self.profile_phases = False
         self.last_phase_ms = None
+        if allreduce_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"allreduce_dtype must be fp32 or bf16, got {allreduce_dtype!r}")
+        self.allreduce_bf16 = allreduce_dtype == "bf16"
 
     @property
     def global_step(self) -> int:
@@ -126,7 +130,12 @@ class CPUBackend:
         (xent * (self.N / self.global_batch)).backward()
         g = master.grad
         if self.dist is not None and self.world > 1:
-            self.dist.all_reduce_sum(g)
+            if self.allreduce_bf16:   # compressed exchange, fp32 accumulate of the result
+                gb = g.to(torch.bfloat16)
+                self.dist.all_reduce_sum(gb)
+                g = gb.float()
+            else:
+                self.dist.all_reduce_sum(g)
         lr = self.sched.at(self.step_count)
         with torch.no_grad():
             gp = g + self.wd * master
@@ -186,7 +195,8 @@ class CPUBackend:
 def make_backend(spec: ModelSpec, batch_size: int, *, device: str, weight_decay: float,
                  lr_schedule, optimizer: str = "mom", seed: int = 0, dist_ctx=None,
                  bucket_mb: float = 25.0, use_graph: bool = False, global_batch=None,
-                 input_mode: str = "auto", data_seed: int = 1234):
+                 input_mode: str = "auto", data_seed: int = 1234,
+                 allreduce_dtype: str = "fp32"):
     """device: gpu | cpu | auto."""
     if device == "auto":
         device = "gpu" if torch.cuda.is_available() else "cpu"
@@ -198,8 +208,9 @@ def make_backend(spec: ModelSpec, batch_size: int, *, device: str, weight_decay:
         eng = Engine(spec, batch_size, weight_decay=weight_decay, lr_schedule=lr_schedule,
                      optimizer=optimizer, device=torch.device("cuda", local), dist_ctx=dist_ctx,
                      bucket_mb=bucket_mb, seed=seed, input_mode=input_mode,
-                     global_batch=global_batch, use_graph=use_graph, data_seed=data_seed)
+                     global_batch=global_batch, use_graph=use_graph, data_seed=data_seed,
+                     allreduce_dtype=allreduce_dtype)
         return GPUBackend(eng, use_graph=use_graph)
     return CPUBackend(spec, batch_size, weight_decay=weight_decay, lr_schedule=lr_schedule,
                       optimizer=optimizer, seed=seed, dist_ctx=dist_ctx,
-                      global_batch=global_batch)
+                      global_batch=global_batch, allreduce_dtype=allreduce_dtype)

@@ -126,14 +126,14 @@ def main(argv=None, kind: str = "cifar") -> int:
         local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-    ctx = DistContext(device=dev)
+    ctx = DistContext(device=dev, timeout_s=flags.comm_timeout_secs)
     dp_ctx = None if flags.variable_update == "independent" else ctx
     rank, world = ctx.rank, ctx.world_size
     sched = cifar_lr_schedule() if spec.dataset.startswith("cifar") else imagenet_lr_schedule()
     backend = make_backend(spec, flags.batch_size, device=device, weight_decay=flags.weight_decay,
                            lr_schedule=sched, optimizer=flags.optimizer, seed=flags.seed,
                            dist_ctx=dp_ctx, bucket_mb=flags.bucket_mb, use_graph=flags.use_graph,
-                           data_seed=1234 + rank)
+                           data_seed=1234 + rank, allreduce_dtype=flags.allreduce_dtype)
     it = _train_batches(flags, spec, rank, world)
     feeder = None
     if it is None:
@@ -175,6 +175,8 @@ def main(argv=None, kind: str = "cifar") -> int:
                                                                  flags.fault_kill_rank))))
     if flags.profile_steps:
         hooks.append(H.ProfilerHook(flags.profile_steps))
+    if flags.step_watchdog_secs > 0:
+        hooks.append(H.StepWatchdogHook(flags.step_watchdog_secs))
     sess = TrainingSession(backend, hooks, chief_hooks, checkpoint_dir=flags.train_dir or None,
                            is_chief=is_chief, rank=rank, feeder=feeder)
     t0 = time.time()

@@ -150,6 +150,15 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_argument("--fault_kill_step", type=int, default=-1,
                    help="Fault injection: rank --fault_kill_rank exits at this step.")
     p.add_argument("--fault_kill_rank", type=int, default=0)
+    p.add_argument("--step_watchdog_secs", type=float, default=0.0,
+                   help="If > 0, abort (exit 3, for the launcher to restart from the latest "
+                        "checkpoint) when no step completes for this many seconds.")
+    p.add_argument("--comm_timeout_secs", type=float, default=600.0,
+                   help="Collective timeout of the process group (RCCL watchdog aborts the "
+                        "communicator after it).")
+    p.add_argument("--allreduce_dtype", default="fp32", choices=("fp32", "bf16"),
+                   help="Gradient all-reduce precision: bf16 halves the bytes on xGMI (fp32 "
+                        "master weights and optimizer are unchanged).")
     return p
 
 

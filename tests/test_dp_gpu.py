@@ -42,6 +42,14 @@ def test_dp_reduce_groups_nested_in_buckets(gpu):
 
 
 @pytest.mark.gpu
+def test_dp_bf16_gradient_allreduce(gpu):
+    # --allreduce_dtype bf16: buckets cast into a bf16 staging buffer, all-reduced, cast back
+    r = _torchrun(["scripts/dp_check.py"], 29714, extra_env={"DP_CHECK_ALLREDUCE": "bf16"})
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "DP_CHECK_OK" in r.stdout, r.stdout[-3000:]
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_contract(gpu):
     r = _torchrun(["bench.py", "--gpus", "2", "--steps", "5", "--warmup", "2"], 29712)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])

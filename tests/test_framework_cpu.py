@@ -308,3 +308,33 @@ def test_notebooks_are_valid():
         for c in nb["cells"]:
             if c["cell_type"] == "code":
                 ast.parse("".join(c["source"]))
+
+
+def test_gloo_data_parallel_bf16_allreduce(tmp_path):
+    """--allreduce_dtype bf16: 2 CPU ranks exchange bf16 gradients (half the bytes)
+    and still train in lockstep (identical checkpoints are written by rank 0)."""
+    td = str(tmp_path / "train")
+    r = run(["-m", "distributed_tensorflow_resnet_amd.parallel.launch", "--nproc", "2",
+             "--master_port", "29637", "resnet_cifar_main.py", "--device", "cpu",
+             "--resnet_size", "8", "--batch_size", "4", "--synthetic", "--train_steps", "3",
+             "--train_dir", td, "--save_checkpoint_steps", "3", "--variable_update", "horovod",
+             "--log_every", "1", "--allreduce_dtype", "bf16", "--step_watchdog_secs", "300"],
+            timeout=900)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-3")
+
+
+def test_step_watchdog_fires_on_hang_only():
+    from distributed_tensorflow_resnet_amd.train.hooks import StepWatchdogHook
+    import time as _t
+
+    exits = []
+    h = StepWatchdogHook(0.3, first_timeout_s=0.3, _exit=exits.append, poll_s=0.02)
+    h.begin(None)
+    for s in range(10):            # steps every 0.05 s: never idle for 0.3 s
+        _t.sleep(0.05)
+        h.after_run(None, s)
+    assert not h.fired and not exits
+    _t.sleep(0.6)                  # a hung step
+    assert h.fired and exits == [StepWatchdogHook.EXIT_CODE]
+    h.end(None)
