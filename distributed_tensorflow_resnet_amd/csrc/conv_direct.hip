@@ -213,7 +213,7 @@ conv3x3_direct_kernel(GemmArgs args) {
           }
           v = r;
           const int hr = pix / HW2;
-          if (hr >= 1 && hr <= R && hc >= 1 && hc <= WI)   // interior: this tile's dh rows
+          if (hr >= 1 && hr <= R && hc >= 1 && hc <= WI && blockIdx.y == 0)   // interior: this tile's dh rows
             *reinterpret_cast<bf16x8*>(args.abwd.a_out + ibase +
                                        ((long)(h0 + hr - 1) * WI + hc - 1) * CA + u * 8) = v;
         }
@@ -293,6 +293,20 @@ static void launch_direct_flags(const GemmArgs& a, hipStream_t s) {
 }
 
 static int g_direct_enabled = -1;   // -1: read DTR_DIRECT_CONV once
+static int g_direct_split = -2;     // -2: read DTR_DIRECT_SPLITN once (bit 0: C32, bit 1: C64)
+
+// Column-split mask for this launch.  Default (DTR_DIRECT_SPLITN unset): always for the
+// 8x8x64 layers, for 16x16x32 only while its grid has fewer workgroups than CUs
+// (measured, CIFAR RN50 step: bs128 1.444 -> 1.400 ms, bs32 1.135 -> 1.077, bs16
+// 1.074 -> 1.022; splitting 16x16x32 at bs128, 512 -> 1024 workgroups, cost 8 %).
+static int direct_split_mask(const GemmArgs& a, int bm) {
+  if (g_direct_split == -2) {
+    const char* e = std::getenv("DTR_DIRECT_SPLITN");
+    g_direct_split = e ? std::atoi(e) : -1;
+  }
+  if (g_direct_split >= 0) return g_direct_split;
+  return 2 | ((a.M / bm) < 256 ? 1 : 0);
+}
 
 void set_conv_direct(int enabled) { g_direct_enabled = enabled ? 1 : 0; }
 
@@ -326,11 +340,22 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
   const int ca = (mode == MODE_FWD) ? g.C : g.K;
   const int bm = conv_gemm_bm(a.M, a.Ncol);
   const bool fwd = mode == MODE_FWD;
-#define DTR_DIRECT(CA_, W_, BM_, WM_, WN_)                                              \
+  const int split = direct_split_mask(a, bm);
+#define DTR_DIRECT_BN(CA_, W_, BM_, BN_, WM_, WN_)                                      \
   if (ca == CA_ && g.W == W_ && bm == BM_) {                                          \
-    if (fwd) launch_direct_flags<CA_, W_, BM_, CA_, WM_, WN_, MODE_FWD>(a, s);        \
-    else launch_direct_flags<CA_, W_, BM_, CA_, WM_, WN_, MODE_DGRAD>(a, s);          \
+    if (fwd) launch_direct_flags<CA_, W_, BM_, BN_, WM_, WN_, MODE_FWD>(a, s);        \
+    else launch_direct_flags<CA_, W_, BM_, BN_, WM_, WN_, MODE_DGRAD>(a, s);          \
     return true;                                                                      \
+  }
+#define DTR_DIRECT(CA_, W_, BM_, WM_, WN_) DTR_DIRECT_BN(CA_, W_, BM_, CA_, WM_, WN_)
+  // two column tiles (half the weights and MFMAs per workgroup, twice the workgroups)
+  // for the layers whose grids are small: 8x8x64 (16 workgroups per image batch of 16)
+  // and, at small batch, 16x16x32
+  if (split & 2) {
+    DTR_DIRECT_BN(64, 8, 64, 32, 2, 2)
+  }
+  if (split & 1) {
+    DTR_DIRECT_BN(32, 16, 64, 16, 4, 1)
   }
   DTR_DIRECT(16, 32, 256, 4, 1)
   DTR_DIRECT(16, 32, 64, 4, 1)
@@ -338,6 +363,7 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
   DTR_DIRECT(32, 16, 64, 2, 2)
   DTR_DIRECT(64, 8, 64, 1, 4)
 #undef DTR_DIRECT
+#undef DTR_DIRECT_BN
   return false;
 }
 

@@ -62,12 +62,18 @@ def main():
         ppart = torch.rand(T * 2 * C, device=dev)   # the producer's partials (mean, M2)
         bpart = torch.empty(T * 2 * C, device=dev)
         p = {k: nat.Plan() for k in ("fwd", "pre", "pre+st", "pre+st+res", "pfin+st+res",
-                                     "dgrad", "bnb", "bnb+abwd")}
+                                     "ACC:pre+st+res", "ACC:pfin+st+res", "dgrad", "bnb",
+                                     "bnb+abwd", "ACC:bnb", "ACC:bnb+abwd")}
+        rep = nat.bn_acc_rep()
+        acc = torch.zeros(rep * 2 * max(C, K), dtype=torch.float64, device=dev)
+        pacc = torch.rand(rep * 2 * C, dtype=torch.float64, device=dev) + M
         V = [v.data_ptr() for v in vec]
         pfin = [ppart.data_ptr(), T, M // T, M, V[0], V[1], V[2], V[3], V[4], V[5], V[6], V[7]]
         abwd = [x.data_ptr(), res.data_ptr(), V[8], V[9], V[10], V[11], V[12], ppart.data_ptr(),
                 T, aout.data_ptr(), V[13], V[14], torch.empty(3 * C, device=dev).data_ptr()]
         bnb = [x.data_ptr(), V[2], V[3], V[4], V[5], bpart.data_ptr()]
+        pfin_acc = [pacc.data_ptr(), 0xFFFFFFFF] + pfin[2:]
+        abwd_acc = abwd[:7] + [pacc.data_ptr(), 0xFFFFFFFF] + abwd[9:]
         xs, ws, ys = x.data_ptr(), w.data_ptr(), y.data_ptr()
         sc, sh = V[4], V[5]
         for _ in range(n):
@@ -82,6 +88,17 @@ def main():
             p["pfin+st+res"].conv_gemm(0, xs, ws, ys, 0, res.data_ptr(), sc, sh, 0, 0,
                                        part.data_ptr(), 0, gl, [], [], [], pfin, [], 0.997, 1e-5,
                                        1)
+            p["ACC:pre+st+res"].conv_gemm(0, xs, ws, ys, 0, res.data_ptr(), sc, sh, 0, 0,
+                                          part.data_ptr(), 0, gl, [], [acc.data_ptr()], [], [],
+                                          [], 0.997, 1e-5, 1)
+            p["ACC:pfin+st+res"].conv_gemm(0, xs, ws, ys, 0, res.data_ptr(), sc, sh, 0, 0,
+                                           part.data_ptr(), 0, gl, [], [acc.data_ptr()], [],
+                                           pfin_acc, [], 0.997, 1e-5, 1)
+            p["ACC:bnb"].conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0,
+                                   0, 0, 0, gl, bnb, [], [acc.data_ptr()], [], [], 0.997, 1e-5, 1)
+            p["ACC:bnb+abwd"].conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0,
+                                        0, 0, 0, 0, 0, gl, bnb, [], [acc.data_ptr()], [],
+                                        abwd_acc, 0.997, 1e-5, 1)
             p["dgrad"].conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0,
                                  0, 0, 0, gl, [], [], [], [], [], 0.997, 1e-5, 1)
             p["bnb"].conv_gemm(1, res.data_ptr(), wh.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, 0,
