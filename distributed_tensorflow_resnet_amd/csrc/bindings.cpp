@@ -373,10 +373,13 @@ static Launch mk_memset(ptr_t p, long bytes) {
 }
 
 static Launch mk_cifar_augment(ptr_t img, ptr_t out, int N, int H, int W, int Cpad, int pad,
-                               unsigned long long seed, ptr_t gstep, int train, ptr_t crop_log) {
+                               unsigned long long seed, ptr_t gstep, int train, ptr_t crop_log,
+                               ptr_t zero, long zero_bytes) {
+  if (zero_bytes % 16) throw std::invalid_argument("cifar_augment: zero_bytes % 16 != 0");
   return [=](hipStream_t s) {
     cifar_augment(P<const uint8_t>(img), P<bf16>(out), N, H, W, Cpad, pad, seed,
-                  P<const long long>(gstep), train, P<int>(crop_log), s);
+                  P<const long long>(gstep), train, P<int>(crop_log), P<void>(zero), zero_bytes,
+                  s);
   };
 }
 

@@ -9,6 +9,8 @@
 // channels so every 16-B fragment is one tap).  Crop/flip randomness comes from
 // a counter-based hash of (seed, global_step, image) read on the device, so the
 // augmentation is part of the captured hipGraph and replays with fresh crops.
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 #include "data.h"
@@ -22,12 +24,90 @@ __device__ __forceinline__ unsigned long long splitmix(unsigned long long x) {
   return x ^ (x >> 31);
 }
 
+// One workgroup per image: the 3 KB record is staged in LDS with 16-B loads, every
+// thread keeps its 4 output pixels' 3 channels in registers across the
+// per-image statistics, and writes each pixel as ONE 16-B NHWC row (3 channels +
+// zero padding).  Optionally zeroes a buffer in the same launch (the step's
+// BatchNorm accumulators), so the step needs no separate memset.
+template <int CPAD>
 __global__ void __launch_bounds__(256)
-cifar_augment_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int H, int W,
-                     int Cpad, int pad, unsigned long long seed, const long long* gstep,
-                     int train, int* crop_log) {
+cifar_augment_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int pad,
+                     unsigned long long seed, const long long* gstep, int train, int* crop_log,
+                     uint4* __restrict__ zero, long zero_vec) {
+  constexpr int H = 32, W = 32, HW = H * W, CHW = 3 * HW, PPT = HW / 256;
+  __shared__ __attribute__((aligned(16))) uint8_t im[CHW];
   __shared__ float red[8];
   const int n = blockIdx.x, tid = threadIdx.x;
+  for (long i = blockIdx.x * 256L + tid; i < zero_vec; i += (long)gridDim.x * 256)
+    zero[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < CHW / 16)
+    reinterpret_cast<uint4*>(im)[tid] = reinterpret_cast<const uint4*>(img + (long)n * CHW)[tid];
+  int oy = pad, ox = pad, flip = 0;
+  if (train) {
+    const unsigned long long step = gstep ? (unsigned long long)*gstep : 0ull;
+    const unsigned long long h = splitmix(seed ^ splitmix(step * 0x100000001B3ull + n));
+    oy = (int)(h % (2 * pad + 1));
+    ox = (int)((h >> 16) % (2 * pad + 1));
+    flip = (int)((h >> 32) & 1);
+  }
+  if (crop_log && tid == 0) {
+    crop_log[n * 3 + 0] = oy;
+    crop_log[n * 3 + 1] = ox;
+    crop_log[n * 3 + 2] = flip;
+  }
+  __syncthreads();
+  // pixel (y,x) of the crop = padded-image pixel (y+oy, x'+ox), x' = flip ? W-1-x : x
+  float v[PPT][3];
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int p = tid + k * 256;
+    const int y = p / W, x = p - y * W;
+    const int xs = flip ? (W - 1 - x) : x;
+    const int py = y + oy - pad, px = xs + ox - pad;
+    const bool in = py >= 0 && py < H && px >= 0 && px < W;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v[k][c] = in ? (float)im[c * HW + py * W + px] : 0.f;
+      s += v[k][c];
+      q += v[k][c] * v[k][c];
+    }
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = s;
+    red[4 + (tid >> 6)] = q;
+  }
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float totq = red[4] + red[5] + red[6] + red[7];
+  const float nel = (float)CHW;
+  const float mean = tot / nel;
+  const float var = fmaxf(totq / nel - mean * mean, 0.f);
+  const float adj = fmaxf(sqrtf(var), rsqrtf(nel));
+  const float inv = 1.f / adj;
+  bf16* o = out + (long)n * HW * CPAD;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int p = tid + k * 256;
+    bf16x8 r = {};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) r[c] = (bf16)((v[k][c] - mean) * inv);
+    *reinterpret_cast<bf16x8*>(o + (long)p * CPAD) = r;
+  }
+}
+
+// Generic-shape fallback (any H, W, Cpad): one element per thread iteration.
+__global__ void __launch_bounds__(256)
+cifar_augment_generic_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int H,
+                             int W, int Cpad, int pad, unsigned long long seed,
+                             const long long* gstep, int train, int* crop_log,
+                             uint4* __restrict__ zero, long zero_vec) {
+  __shared__ float red[8];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  for (long i = blockIdx.x * 256L + tid; i < zero_vec; i += (long)gridDim.x * 256)
+    zero[i] = make_uint4(0u, 0u, 0u, 0u);
   const int HW = H * W, CHW = 3 * HW;
   const uint8_t* src = img + (long)n * CHW;
   int oy = pad, ox = pad, flip = 0;
@@ -43,7 +123,6 @@ cifar_augment_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, in
     crop_log[n * 3 + 1] = ox;
     crop_log[n * 3 + 2] = flip;
   }
-  // pixel (y,x) of the crop = padded-image pixel (y+oy, x'+ox), x' = flip ? W-1-x : x
   auto val = [&](int p, int c) -> float {
     const int y = p / W, x = p - y * W;
     const int xs = flip ? (W - 1 - x) : x;
@@ -80,9 +159,16 @@ cifar_augment_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, in
 
 void cifar_augment(const uint8_t* img, bf16* out, int N, int H, int W, int Cpad, int pad,
                    unsigned long long seed, const long long* gstep, int train, int* crop_log,
-                   hipStream_t s) {
-  hipLaunchKernelGGL(cifar_augment_kernel, dim3(N), dim3(256), 0, s, img, out, H, W, Cpad, pad,
-                     seed, gstep, train, crop_log);
+                   void* zero, long zero_bytes, hipStream_t s) {
+  if (zero_bytes % 16) throw std::invalid_argument("cifar_augment: zero_bytes % 16 != 0");
+  uint4* z = reinterpret_cast<uint4*>(zero);
+  const long zv = zero ? zero_bytes / 16 : 0;
+  if (H == 32 && W == 32 && Cpad == 8)
+    hipLaunchKernelGGL(cifar_augment_kernel<8>, dim3(N), dim3(256), 0, s, img, out, pad, seed,
+                       gstep, train, crop_log, z, zv);
+  else
+    hipLaunchKernelGGL(cifar_augment_generic_kernel, dim3(N), dim3(256), 0, s, img, out, H, W,
+                       Cpad, pad, seed, gstep, train, crop_log, z, zv);
   DTR_CHECK_LAUNCH();
 }
 

@@ -288,5 +288,5 @@ def cifar_augment(img_u8, cpad=8, pad=4, seed=0, gstep=None, train=True, log_cro
     out = torch.empty((N, H, W, cpad), device=img_u8.device, dtype=BF16)
     log = torch.zeros((N, 3), device=img_u8.device, dtype=torch.int32) if log_crops else None
     native().cifar_augment(img_u8.data_ptr(), out.data_ptr(), N, H, W, cpad, pad, seed,
-                           _ptr(gstep), int(train), _ptr(log), _stream())
+                           _ptr(gstep), int(train), _ptr(log), 0, 0, _stream())
     return (out, log) if log_crops else out

@@ -389,7 +389,7 @@ class Engine:
         self.bn_bacc_on = acc_mode in ("1", "bwd")
         rep = self.nat.bn_acc_rep()
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
-        self.bn_acc = torch.zeros(max(tot, 1), dtype=torch.float64, device=dev)
+        self.bn_acc = torch.zeros(max(_ceil(tot, 2) * 2, 2), dtype=torch.float64, device=dev)
         off = 0
         for b in self.bns.values():
             n = 2 * rep * b.spec.channels
@@ -768,13 +768,17 @@ class Engine:
             e.pending = None
         self._cnt_next = 0
         b0 = plan.size()
-        if self.bn_acc_on or self.bn_bacc_on:   # the step's BN accumulators start at zero
-            plan.memset(self.bn_acc.data_ptr(), self.bn_acc.numel() * 8)
+        # the step's BN accumulators start at zero: cleared by the CIFAR augmentation
+        # kernel (no extra launch), else by a memset
+        zero = (self.bn_acc.data_ptr(), self.bn_acc.numel() * 8) \
+            if (self.bn_acc_on or self.bn_bacc_on) else (0, 0)
+        if zero[0] and self.input_mode != "cifar_u8":
+            plan.memset(*zero)
         # ---- input
         if self.input_mode == "cifar_u8":
             plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
                                spec.image_w, self.cpad_in, 4, self.data_seed,
-                               self.gstep.data_ptr(), 1, 0)
+                               self.gstep.data_ptr(), 1, 0, *zero)
         # ---- forward
         stem = self.convs[spec.stem.name]
         blocks = spec.blocks
@@ -1113,7 +1117,7 @@ class _EvalPlan:
         self.plan = p
         self.input_plan = nat.Plan()
         self.input_plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, H, W,
-                                      eng.cpad_in, 4, 0, 0, 0, 0)
+                                      eng.cpad_in, 4, 0, 0, 0, 0, 0, 0)
         st = spec.stem
         stem = eng.convs[st.name]
         bufs = []
