@@ -21,6 +21,7 @@
 //   4. the WK slice results are summed in LDS in fixed order and the workgroup's
 //      [K][TJ*C] block is written into its split's fp32 partial slab -- the same
 //      [split][K][9C] layout the grouped deterministic reduce already consumes.
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -204,12 +205,25 @@ int wgrad_direct_bmp(const ConvGeom& g) {
   if (g.kh != 3 || g.kw != 3 || g.stride != 1 || g.pad != 1 || g.C != g.K || g.H != g.W ||
       g.Ho != g.H || g.Wo != g.W)
     return 0;
+  // pixels per split (= per workgroup): larger -> fewer split-K slabs for the grouped
+  // reduce to read, fewer workgroups.  DTR_WGD_BMP="c16,c32,c64" overrides (sweeps).
+  static int bm16 = -1, bm32 = -1, bm64 = -1;
+  if (bm16 < 0) {
+    // measured (CIFAR RN50 step, bs128): 256/256/128 -> 512/512/256 = 1.396 -> 1.320 ms
+    // (the grouped reduce reads half the slabs; the side stream has the slack)
+    bm16 = 512, bm32 = 512, bm64 = 256;
+    if (const char* e = std::getenv("DTR_WGD_BMP")) std::sscanf(e, "%d,%d,%d", &bm16, &bm32, &bm64);
+  }
   int bmp = 0;
-  if (g.C == 16 && g.W == 32) bmp = 256;
-  else if (g.C == 32 && g.W == 16) bmp = 256;
-  else if (g.C == 64 && g.W == 8) bmp = 128;
+  if (g.C == 16 && g.W == 32) bmp = bm16;
+  else if (g.C == 32 && g.W == 16) bmp = bm32;
+  else if (g.C == 64 && g.W == 8) bmp = bm64;
   const long P = (long)g.N * g.H * g.W;
-  if (bmp == 0 || P % bmp != 0) return 0;
+  const int lo = g.C == 64 ? 128 : 256;          // smallest instantiated tile
+  const int hi = g.C == 16 ? 1024 : g.C == 32 ? 512 : 256;
+  if (bmp < lo || bmp > hi || (bmp & (bmp - 1))) return 0;
+  while (bmp > lo && P % bmp != 0) bmp >>= 1;     // the largest tile that divides P
+  if (P % bmp != 0) return 0;
   return bmp;
 }
 
@@ -217,9 +231,17 @@ bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) {
   const int bmp = wgrad_direct_bmp(a.g);
   if (bmp == 0 || a.px_per_split != bmp) return false;
   const ConvGeom& g = a.g;
-  if (g.C == 16) wgd_launch<16, 32, 32, 256, 9>(a, s);
-  else if (g.C == 32) wgd_launch<32, 16, 16, 256, 3>(a, s);
-  else wgd_launch<64, 8, 8, 128, 3>(a, s);
+  if (g.C == 16) {
+    if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s);
+    else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s);
+    else wgd_launch<16, 32, 32, 256, 9>(a, s);
+  } else if (g.C == 32) {
+    if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s);
+    else wgd_launch<32, 16, 16, 256, 3>(a, s);
+  } else {
+    if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s);
+    else wgd_launch<64, 8, 8, 128, 3>(a, s);
+  }
   return true;
 }
 
