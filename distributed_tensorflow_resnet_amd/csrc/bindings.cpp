@@ -332,10 +332,10 @@ static LrSchedule make_sched(float init, long long warm_steps, float warm_from, 
 }
 
 static Launch mk_ohwi_pack(ptr_t master, ptr_t segs, ptr_t tile0, int nseg, long long tiles,
-                           ptr_t bf) {
+                           ptr_t bf, ptr_t gstep_inc) {
   return [=](hipStream_t s) {
     ohwi_pack(P<const float>(master), P<const ParamSeg>(segs), P<const long long>(tile0), nseg,
-              tiles, P<bf16>(bf), s);
+              tiles, P<bf16>(bf), P<long long>(gstep_inc), s);
   };
 }
 

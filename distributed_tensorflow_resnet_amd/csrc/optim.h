@@ -18,9 +18,10 @@ void sgd_update_pack(float* master, const float* grad, float* mom, long n, const
                      const long long* gstep, float momentum, float wd, float grad_scale,
                      int use_momentum, const ParamSeg* segs, int nseg, bf16* bf, float* lr_out,
                      int update, hipStream_t st);
-// OHWI bf16 weight copies by a tiled transpose of the fp32 master (after the update).
+// OHWI bf16 weight copies by a tiled transpose of the fp32 master (after the update);
+// gstep_inc (optional): global_step += 1 in the same launch.
 void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0, int nseg,
-               long long total_tiles, bf16* bf, hipStream_t s);
+               long long total_tiles, bf16* bf, long long* gstep_inc, hipStream_t s);
 void step_increment(long long* gstep, hipStream_t s);
 int l2_workspace_floats();
 void l2_half_sum(const float* v, long n, float* ws, float* out, hipStream_t s);

@@ -137,9 +137,12 @@ void sgd_update_pack(float* master, const float* grad, float* mom, long n, const
 // ceil(taps*C/64) x ceil(K/64) tiles; segments without an OHWI copy have 0 tiles).
 __global__ void __launch_bounds__(256)
 ohwi_pack_kernel(const float* __restrict__ w, const ParamSeg* __restrict__ segs,
-                 const long long* __restrict__ tile0, int nseg, bf16* __restrict__ bf) {
+                 const long long* __restrict__ tile0, int nseg, bf16* __restrict__ bf,
+                 long long* gstep_inc) {
   __shared__ bf16 tile[64][66];
   const long long b = blockIdx.x;
+  // the step's global_step += 1 rides here (this kernel never reads it): one launch less
+  if (gstep_inc != nullptr && b == 0 && threadIdx.x == 0) *gstep_inc += 1;
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -169,10 +172,13 @@ ohwi_pack_kernel(const float* __restrict__ w, const ParamSeg* __restrict__ segs,
 }
 
 void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0, int nseg,
-               long long total_tiles, bf16* bf, hipStream_t s) {
-  if (total_tiles <= 0) return;
+               long long total_tiles, bf16* bf, long long* gstep_inc, hipStream_t s) {
+  if (total_tiles <= 0) {
+    if (gstep_inc) step_increment(gstep_inc, s);
+    return;
+  }
   hipLaunchKernelGGL(ohwi_pack_kernel, dim3((unsigned)total_tiles), dim3(256), 0, s, master,
-                     segs, tile0, nseg, bf);
+                     segs, tile0, nseg, bf, gstep_inc);
   DTR_CHECK_LAUNCH();
 }
 

@@ -940,8 +940,8 @@ class Engine:
                              int(self.use_momentum), self.segs.data_ptr(), self.nseg,
                              self.wbf.data_ptr(), sp + 8, 1)
         plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
-                       self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr())
-        plan.step_increment(self.gstep.data_ptr())
+                       self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr(),
+                       self.gstep.data_ptr())   # + global_step += 1
         self.seg["opt"] = (b2, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
         assert not missing, f"gradients never produced: {missing[:4]}"
@@ -956,7 +956,7 @@ class Engine:
                                  self.wbf.data_ptr(), 0, 0, torch.cuda.current_stream().cuda_stream)
         self.nat.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
                            self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
-                           self.wbf.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                           self.wbf.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
 
     def _run(self, name, stream):
         a, b = self.seg[name]
