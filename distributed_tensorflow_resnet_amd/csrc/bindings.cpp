@@ -298,6 +298,55 @@ static Launch mk_softmax_xent(ptr_t logits, int ld, ptr_t labels, int N, int cla
   };
 }
 
+static Launch mk_softmax_xent_reduce(ptr_t ws, int ld, int N, int classes, ptr_t loss_sum,
+                                     ptr_t correct, ptr_t dbias) {
+  return [=](hipStream_t s) {
+    softmax_xent_reduce(P<const float>(ws), ld, N, classes, P<float>(loss_sum), P<float>(correct),
+                        P<float>(dbias), s);
+  };
+}
+
+// head_fused(x, bn=[acc, gamma, beta, mmean, mvar, mean, rstd, scale, shift], momentum, eps,
+//            update_moving, w_hwio, bias, labels, shape=[N, HW, C, classes, kpad], grad_scale,
+//            out=[pooled, dlogits, ws, dact, bacc])
+static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, float eps,
+                            int update_moving, ptr_t w, ptr_t bias, ptr_t labels,
+                            std::vector<int> shape, float grad_scale, std::vector<ptr_t> out) {
+  if (bn.size() != 9 || shape.size() != 5 || out.size() != 5)
+    throw std::invalid_argument("head_fused: bn needs 9 pointers, shape 5 ints, out 5 pointers");
+  HeadArgs a{};
+  a.x = P<const bf16>(x);
+  a.acc = P<const double>(bn[0]);
+  a.gamma = P<const float>(bn[1]);
+  a.beta = P<const float>(bn[2]);
+  a.mmean = P<float>(bn[3]);
+  a.mvar = P<float>(bn[4]);
+  a.mean = P<float>(bn[5]);
+  a.rstd = P<float>(bn[6]);
+  a.scale = P<float>(bn[7]);
+  a.shift = P<float>(bn[8]);
+  a.momentum = momentum;
+  a.eps = eps;
+  a.update_moving = update_moving;
+  a.w = P<const bf16>(w);
+  a.bias = P<const float>(bias);
+  a.labels = P<const int>(labels);
+  a.N = shape[0];
+  a.HW = shape[1];
+  a.C = shape[2];
+  a.classes = shape[3];
+  a.kpad = shape[4];
+  a.grad_scale = grad_scale;
+  a.pooled = P<bf16>(out[0]);
+  a.dlogits = P<bf16>(out[1]);
+  a.ws = P<float>(out[2]);
+  a.dact = P<bf16>(out[3]);
+  a.bacc = P<double>(out[4]);
+  if (!head_fused_supported(a.N, a.HW, a.C, a.classes, a.kpad))
+    throw std::invalid_argument("head_fused: unsupported head shape");
+  return [a](hipStream_t s) { head_fused(a, s); };
+}
+
 static Launch mk_maxpool_fwd(ptr_t x, ptr_t y, ptr_t argmax, std::vector<int> geom, int k) {
   ConvGeom g = geom_from(geom);
   if (g.C % 8) throw std::invalid_argument("maxpool: C % 8");
@@ -527,6 +576,10 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "bnrelu_avgpool", mk_bnrelu_avgpool);
   def_op(m, plan, "avgpool_bwd", mk_avgpool_bwd);
   def_op(m, plan, "softmax_xent", mk_softmax_xent);
+  def_op(m, plan, "softmax_xent_reduce", mk_softmax_xent_reduce);
+  def_op(m, plan, "head_fused", mk_head_fused);
+  m.def("head_fused_supported", &head_fused_supported,
+        "whether head_fused covers (N, HW, C, classes, kpad)");
   def_op(m, plan, "maxpool_fwd", mk_maxpool_fwd);
   def_op(m, plan, "maxpool_bwd", mk_maxpool_bwd);
   def_op(m, plan, "sgd_update_pack", mk_sgd_update_pack);

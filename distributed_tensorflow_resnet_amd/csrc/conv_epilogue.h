@@ -451,8 +451,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     }
     if constexpr (BNB) {
       if (ph == EL::PHASES - 1 || prow0 + EL::PR >= M) {   // last phase: reduce before storing
-        colsum8<EL::CPR, BN>(s1, red);
-        colsum8<EL::CPR, BN>(s2, red2);
+        colsum8x2<EL::CPR, BN>(s1, s2, red, red2);   // both sums behind one barrier
         if (tid < BN) {
           bnb_t1 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
           bnb_t2 = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];

@@ -9,6 +9,7 @@
 //     first-max window index, the backward gathers through it (deterministic).
 #include <stdexcept>
 
+#include "bn_fused.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -259,6 +260,215 @@ softmax_xent_reduce_kernel(const float* __restrict__ ws, int ld, int N, int clas
 }
 
 long softmax_xent_ws_floats(int N, int ld) { return (long)N * ld + 2L * N; }
+
+void softmax_xent_reduce(const float* ws, int ld, int N, int classes, float* loss_sum,
+                         float* correct, float* dbias, hipStream_t s) {
+  const int cb = dbias ? (classes + 63) / 64 : 1;
+  hipLaunchKernelGGL(softmax_xent_reduce_kernel, dim3((unsigned)cb), dim3(256), 0, s, ws, ld, N,
+                     classes, loss_sum, correct, dbias);
+  DTR_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Fused training head (HeadArgs, kernels.h): one workgroup per image.  Thread t owns
+// the 8-channel group t % G of pixels t / G, t / G + 256 / G, ...; per-channel sums
+// over the image fold the wave by xor-shuffles (lanes G apart share a group) and
+// the 4 waves through LDS in fixed order.  Numerics follow the unfused chain: bf16
+// pooled, fp32 logits + bias, bf16 dlogits, fp32-accumulated dense dgrad rounded to
+// bf16, avg-pool backward rounded to bf16, BN backward sums of that bf16 gradient.
+template <int C>
+__device__ __forceinline__ void head_colsum(float (&v)[8], float (*red)[C]) {
+  constexpr int G = C / 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int off = G; off < 64; off <<= 1) v[j] += __shfl_xor(v[j], off, 64);
+  if (lane < G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = v[j];
+  }
+}
+
+template <int C, int UPT>
+__global__ void __launch_bounds__(256) head_fused_kernel(HeadArgs a) {
+  constexpr int G = C / 8;
+  __shared__ float sc_s[C], sh_s[C], mu_s[C], rs_s[C], pool_s[C], dp_s[C], g_s[64];
+  __shared__ float red[4][C], red2[4][C];
+  __shared__ float w_s[C * 64];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = tid % G;
+  const int HW = a.HW, kpad = a.kpad, nunits = HW * G;
+  const bf16x8 zero8 = {};
+  // ---- loads: this image's activations (registers), dense weights (LDS) ----
+  bf16x8 xv[UPT];
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int u = tid + i * 256;
+    xv[i] = u < nunits ? *reinterpret_cast<const bf16x8*>(a.x + ((long)n * nunits + u) * 8)
+                       : zero8;
+  }
+  for (int e = tid; e < C * kpad; e += 256) w_s[e] = (float)a.w[e];
+  // ---- final BN statistics from the accumulators (block 0 publishes them) ----
+  if (tid < C) {
+    const int c = tid;
+    double s1, s2;
+    bn_acc_sums(a.acc, C, c, s1, s2);
+    const double M = (double)a.N * HW;
+    const double dm = s1 / M;
+    const double var = fmax(s2 / M - dm * dm, 0.0);
+    const float fmu = (float)dm, fvar = (float)var;
+    const float rs = rsqrtf(fvar + a.eps);
+    const float sc = a.gamma[c] * rs;
+    const float sh = a.beta[c] - fmu * sc;
+    sc_s[c] = sc;
+    sh_s[c] = sh;
+    mu_s[c] = fmu;
+    rs_s[c] = rs;
+    if (n == 0) {
+      a.mean[c] = fmu;
+      a.rstd[c] = rs;
+      a.scale[c] = sc;
+      a.shift[c] = sh;
+      if (a.update_moving) {
+        const float uvar = M > 1.0 ? (float)(var * M / (M - 1.0)) : fvar;
+        const float mm = a.mmean[c], mv = a.mvar[c];
+        a.mmean[c] = mm - (1.f - a.momentum) * (mm - fmu);
+        a.mvar[c] = mv - (1.f - a.momentum) * (mv - uvar);
+      }
+    }
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = sc_s[grp * 8 + j];
+    sh[j] = sh_s[grp * 8 + j];
+  }
+  // ---- BN + ReLU + global average pool ----
+  {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      if (tid + i * 256 >= nunits) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += fmaxf((float)xv[i][j] * sc[j] + sh[j], 0.f);
+    }
+    head_colsum<C>(s, red);
+  }
+  __syncthreads();
+  if (tid < C) {
+    const float t = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    const bf16 pb = (bf16)(t / (float)HW);
+    a.pooled[(long)n * C + tid] = pb;
+    pool_s[tid] = (float)pb;
+  }
+  __syncthreads();
+  // ---- dense + softmax cross-entropy row (wave 0, one class per lane) ----
+  if (wave == 0) {
+    const int y = a.labels[n];
+    float z = -INFINITY;
+    if (lane < a.classes) {
+      float acc = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < C; ++c) acc += pool_s[c] * w_s[c * kpad + lane];
+      z = acc + a.bias[lane];
+    }
+    float mx = z;
+    int amax = lane < a.classes ? lane : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {   // first max on ties, like tf.argmax
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(amax, o, 64);
+      if (om > mx || (om == mx && oa < amax)) {
+        mx = om;
+        amax = oa;
+      }
+    }
+    const float se = wave_sum(lane < a.classes ? __expf(z - mx) : 0.f);
+    const float lse = mx + __logf(se);
+    const float zy = __shfl(z, (y >= 0 && y < a.classes) ? y : 0, 64);
+    float g = 0.f;
+    if (lane < a.classes) g = (__expf(z - lse) - (lane == y ? 1.f : 0.f)) * a.grad_scale;
+    if (lane < kpad) {
+      const bf16 gb = (bf16)g;
+      a.dlogits[(long)n * kpad + lane] = gb;
+      a.ws[(long)n * kpad + lane] = g;
+      g_s[lane] = (float)gb;
+    }
+    if (lane == 0) {
+      float* rs = a.ws + (long)a.N * kpad + 2 * n;
+      rs[0] = lse - ((y >= 0 && y < a.classes) ? zy : lse);
+      rs[1] = (amax == y) ? 1.f : 0.f;
+    }
+  }
+  __syncthreads();
+  // ---- dense dgrad (bf16 out) -> average-pool backward (bf16) ----
+  if (tid < C) {
+    float d = 0.f;
+    for (int k = 0; k < kpad; ++k) d += g_s[k] * w_s[tid * kpad + k];
+    const float db = (float)(bf16)d;
+    dp_s[tid] = (float)(bf16)(db * (1.f / (float)HW));
+  }
+  __syncthreads();
+  // ---- dact rows + the final BN's backward sums (g = dact * relu mask) ----
+  {
+    float dv[8], mu[8], rs[8], s1[8], s2[8];
+    bf16x8 dvb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dv[j] = dp_s[grp * 8 + j];
+      dvb[j] = (bf16)dv[j];
+      mu[j] = mu_s[grp * 8 + j];
+      rs[j] = rs_s[grp * 8 + j];
+      s1[j] = s2[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int u = tid + i * 256;
+      if (u >= nunits) continue;
+      *reinterpret_cast<bf16x8*>(a.dact + ((long)n * nunits + u) * 8) = dvb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = (float)xv[i][j];
+        const float gg = (xf * sc[j] + sh[j] > 0.f) ? dv[j] : 0.f;
+        s1[j] += gg;
+        s2[j] += gg * (xf - mu[j]) * rs[j];
+      }
+    }
+    head_colsum<C>(s1, red);
+    head_colsum<C>(s2, red2);
+  }
+  __syncthreads();
+  if (tid < C) {
+    const float t1 = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    const float t2 = (red2[0][tid] + red2[1][tid]) + (red2[2][tid] + red2[3][tid]);
+    bn_acc_add(a.bacc, C, tid, (double)t1, (double)t2);
+  }
+}
+
+bool head_fused_supported(int N, int HW, int C, int classes, int kpad) {
+  return N > 0 && (C == 16 || C == 32 || C == 64) && HW >= 1 && HW * (C / 8) <= 4 * 256 &&
+         kpad <= 64 && classes <= kpad && classes >= 1;
+}
+
+void head_fused(const HeadArgs& a, hipStream_t s) {
+  if (!head_fused_supported(a.N, a.HW, a.C, a.classes, a.kpad))
+    throw std::invalid_argument("head_fused: unsupported head shape");
+  const int units = a.HW * (a.C / 8);
+  const dim3 grid((unsigned)a.N);
+#define DTR_HEAD(C_)                                                                        \
+  if (a.C == C_) {                                                                          \
+    if (units <= 256) hipLaunchKernelGGL((head_fused_kernel<C_, 1>), grid, dim3(256), 0, s, a); \
+    else if (units <= 512) hipLaunchKernelGGL((head_fused_kernel<C_, 2>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((head_fused_kernel<C_, 4>), grid, dim3(256), 0, s, a);           \
+  }
+  DTR_HEAD(16)
+  DTR_HEAD(32)
+  DTR_HEAD(64)
+#undef DTR_HEAD
+  DTR_CHECK_LAUNCH();
+}
 
 void softmax_xent(const float* logits, int ld, const int* labels, int N, int classes,
                   float* loss_sum, float* correct, bf16* dlogits, float* dbias, float grad_scale,

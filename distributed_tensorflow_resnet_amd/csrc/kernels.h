@@ -207,6 +207,43 @@ int bn_stats_tile_rows();
 // ---- head: BN-ReLU + global average pool, softmax cross-entropy ----
 void bnrelu_avgpool(const bf16* x, const float* scale, const float* shift, bf16* pooled,
                     int N, int HW, int C, hipStream_t s);
+
+// Whole training head in one launch (small heads: C <= 64 channels, HW <= 64, <= 64
+// padded classes -- the CIFAR networks): final BN finalize from its fp64
+// accumulators, BN+ReLU + global average pool, dense + bias, softmax cross-entropy
+// rows (per-row loss / correct / gradient into the softmax_xent workspace),
+// dense data gradient, average-pool backward (writes dact) and the final BN's
+// backward sums into its fp64 accumulators.  One workgroup per image.  The
+// batch-level folds (loss, precision, dbias) are softmax_xent_reduce's, the dense
+// weight gradient conv_wgrad's -- both off the critical path.
+struct HeadArgs {
+  const bf16* x;            // [N][HW][C] final BN input
+  const double* acc;        // final BN forward accumulators [BN_ACC_REP][2][C]
+  const float* gamma;
+  const float* beta;
+  float* mmean;
+  float* mvar;
+  float* mean;              // outputs (block 0): mean, rstd, scale, shift
+  float* rstd;
+  float* scale;
+  float* shift;
+  float momentum, eps;
+  int update_moving;
+  const bf16* w;            // dense weights, bf16 HWIO [C][kpad] (padded columns zero)
+  const float* bias;        // [classes]
+  const int* labels;        // [N]
+  int N, HW, C, classes, kpad;
+  float grad_scale;         // 1 / global batch
+  bf16* pooled;             // [N][C]
+  bf16* dlogits;            // [N][kpad]
+  float* ws;                // softmax_xent workspace: [N][kpad] fp32 gradient rows, [N][2]
+  bf16* dact;               // [N][HW][C] gradient of the pooled activations
+  double* bacc;             // final BN backward accumulators (sum g, sum g*xhat)
+};
+bool head_fused_supported(int N, int HW, int C, int classes, int kpad);
+void head_fused(const HeadArgs& a, hipStream_t s);
+void softmax_xent_reduce(const float* ws, int ld, int N, int classes, float* loss_sum,
+                         float* correct, float* dbias, hipStream_t s);
 void avgpool_bwd(const bf16* dpooled, bf16* dx, int N, int HW, int C, hipStream_t s);
 void softmax_xent(const float* logits, int ld, const int* labels, int N, int classes,
                   float* loss_sum, float* correct, bf16* dlogits, float* dbias,

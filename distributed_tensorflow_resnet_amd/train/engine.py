@@ -826,18 +826,41 @@ class Engine:
                 self._conv_fwd(plan, convs[2], a2, Xn, N, pre=p2, residual=residual,
                                stats_for=nxt)
         fbn = self.bns[spec.final_bn.name]
-        self._bn_finalize(plan, fbn, consumer_conv=False)   # consumer: bnrelu_avgpool
         XL = self.X[-1]
         HL, WL, F = XL.shape[1], XL.shape[2], XL.shape[3]
-        plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
-                            self.pooled.data_ptr(), N, HL * WL, F)
-        plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(), 0,
-                       0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N), [], [], [], [], [], BN_DECAY, BN_EPS, 1)
         sp = self.scalars.data_ptr()
-        plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
-                          spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
-                          self.dense_bias_grad, 1.0 / self.global_batch, 0,
-                          self.xent_ws.data_ptr())
+        # Small (CIFAR) heads: ONE launch for final BN finalize + BN-ReLU-avgpool + dense +
+        # softmax-xent rows + dense dgrad + avgpool backward + the final BN's backward
+        # sums (head_fused, head.hip) instead of 8 dependent launches; the batch folds
+        # (loss, precision, dbias) and the dense wgrad go to the side stream.
+        self._head_fused = (self.bn_acc_on and self.bn_bacc_on and fbn.pending is not None
+                            and fbn.pending[0] == "acc"
+                            and os.environ.get("DTR_FUSED_HEAD", "1") != "0"
+                            and self.nat.head_fused_supported(N, HL * WL, F, spec.num_classes,
+                                                              self.kpad))
+        self._dact = self._g(0, (N, HL, WL, F))
+        if self._head_fused:
+            fbn.pending = None
+            plan.head_fused(XL.data_ptr(),
+                            [fbn.acc.data_ptr(), fbn.gamma, fbn.beta, fbn.mmean, fbn.mvar,
+                             fbn.mean.data_ptr(), fbn.rstd.data_ptr(), fbn.scale.data_ptr(),
+                             fbn.shift.data_ptr()], BN_DECAY, BN_EPS, 1, self.dense_hwio,
+                            self.dense_bias, self.labels.data_ptr(),
+                            [N, HL * WL, F, spec.num_classes, self.kpad], 1.0 / self.global_batch,
+                            [self.pooled.data_ptr(), self.dlogits.data_ptr(),
+                             self.xent_ws.data_ptr(), self._dact.data_ptr(),
+                             fbn.bacc.data_ptr()])
+        else:
+            self._bn_finalize(plan, fbn, consumer_conv=False)   # consumer: bnrelu_avgpool
+            plan.bnrelu_avgpool(XL.data_ptr(), fbn.scale.data_ptr(), fbn.shift.data_ptr(),
+                                self.pooled.data_ptr(), N, HL * WL, F)
+            plan.conv_gemm(0, self.pooled.data_ptr(), self.dense_ohwi, 0, self.logits.data_ptr(),
+                           0, 0, 0, self.dense_bias, spec.num_classes, 0, 0, self._dense_geom(N),
+                           [], [], [], [], [], BN_DECAY, BN_EPS, 1)
+            plan.softmax_xent(self.logits.data_ptr(), self.kpad, self.labels.data_ptr(), N,
+                              spec.num_classes, sp, sp + 4, self.dlogits.data_ptr(),
+                              self.dense_bias_grad, 1.0 / self.global_batch, 0,
+                              self.xent_ws.data_ptr())
         self.seg["fwd"] = (b0, plan.size())
 
         # ---- backward
@@ -845,7 +868,8 @@ class Engine:
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
         self._reduced = set()
         self._side_q, self._side_blocks = [], 0
-        self._main_wgrad = self.fork_wgrad   # the dense wgrad below runs on the main stream
+        # the dense wgrad below runs on the main stream (unless the head is fused)
+        self._main_wgrad = self.fork_wgrad and not self._head_fused
         # 1/2 sum v^2 of the (pre-update) weights for the reported `cost` only: it
         # rides in the first side-stream batch, off the critical path (ImageNet:
         # 25.5 M floats, ~80 us on the main stream).
@@ -859,17 +883,34 @@ class Engine:
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
         dpart = self.wg_part.data_ptr() + 4 * off
-        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0, dpart, dg, spl, pps)
+        dense_wgrad = lambda: plan.conv_wgrad(self.dlogits.data_ptr(),  # noqa: E731
+                                              self.pooled.data_ptr(), 0, 0, dpart, dg, spl, pps)
         self._pending[self.dense_name] = (dpart, self.dense_grad, spl, self.kpad,
                                           spec.num_classes, 1, F, F)
         self._produced.add(self.dense_name)
-        plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0, 0,
-                       0, 0, 0, 0, 0, 0, dg, [], [], [], [], [], BN_DECAY, BN_EPS, 1)
-        dact = self._g(0, (N, HL, WL, F))
-        plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
+        dact = self._dact
         d = 1
         dout = self._g(d, tuple(XL.shape))
-        self._bn_bwd(plan, fbn, dact, XL, dout)
+        if self._head_fused:
+            # batch folds of the head's rows (loss, precision, dbias) and the dense
+            # weight gradient: side stream; the final BN backward is pending on its
+            # accumulator sums for the first dgrad's BN-backward prologue
+            xr = lambda: plan.softmax_xent_reduce(  # noqa: E731
+                self.xent_ws.data_ptr(), self.kpad, N, spec.num_classes, sp, sp + 4,
+                self.dense_bias_grad)
+            if self.fork_wgrad:
+                self._side_q += [xr, dense_wgrad]
+            else:
+                xr()
+                dense_wgrad()
+            self._bnb_src = (fbn.bacc.data_ptr(), -1)
+            self._bn_bwd(plan, fbn, dact, XL, dout, reduced=True)
+        else:
+            dense_wgrad()
+            plan.conv_gemm(1, self.dlogits.data_ptr(), self.dense_hwio, self.dpooled.data_ptr(), 0,
+                           0, 0, 0, 0, 0, 0, 0, dg, [], [], [], [], [], BN_DECAY, BN_EPS, 1)
+            plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
+            self._bn_bwd(plan, fbn, dact, XL, dout)
         for i in range(len(blocks) - 1, -1, -1):
             b = blocks[i]
             X = self.X[i]

@@ -188,3 +188,24 @@ def test_bn_accumulator_mode_matches_partials(gpu, monkeypatch):
     assert abs(l1 - l0) <= 1e-4 * max(1.0, abs(l0))
     assert _rel(g1, g0) < 1e-2
     assert _rel(s1, s0) < 1e-5
+
+
+def test_fused_head_matches_unfused(gpu, monkeypatch):
+    """head_fused (one launch: final BN finalize .. final BN backward sums) vs the
+    8-launch head: same loss, precision, gradients and BN statistics up to rounding."""
+    spec = cifar_spec(8)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DTR_FUSED_HEAD", mode)
+        eng, _, _, _ = _make(spec, 64, gpu)
+        assert eng._head_fused == (mode == "1")
+        st = torch.cuda.current_stream().cuda_stream
+        eng._run("fwd", st)
+        eng._run("bwd", st)
+        torch.cuda.synchronize()
+        res[mode] = (eng.scalars[:2].clone(), eng.grad.clone(), eng.params.stats.clone())
+    (s0, g0, t0), (s1, g1, t1) = res["0"], res["1"]
+    assert abs(s1[0].item() - s0[0].item()) <= 1e-4 * max(1.0, abs(s0[0].item()))
+    assert s1[1].item() == s0[1].item()
+    assert _rel(g1, g0) < 1e-2
+    assert _rel(t1, t0) < 1e-5
