@@ -347,6 +347,22 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
   return [a](hipStream_t s) { head_fused(a, s); };
 }
 
+// bn_bwd_apply with the finalize fused in: fin = [acc, gamma, dgamma, dbeta, coef]
+static Launch mk_bn_bwd_apply_acc(ptr_t dy, ptr_t x, ptr_t mean, ptr_t rstd, ptr_t scale,
+                                  ptr_t shift, std::vector<ptr_t> fin, ptr_t add, ptr_t dx, int M,
+                                  int C) {
+  if (fin.size() != 5) throw std::invalid_argument("bn_bwd_apply_acc: fin needs 5 pointers");
+  if (!bn_bwd_apply_acc_fits(M, C))
+    throw std::invalid_argument("bn_bwd_apply_acc: shape exceeds the fused-finalize bound");
+  const BwdAccFin f{P<const double>(fin[0]), P<const float>(fin[1]), P<float>(fin[2]),
+                    P<float>(fin[3]), P<float>(fin[4]), M};
+  return [=](hipStream_t s) {
+    bn_relu_bwd_apply_acc(P<const bf16>(dy), P<const bf16>(x), P<const float>(mean),
+                          P<const float>(rstd), P<const float>(scale), P<const float>(shift), f,
+                          P<const bf16>(add), P<bf16>(dx), M, C, s);
+  };
+}
+
 static Launch mk_maxpool_fwd(ptr_t x, ptr_t y, ptr_t argmax, std::vector<int> geom, int k) {
   ConvGeom g = geom_from(geom);
   if (g.C % 8) throw std::invalid_argument("maxpool: C % 8");
@@ -577,6 +593,9 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "avgpool_bwd", mk_avgpool_bwd);
   def_op(m, plan, "softmax_xent", mk_softmax_xent);
   def_op(m, plan, "softmax_xent_reduce", mk_softmax_xent_reduce);
+  def_op(m, plan, "bn_bwd_apply_acc", mk_bn_bwd_apply_acc);
+  m.def("bn_bwd_apply_acc_fits", &bn_bwd_apply_acc_fits,
+        "whether bn_bwd_apply_acc (finalize fused into the apply) covers (M, C)");
   def_op(m, plan, "head_fused", mk_head_fused);
   m.def("head_fused_supported", &head_fused_supported,
         "whether head_fused covers (N, HW, C, classes, kpad)");

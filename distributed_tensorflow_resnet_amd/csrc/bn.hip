@@ -582,11 +582,36 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                     const float* __restrict__ mean, const float* __restrict__ rstd,
                     const float* __restrict__ scale, const float* __restrict__ shift,
                     const float* __restrict__ coef, const bf16* __restrict__ add,
-                    bf16* __restrict__ dx, long nvec, int C) {
+                    bf16* __restrict__ dx, long nvec, int C, BwdAccFin fin) {
   const int G = C / 8;
   const long T = (long)gridDim.x * 256;
   const int c0 = (int)(threadIdx.x % G) * 8;
   float sc[8], sh[8], mu[8], rs[8], ca[8], cb[8], cc[8];
+  __shared__ float cf[3][BWD_ACC_FIN_MAXC];
+  const float* cfp = coef;
+  int ld = C;
+  if (fin.acc != nullptr) {   // accumulator mode: this launch is also the finalize
+    const int c = threadIdx.x;
+    if (c < C) {
+      double s1, s2;
+      bn_acc_sums(fin.acc, C, c, s1, s2);
+      const float sg = (float)s1, sgx = (float)s2;
+      const float a = fin.gamma[c] * rstd[c];
+      cf[0][c] = a;
+      cf[1][c] = a * sg / (float)fin.M;
+      cf[2][c] = a * sgx / (float)fin.M;
+      if (blockIdx.x == 0) {
+        fin.dbeta[c] = sg;
+        fin.dgamma[c] = sgx;
+        fin.coef[c] = cf[0][c];
+        fin.coef[C + c] = cf[1][c];
+        fin.coef[2 * C + c] = cf[2][c];
+      }
+    }
+    __syncthreads();
+    cfp = &cf[0][0];
+    ld = BWD_ACC_FIN_MAXC;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = c0 + j;
@@ -594,9 +619,9 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
     sh[j] = shift[c];
     mu[j] = mean[c];
     rs[j] = rstd[c];
-    ca[j] = coef[c];
-    cb[j] = coef[C + c];
-    cc[j] = coef[2 * C + c];
+    ca[j] = cfp[c];
+    cb[j] = cfp[ld + c];
+    cc[j] = cfp[2 * ld + c];
   }
   const bf16x8 zero8 = {};
   for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += U * T) {
@@ -637,7 +662,26 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
   long blocks = (nvec + 256L * U - 1) / (256L * U);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3((unsigned)blocks), dim3(256), 0, s, dy, x,
-                     mean, rstd, scale, shift, coef, add, dx, nvec, C);
+                     mean, rstd, scale, shift, coef, add, dx, nvec, C, BwdAccFin{});
+  DTR_CHECK_LAUNCH();
+}
+
+bool bn_bwd_apply_acc_fits(int M, int C) {
+  const long nvec = (long)M * C / 8;
+  return C <= BWD_ACC_FIN_MAXC && C % 8 == 0 && 256 % (C / 8) == 0 &&
+         (nvec + 511) / 512 <= 1024;   // every block re-reads 16 fp64 per channel
+}
+
+void bn_relu_bwd_apply_acc(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                           const float* scale, const float* shift, const BwdAccFin& fin,
+                           const bf16* add, bf16* dx, int M, int C, hipStream_t s) {
+  if (!bn_bwd_apply_acc_fits(M, C))
+    throw std::runtime_error("bn_relu_bwd_apply_acc: shape exceeds the fused-finalize bound");
+  const long nvec = (long)M * C / 8;
+  constexpr int U = 2;
+  const long blocks = (nvec + 256L * U - 1) / (256L * U);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3((unsigned)blocks), dim3(256), 0, s, dy, x,
+                     mean, rstd, scale, shift, fin.coef, add, dx, nvec, C, fin);
   DTR_CHECK_LAUNCH();
 }
 

@@ -200,6 +200,21 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
                        const bf16* add, bf16* dx, int M, int C, hipStream_t s);
 void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M,
                    int C, hipStream_t s);
+// The same apply with the finalize fused in (accumulator mode, small C): every block
+// derives the coefficients from the fp64 sums; block 0 writes dgamma/dbeta/coef.
+constexpr int BWD_ACC_FIN_MAXC = 64;
+struct BwdAccFin {
+  const double* acc;        // [BN_ACC_REP][2][C] (sum g, sum g*xhat); nullptr = off
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* coef;              // [3][C] out
+  int M;
+};
+bool bn_bwd_apply_acc_fits(int M, int C);
+void bn_relu_bwd_apply_acc(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
+                           const float* scale, const float* shift, const BwdAccFin& fin,
+                           const bf16* add, bf16* dx, int M, int C, hipStream_t s);
 
 void bn_stats(const bf16* x, int M, int C, float* part, hipStream_t s);
 int bn_stats_tile_rows();

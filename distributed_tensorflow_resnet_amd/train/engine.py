@@ -680,10 +680,18 @@ class Engine:
             return
         self._pending_bwd = None
         bn, M, C = pb["bn"], pb["M"], pb["bn"].spec.channels
+        add = pb["add"]
+        self._produced.update(bn.names)
+        if pb["cnt"] == -1 and self.nat.bn_bwd_apply_acc_fits(M, C):
+            # accumulator sums, small C: the apply launch finalizes too (one launch less)
+            plan.bn_bwd_apply_acc(pb["da"].data_ptr(), pb["x"].data_ptr(), bn.mean.data_ptr(),
+                                  bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(),
+                                  [pb["part"], bn.gamma, bn.dgamma, bn.dbeta,
+                                   self.coef.data_ptr()],
+                                  0 if add is None else add.data_ptr(), pb["out"].data_ptr(), M, C)
+            return
         plan.bn_bwd_finalize(pb["part"], pb["cnt"], M, C, bn.gamma, bn.rstd.data_ptr(),
                              bn.dgamma, bn.dbeta, self.coef.data_ptr())
-        self._produced.update(bn.names)
-        add = pb["add"]
         plan.bn_bwd_apply(pb["da"].data_ptr(), pb["x"].data_ptr(), bn.mean.data_ptr(),
                           bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(),
                           self.coef.data_ptr(), 0 if add is None else add.data_ptr(),
