@@ -47,7 +47,8 @@ def main(argv=None) -> int:
                     help="capture the step in a hipGraph (single stream); default: eager native "
                          "plan with weight gradients on a second stream (measured faster)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for compatibility)")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-mb", type=float, default=0.0,
+                    help="all-reduce bucket size (MiB); 0 = auto (~4 buckets, <= 25 MiB)")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=("fp32", "bf16"),
                     help="gradient all-reduce precision (bf16 halves the xGMI bytes)")
     args = ap.parse_args(argv)

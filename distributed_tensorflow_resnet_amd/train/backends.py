@@ -194,7 +194,7 @@ class CPUBackend:
 
 def make_backend(spec: ModelSpec, batch_size: int, *, device: str, weight_decay: float,
                  lr_schedule, optimizer: str = "mom", seed: int = 0, dist_ctx=None,
-                 bucket_mb: float = 25.0, use_graph: bool = False, global_batch=None,
+                 bucket_mb: float | None = None, use_graph: bool = False, global_batch=None,
                  input_mode: str = "auto", data_seed: int = 1234,
                  allreduce_dtype: str = "fp32"):
     """device: gpu | cpu | auto."""

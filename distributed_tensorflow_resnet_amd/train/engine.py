@@ -144,7 +144,7 @@ class Engine:
 
     def __init__(self, spec: ModelSpec, batch_size: int, *, weight_decay: float,
                  lr_schedule: LRSchedule, optimizer: str = "mom", momentum: float = 0.9,
-                 device=None, dist_ctx=None, bucket_mb: float = 25.0, reduce_mb: float | None = None,
+                 device=None, dist_ctx=None, bucket_mb: float | None = None, reduce_mb: float | None = None,
                  seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
                  use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None,
@@ -195,6 +195,12 @@ class Engine:
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
         if self.dist is not None and self.world > 1:
+            if not bucket_mb:
+                # ~4 buckets, at most 25 MB each: ImageNet RN50's 97 MB of gradients in
+                # 25 MB all-reduces overlapping the backward; CIFAR RN50's 2.9 MB in four,
+                # so all but the last (stage 1's small kernels) overlap the backward
+                # instead of one latency-bound all-reduce after it
+                bucket_mb = min(25.0, 4.0 * self.params.n_train / 2 ** 20 / 4)
             self.buckets = assign_buckets(self.params.train_slots, int(bucket_mb * 2 ** 20))
         else:  # one bucket: nothing to all-reduce, only the split-K reduces
             self.buckets = [(0, self.params.n_train, [s.name for s in self.params.train_slots])]

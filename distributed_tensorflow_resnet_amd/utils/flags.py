@@ -133,7 +133,8 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_bool("synthetic", False, "Synthetic data of the dataset's shape.")
     p.add_argument("--weight_decay", type=float, default=d["weight_decay"])
     p.add_argument("--optimizer", default="mom", choices=("mom", "sgd"))
-    p.add_argument("--bucket_mb", type=float, default=25.0, help="All-reduce bucket size (MiB).")
+    p.add_argument("--bucket_mb", type=float, default=0.0,
+                   help="All-reduce bucket size (MiB); 0 = auto (~4 buckets, <= 25 MiB).")
     p.add_bool("use_graph", False, "Capture the training step in a hipGraph (single stream; "
                "default eager native plan with a second weight-gradient stream).")
     p.add_argument("--seed", type=int, default=0)
