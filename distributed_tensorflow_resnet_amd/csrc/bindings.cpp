@@ -576,6 +576,18 @@ PYBIND11_MODULE(_C, m) {
         std::vector<int> v;
         for (const auto& o : p.ops) v.push_back(o.stream);
         return v;
+      })
+      // (kind, event) per op for the host-side stream-ordering check
+      // (utils/streamcheck.py): kind 0 launch, 1 record, 2 wait; event -1 for launches.
+      .def("op_kinds", [](const Plan& p) {
+        std::vector<int> v;
+        for (const auto& o : p.ops) v.push_back(o.kind);
+        return v;
+      })
+      .def("op_events", [](const Plan& p) {
+        std::vector<int> v;
+        for (const auto& o : p.ops) v.push_back(o.ev);
+        return v;
       });
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);

@@ -39,6 +39,7 @@ from .. import native
 from ..models.params import ParamStore
 from ..models.spec import BNSpec, ConvSpec, ModelSpec
 from ..parallel.buckets import assign_buckets, schedule_buckets
+from ..utils.streamcheck import check_plan
 
 BF16 = torch.bfloat16
 BN_DECAY = 0.997
@@ -1000,6 +1001,9 @@ class Engine:
         self.seg["opt"] = (b2, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
         assert not missing, f"gradients never produced: {missing[:4]}"
+        errs = check_plan(plan, self.seg)   # fork/join of the two streams (race check)
+        if errs:
+            raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
 
     # ------------------------------------------------------------------ running
     def repack(self):

@@ -209,3 +209,25 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
     assert s1[1].item() == s0[1].item()
     assert _rel(g1, g0) < 1e-2
     assert _rel(t1, t0) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec_fn,N,fork_every", [
+    (lambda: cifar_spec(50), 16, "2"),
+    (lambda: cifar_spec(20), 32, "1"),
+    (lambda: imagenet_spec(18), 8, "2"),
+])
+def test_built_plans_pass_stream_order_check(gpu, monkeypatch, spec_fn, N, fork_every):
+    """The engine refuses a plan with a fork/join race at construction
+    (utils/streamcheck.py); pin that real plans are checked and pass, and that the
+    check sees side-stream work at all (otherwise it would pass vacuously)."""
+    from distributed_tensorflow_resnet_amd.utils.streamcheck import check_plan
+
+    monkeypatch.setenv("DTR_FORK_EVERY", fork_every)
+    eng = Engine(spec_fn(), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
+                 device=gpu, use_graph=False)
+    assert eng.fork_wgrad
+    assert check_plan(eng.plan, eng.seg) == []
+    a, b = eng.seg["bwd"]
+    assert 1 in eng.plan.op_streams()[a:b]
+    assert 2 in eng.plan.op_kinds()[a:b]
