@@ -51,7 +51,11 @@ def main(argv=None) -> int:
                     help="all-reduce bucket size (MiB); 0 = auto (~4 buckets, <= 25 MiB)")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=("fp32", "bf16"),
                     help="gradient all-reduce precision (bf16 halves the xGMI bytes)")
+    ap.add_argument("--roctx", action="store_true",
+                    help="wrap each step's phases in roctx ranges (rocprofv3 --marker-trace)")
     args = ap.parse_args(argv)
+    if args.roctx:
+        os.environ["DTR_ROCTX"] = "1"
 
     import torch
 

@@ -173,6 +173,7 @@ class Engine:
             # handles the cross-stream event edges poorly); graphs stay single-stream
             fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
         self.fork_every = max(1, int(os.environ.get("DTR_FORK_EVERY", "2")))
+        self.markers = os.environ.get("DTR_ROCTX", "0") != "0"
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
             input_mode = "cifar_u8" if spec.dataset.startswith("cifar") else "nhwc"
@@ -1023,9 +1024,23 @@ class Engine:
 
     def _step_eager(self):
         st = torch.cuda.current_stream().cuda_stream
+        if self.markers:
+            return self._step_marked(st)
         self._run("fwd", st)
         self._run_bwd(st)
         self._run("opt", st)
+
+    def _step_marked(self, st):
+        """The eager step inside roctx ranges (DTR_ROCTX=1 / bench --roctx): the
+        phases show up as markers in `rocprofv3 --marker-trace` timelines."""
+        nvtx = torch.cuda.nvtx   # roctx on ROCm builds of PyTorch
+        nvtx.range_push("dtr.step")
+        for name, fn in (("fwd", lambda: self._run("fwd", st)), ("bwd+allreduce",
+                         lambda: self._run_bwd(st)), ("opt", lambda: self._run("opt", st))):
+            nvtx.range_push(f"dtr.{name}")
+            fn()
+            nvtx.range_pop()
+        nvtx.range_pop()
 
     def _run_bwd(self, st):
         a, b = self.seg["bwd"]
