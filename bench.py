@@ -7,19 +7,29 @@ n=8; 758,618 params), global batch 128 split over the N ranks (strong scaling),
 bf16 compute / fp32 master weights, synthetic data (random uint8 CIFAR records
 augmented on the device every step: pad-4/crop/flip/standardize), random-init
 weights.  One full training step is timed: forward, backward, RCCL gradient
-all-reduce (N>1), SGD-momentum + weight-decay update, BN moving averages.
+all-reduce (N>1, native communicator on a comm stream overlapping backward),
+SGD-momentum + weight-decay update, BN moving averages.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--model cifar_resnet50]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  `--model imagenet_resnet50` measures BASELINE
-config 4 (128 images per GPU, weak scaling, baseline 0.93 stp/s).
+Without torchrun, `--gpus N` (N > 1) spawns the N rank processes itself before
+anything touches the GPU (env RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT, as torchrun sets them) and relays rank 0's line; it fails if any
+rank fails.  Rank 0 prints ONE JSON line.  `--model imagenet_resnet50` measures
+BASELINE config 4 (128 images per GPU, weak scaling, baseline 0.93 stp/s),
+`--model imagenet_resnet101` config 5 (256 per GPU).
+
+`--device cpu` runs the fp32 PyTorch CPU trainer (gloo for N > 1): a plumbing
+check of this contract for hosts without a GPU, never a headline number.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,30 +43,125 @@ MODELS = {
     "imagenet_resnet50": ("imagenet", 50, 128, False, 0.93, "README.md:39-44 (8 P100, 8ps-8wk)"),
     "imagenet_resnet101": ("imagenet", 101, 256, False, None, None),
 }
+METRIC = "steps/sec (global_batch=128 CIFAR-10 / 1024 ImageNet) ResNet-50 at 1/2/4/8 MI355X"
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description=__doc__)
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="cifar_resnet50", choices=sorted(MODELS))
     ap.add_argument("--batch", type=int, default=None,
                     help="global batch (cifar) or per-GPU batch (imagenet)")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: fp32 PyTorch trainer (contract check only, not a headline)")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the step in a hipGraph (single stream); default: eager native "
-                         "plan with weight gradients on a second stream (measured faster)")
+                    help="capture the step in a hipGraph (single stream, 1 GPU only); default: "
+                         "eager native plan with weight gradients on a second stream (measured faster)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for compatibility)")
     ap.add_argument("--bucket-mb", type=float, default=0.0,
                     help="all-reduce bucket size (MiB); 0 = auto (~4 buckets, <= 25 MiB)")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=("fp32", "bf16"),
                     help="gradient all-reduce precision (bf16 halves the xGMI bytes)")
+    ap.add_argument("--phase-steps", type=int, default=5,
+                    help="extra steps after the timed region with per-phase HIP-event timing "
+                         "(forward / backward / exposed all-reduce / optimizer); 0 = skip")
     ap.add_argument("--roctx", action="store_true",
-                    help="wrap each step's phases in roctx ranges (rocprofv3 --marker-trace)")
-    args = ap.parse_args(argv)
-    if args.roctx:
-        os.environ["DTR_ROCTX"] = "1"
+                    help="wrap each step's phases in roctx ranges (rocprofv3 --marker-trace); "
+                         "adds host overhead, recorded in the JSON")
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Run this script as n rank processes (torchrun's env contract) and relay rank
+    0's stdout.  The parent never imports torch, so it never touches the GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        out = subprocess.PIPE if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=out, text=True))
+    rc = 0
+    failed = None
+    while True:
+        alive = False
+        for r, p in enumerate(procs):
+            c = p.poll()
+            if c is None:
+                alive = True
+            elif c != 0 and failed is None:
+                failed = (r, c)
+        if failed is not None or not alive:
+            break
+        time.sleep(0.2)
+    if failed is not None:
+        print(f"bench.py: rank {failed[0]} exited with {failed[1]}; stopping the others",
+              file=sys.stderr)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        rc = 1
+    out = procs[0].stdout.read() if procs[0].stdout else ""
+    for line in out.splitlines():
+        print(line, flush=True)
+    return rc or max(p.returncode or 0 for p in procs)
+
+
+def dtr_env() -> dict:
+    """Every DTR_* knob of this run (fusion modes, diagnostics): echoed into the JSON."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("DTR_")}
+
+
+def run_cpu(args, dataset, size, per_rank, global_batch, world):
+    import torch
+
+    from distributed_tensorflow_resnet_amd.models.spec import build_spec
+    from distributed_tensorflow_resnet_amd.parallel.dist import DistContext
+    from distributed_tensorflow_resnet_amd.train.backends import CPUBackend
+    from distributed_tensorflow_resnet_amd.train.engine import cifar_lr_schedule, imagenet_lr_schedule
+
+    ctx = DistContext(backend="gloo")
+    spec = build_spec(dataset, size)
+    sched = cifar_lr_schedule() if dataset.startswith("cifar") else imagenet_lr_schedule()
+    be = CPUBackend(spec, per_rank, weight_decay=2e-4, lr_schedule=sched, seed=0, dist_ctx=ctx,
+                    global_batch=global_batch)
+    be.broadcast_parameters(0)
+    g = torch.Generator().manual_seed(ctx.rank)
+    x = torch.randint(0, 256, (per_rank, 3, spec.image_h, spec.image_w), generator=g,
+                      dtype=torch.uint8)
+    y = torch.randint(0, spec.num_classes, (per_rank,), generator=g)
+    for _ in range(args.warmup):
+        be.set_batch(x, y)
+        be.step()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        be.set_batch(x, y)
+        be.step()
+    ctx.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    ctx.all_reduce_max(el)
+    m = be.metrics()
+    return ctx, float(el.item()), m, {"dtype": "fp32", "device": "cpu"}, None
+
+
+def run_gpu(args, dataset, size, per_rank, global_batch, world):
     import torch
 
     from distributed_tensorflow_resnet_amd.models.spec import build_spec
@@ -64,25 +169,10 @@ def main(argv=None) -> int:
     from distributed_tensorflow_resnet_amd.train.engine import (Engine, cifar_lr_schedule,
                                                                 imagenet_lr_schedule)
 
-    dataset, size, batch, is_global, baseline, _src = MODELS[args.model]
-    if args.batch:
-        batch = args.batch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus > 1 must be launched with torchrun", file=sys.stderr)
-            return 2
     local_rank = local_device_index()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     ctx = DistContext(device=device)
-    if is_global:
-        if batch % world:
-            raise SystemExit(f"global batch {batch} not divisible by {world}")
-        per_rank, global_batch = batch // world, batch
-    else:
-        per_rank, global_batch = batch, batch * world
-
     spec = build_spec(dataset, size)
     sched = cifar_lr_schedule() if dataset.startswith("cifar") else imagenet_lr_schedule()
     wd = 2e-4 if dataset.startswith("cifar") else 1e-4
@@ -113,10 +203,61 @@ def main(argv=None) -> int:
     ctx.all_reduce_max(t)
     elapsed = float(t.item())
     m = eng.metrics()
+    # per-phase timing, outside the timed region (not part of `value`)
+    phases = None
+    if args.phase_steps > 0 and not use_graph:
+        acc = {}
+        for _ in range(args.phase_steps):
+            for k, v in eng.step_timed().items():
+                acc[k] = acc.get(k, 0.0) + v
+        phases = {k: round(v / args.phase_steps, 4) for k, v in acc.items()}
+    extra = {"dtype": "bf16", "device": torch.cuda.get_device_name(device),
+             "graph": use_graph, "wgrad_stream": eng.fork_wgrad, "comm": eng.comm_info(),
+             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
+    return ctx, elapsed, m, extra, phases
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if os.environ.get("DTR_DIAG_SKIP"):
+        print("bench.py: refusing to benchmark with DTR_DIAG_SKIP set (it drops launches: "
+              "wrong math, timing only)", file=sys.stderr)
+        return 2
+    under_launcher = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not under_launcher:
+        return spawn_ranks(args.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.graph and world > 1:
+        print("bench.py: --graph is single-GPU only (no test covers RCCL inside a captured "
+              "multi-stream step)", file=sys.stderr)
+        return 2
+    if args.roctx:
+        os.environ["DTR_ROCTX"] = "1"
+
+    dataset, size, batch, is_global, baseline, _src = MODELS[args.model]
+    if args.batch:
+        batch = args.batch
+    if is_global:
+        if batch % world:
+            raise SystemExit(f"global batch {batch} not divisible by {world}")
+        per_rank, global_batch = batch // world, batch
+    else:
+        per_rank, global_batch = batch, batch * world
+
+    runner = run_cpu if args.device == "cpu" else run_gpu
+    ctx, elapsed, m, extra, phases = runner(args, dataset, size, per_rank, global_batch, world)
+    import torch.distributed as dist
+
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else None
     sps = args.steps / elapsed
     if ctx.is_chief:
         out = {
-            "metric": "steps/sec (global_batch=128 CIFAR-10 / 1024 ImageNet) ResNet-50 at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(sps, 3),
             "unit": "steps/s",
             "n_gpus": world,
@@ -126,19 +267,23 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "strong" if is_global else "weak",
             "vs_baseline": round(sps / baseline, 3) if baseline else None,
-            "dtype": "bf16",
+            "dtype": extra["dtype"],
             "data": "synthetic (random uint8 images, on-device augmentation each step), random-init weights",
             "config": {
                 "model": f"resnet{size}_v2_{dataset}",
                 "global_batch": global_batch,
                 "per_gpu_batch": per_rank,
                 "seq_len": None,
-                "image_size": spec.image_h,
+                "image_size": 32 if dataset.startswith("cifar") else 224,
                 "parallelism": f"dp{world}",
-                "graph": use_graph,
-                "wgrad_stream": eng.fork_wgrad,
                 "allreduce_dtype": args.allreduce_dtype,
+                "roctx": bool(args.roctx),
+                "env": dtr_env(),
+                **{k: v for k, v in extra.items() if k != "dtype"},
             },
+            "dist_backend": backend,
+            "pg_world_size": pg_world,
+            "phase_ms": phases,
             "images_per_sec": round(sps * global_batch, 1),
             "final_loss": round(m["cross_entropy"], 4),
         }

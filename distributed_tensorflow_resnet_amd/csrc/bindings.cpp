@@ -18,10 +18,12 @@
 
 #include <chrono>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "comm.h"
 #include "data.h"
 #include "kernels.h"
 #include "optim.h"
@@ -464,29 +466,38 @@ static Launch mk_cast_b2f(ptr_t a, ptr_t b, long n) {
 }
 
 // ---------------------------------------------------------------- Plan
-// A plan is a list of ops, each bound to one of two streams (0 = main,
-// 1 = side), plus cross-stream event record/wait ops.  Recording the side
-// stream's first op behind a wait on a main-stream event makes the fork/join
-// structure capturable into a hipGraph (it becomes graph edges).
+// A plan is a list of ops, each bound to one of three streams (0 = main
+// compute, 1 = side compute for weight gradients, 2 = RCCL comm), plus
+// cross-stream event record/wait ops.  Recording a stream's first op behind a
+// wait on another stream's event makes the fork/join structure explicit (and
+// capturable into a hipGraph: the waits become graph edges).  The structure is
+// checked host-side when a plan is built (utils/streamcheck.py).
+enum OpKind { OP_LAUNCH = 0, OP_RECORD = 1, OP_WAIT = 2, OP_TIMING = 3 };
+constexpr int PLAN_STREAMS = 3;
+
 struct PlanOp {
-  Launch fn;       // launch (kind 0)
-  int stream;      // 0 main, 1 side
-  int kind;        // 0 launch, 1 record event, 2 wait event
-  int ev;
+  Launch fn;       // launch (OP_LAUNCH)
+  int stream;      // 0 main, 1 side, 2 comm
+  int kind;        // OpKind
+  int ev;          // event index (record / wait), timing-event index (OP_TIMING)
 };
 
 struct Plan {
   std::vector<PlanOp> ops;
   std::vector<std::string> names;
   std::vector<hipEvent_t> events;
+  std::vector<hipEvent_t> tevents;            // timing events (OP_TIMING)
+  std::vector<std::shared_ptr<void>> keep;   // objects the launches reference (communicators)
   std::vector<double> host_us;   // per-op host issue time (profile mode only)
   bool profile = false;
+  bool timing = false;           // OP_TIMING ops record only when enabled
   int cur = 0;
   ~Plan() {
     for (auto e : events) (void)hipEventDestroy(e);
+    for (auto e : tevents) (void)hipEventDestroy(e);
   }
   int add(Launch l, const std::string& name) {
-    ops.push_back(PlanOp{std::move(l), cur, 0, -1});
+    ops.push_back(PlanOp{std::move(l), cur, OP_LAUNCH, -1});
     names.push_back(name);
     return (int)ops.size() - 1;
   }
@@ -498,37 +509,83 @@ struct Plan {
     return (int)events.size() - 1;
   }
   int record(int ev) {
-    ops.push_back(PlanOp{Launch(), cur, 1, ev});
+    if (ev < 0 || ev >= (int)events.size()) throw std::out_of_range("record: unknown event");
+    ops.push_back(PlanOp{Launch(), cur, OP_RECORD, ev});
     names.push_back("record");
     return (int)ops.size() - 1;
   }
   int wait(int ev) {
-    ops.push_back(PlanOp{Launch(), cur, 2, ev});
+    if (ev < 0 || ev >= (int)events.size()) throw std::out_of_range("wait: unknown event");
+    ops.push_back(PlanOp{Launch(), cur, OP_WAIT, ev});
     names.push_back("wait");
     return (int)ops.size() - 1;
   }
-  void run(int begin, int end, ptr_t main_stream, ptr_t side_stream) {
+  // A timing probe on the current stream (HIP event with timing); a no-op unless
+  // set_timing(true).  Not a synchronisation op: the stream check ignores it.
+  int timing_point(const std::string& label) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
+    tevents.push_back(e);
+    ops.push_back(PlanOp{Launch(), cur, OP_TIMING, (int)tevents.size() - 1});
+    names.push_back("timing:" + label);
+    return (int)ops.size() - 1;
+  }
+  double elapsed_ms(int op_a, int op_b) const {
+    for (int i : {op_a, op_b})
+      if (i < 0 || i >= (int)ops.size() || ops[i].kind != OP_TIMING)
+        throw std::invalid_argument("elapsed_ms: not a timing op");
+    float ms = 0.f;
+    const hipError_t e = hipEventElapsedTime(&ms, tevents[ops[op_a].ev], tevents[ops[op_b].ev]);
+    if (e != hipSuccess)
+      throw std::runtime_error(std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
+    return ms;
+  }
+  void run(int begin, int end, ptr_t main_stream, ptr_t side_stream, ptr_t comm_stream) {
     if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
-    hipStream_t st[2] = {S(main_stream), S(side_stream ? side_stream : main_stream)};
-    py::gil_scoped_release nogil;
-    if (profile && host_us.size() != ops.size()) host_us.assign(ops.size(), 0.0);
-    for (int i = begin; i < end; ++i) {
-      const PlanOp& o = ops[i];
-      hipStream_t s = st[o.stream];
-      const auto t0 = profile ? std::chrono::steady_clock::now()
-                              : std::chrono::steady_clock::time_point();
-      if (o.kind == 0) {
-        o.fn(s);
-      } else if (o.kind == 1) {
-        if (hipEventRecord(events[o.ev], s) != hipSuccess) fprintf(stderr, "hipEventRecord failed\n");
-      } else {
-        if (hipStreamWaitEvent(s, events[o.ev], 0) != hipSuccess)
-          fprintf(stderr, "hipStreamWaitEvent failed\n");
+    hipStream_t st[PLAN_STREAMS] = {S(main_stream), S(side_stream ? side_stream : main_stream),
+                                    S(comm_stream ? comm_stream : main_stream)};
+    int bad_op = -1;
+    hipError_t bad = hipSuccess;
+    {
+      py::gil_scoped_release nogil;
+      if (profile && host_us.size() != ops.size()) host_us.assign(ops.size(), 0.0);
+      for (int i = begin; i < end; ++i) {
+        const PlanOp& o = ops[i];
+        hipStream_t s = st[o.stream];
+        const auto t0 = profile ? std::chrono::steady_clock::now()
+                                : std::chrono::steady_clock::time_point();
+        hipError_t e = hipSuccess;
+        if (o.kind == OP_LAUNCH) {
+          o.fn(s);
+        } else if (o.kind == OP_RECORD) {
+          e = hipEventRecord(events[o.ev], s);
+        } else if (o.kind == OP_WAIT) {
+          e = hipStreamWaitEvent(s, events[o.ev], 0);
+        } else if (timing) {
+          e = hipEventRecord(tevents[o.ev], s);
+        }
+        // A failed record/wait silently drops a fork or join the stream check
+        // certified: remember the first failure and stop issuing.
+        if (e != hipSuccess) {
+          bad_op = i;
+          bad = e;
+          break;
+        }
+        if (profile)
+          host_us[i] += std::chrono::duration<double, std::micro>(
+                            std::chrono::steady_clock::now() - t0).count();
       }
-      if (profile)
-        host_us[i] += std::chrono::duration<double, std::micro>(
-                          std::chrono::steady_clock::now() - t0).count();
+      if (bad == hipSuccess) {
+        const hipError_t e = hipGetLastError();   // a failed kernel launch anywhere in the range
+        if (e != hipSuccess) {
+          bad = e;
+          bad_op = end - 1;
+        }
+      }
     }
+    if (bad != hipSuccess)
+      throw std::runtime_error("plan op " + std::to_string(bad_op) + " (" + names[bad_op] +
+                               ") failed: " + hipGetErrorString(bad));
   }
   int size() const { return (int)ops.size(); }
 };
@@ -538,7 +595,12 @@ struct Plan {
 template <typename R, typename... Args>
 static void def_op(py::module_& m, py::class_<Plan>& plan, const char* name,
                    R (*maker)(Args...)) {
-  m.def(name, [maker](Args... args, ptr_t stream) { maker(args...)(S(stream)); });
+  m.def(name, [maker, name](Args... args, ptr_t stream) {
+    maker(args...)(S(stream));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      throw std::runtime_error(std::string(name) + " launch failed: " + hipGetErrorString(e));
+  });
   plan.def(name, [maker, name](Plan& p, Args... args) { return p.add(maker(args...), name); });
 }
 
@@ -557,14 +619,31 @@ PYBIND11_MODULE(_C, m) {
   py::class_<Plan> plan(m, "Plan");
   plan.def(py::init<>())
       .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"),
-           py::arg("side_stream") = 0)
+           py::arg("side_stream") = 0, py::arg("comm_stream") = 0)
       .def("size", &Plan::size)
       .def("new_event", &Plan::new_event)
       .def("record", &Plan::record)
       .def("wait", &Plan::wait)
       .def("use_stream", [](Plan& p, int s) {
-        if (s != 0 && s != 1) throw std::invalid_argument("stream index must be 0 or 1");
+        if (s < 0 || s >= PLAN_STREAMS)
+          throw std::invalid_argument("stream index must be 0 (main), 1 (side) or 2 (comm)");
         p.cur = s;
+      })
+      .def("current_stream", [](const Plan& p) { return p.cur; })
+      .def("timing_point", &Plan::timing_point)
+      .def("set_timing", [](Plan& p, bool on) { p.timing = on; })
+      .def("elapsed_ms", &Plan::elapsed_ms)
+      // in-place SUM all-reduce of `count` elements at `ptr` on the plan's current
+      // stream through the native RCCL communicator (dtype: 7 fp32, 9 bf16)
+      .def("all_reduce", [](Plan& p, std::shared_ptr<Comm> c, ptr_t ptr, long long count,
+                            int dtype) {
+        if (!c) throw std::invalid_argument("all_reduce: no communicator");
+        if (count <= 0) throw std::invalid_argument("all_reduce: empty buffer");
+        Comm* cp = c.get();
+        p.keep.push_back(c);
+        return p.add([cp, ptr, count, dtype](hipStream_t s) {
+          cp->all_reduce(P<void>(ptr), (size_t)count, dtype, s);
+        }, "all_reduce");
       })
       .def("names", [](const Plan& p) { return p.names; })
       .def("set_profile", [](Plan& p, bool on) {
@@ -589,6 +668,32 @@ PYBIND11_MODULE(_C, m) {
         for (const auto& o : p.ops) v.push_back(o.ev);
         return v;
       });
+
+  // Native RCCL communicator (comm.h).  Construction is collective and blocks
+  // until every rank has joined, so the GIL is released.
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def(py::init([](py::bytes id, int world, int rank, int device) {
+             std::string uid = id;
+             py::gil_scoped_release nogil;
+             return std::make_shared<Comm>(uid, world, rank, device);
+           }),
+           py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"))
+      .def("all_reduce", [](const Comm& c, ptr_t p, long long n, int dtype, ptr_t s) {
+        c.all_reduce(P<void>(p), (size_t)n, dtype, S(s));
+      })
+      .def("broadcast", [](const Comm& c, ptr_t p, long long n, int dtype, int root, ptr_t s) {
+        c.broadcast(P<void>(p), (size_t)n, dtype, root, S(s));
+      })
+      .def("async_error", &Comm::async_error)
+      .def("abort", &Comm::abort)
+      .def_property_readonly("world", &Comm::world)
+      .def_property_readonly("rank", &Comm::rank)
+      .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
+      .def_static("library", &Comm::library);
+  m.attr("COMM_F32") = (int)COMM_F32;
+  m.attr("COMM_BF16") = (int)COMM_BF16;
+  m.attr("COMM_F64") = (int)COMM_F64;
+  m.attr("COMM_I64") = (int)COMM_I64;
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);
   def_op(m, plan, "conv_wgrad", mk_conv_wgrad);
@@ -666,6 +771,13 @@ PYBIND11_MODULE(_C, m) {
       "crc32c",
       [](py::buffer b, uint32_t crc) {
         py::buffer_info info = b.request();
+        // the byte count below assumes a dense C-contiguous buffer
+        py::ssize_t expect = info.itemsize;
+        for (int d = info.ndim - 1; d >= 0; --d) {
+          if (info.shape[d] > 1 && info.strides[d] != expect)
+            throw std::invalid_argument("crc32c: buffer must be C-contiguous");
+          expect *= info.shape[d];
+        }
         const size_t n = (size_t)info.size * (size_t)info.itemsize;
         py::gil_scoped_release nogil;
         return dtr::crc32c_extend(crc, reinterpret_cast<const uint8_t*>(info.ptr), n);

@@ -61,6 +61,36 @@ class DistContext:
         elif dist.is_initialized():
             self.backend = dist.get_backend()
 
+    def native_comm(self, device_index: int, force: bool = False):
+        """The native RCCL communicator of this job (`_C.Comm`, csrc/comm.h) or None.
+
+        Built when the job runs on RCCL ("nccl" backend) with more than one rank,
+        or when ``force`` (single-rank tests of the comm path).  Rank 0's
+        ncclUniqueId travels through the c10d TCP store, the same rendezvous the
+        process group used; each call makes a fresh communicator (the ranks must
+        call in the same order, as they build their engines in the same order).
+        DTR_NATIVE_COMM=0 keeps the gradient all-reduce on c10d instead."""
+        if os.environ.get("DTR_NATIVE_COMM", "1") == "0" and not force:
+            return None
+        if not force and not (self.active and self.backend == "nccl"):
+            return None
+        from .. import native
+
+        nat = native(required=True)
+        self._comm_seq = getattr(self, "_comm_seq", 0) + 1
+        if self.active:
+            store = dist.distributed_c10d._get_default_store()
+            key = f"dtr/rccl_uid/{self._comm_seq}"
+            if self.rank == 0:
+                uid = nat.Comm.unique_id()
+                store.set(key, uid)
+            else:
+                uid = bytes(store.get(key))
+            world, rank = self.world_size, self.rank
+        else:
+            uid, world, rank = nat.Comm.unique_id(), 1, 0
+        return nat.Comm(uid, world, rank, device_index)
+
     @property
     def is_chief(self) -> bool:
         return self.rank == 0

@@ -11,6 +11,7 @@ checkpoint layout, so a run can be resumed on either.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -83,7 +84,11 @@ class CPUBackend:
                  optimizer: str = "mom", momentum: float = 0.9, seed: int = 0, dist_ctx=None,
                  global_batch: int | None = None, threads: int = 0,
                  allreduce_dtype: str = "fp32"):
-        if threads:
+        # intra-op threads: DTR_CPU_THREADS, default 1 -- on small containers the
+        # OpenMP pool's spin-waits oversubscribe the CPU quota (measured here: one
+        # 8x32x32x16 conv fwd+bwd 1.2 ms on 1 thread, 612 ms on 8)
+        threads = threads or int(os.environ.get("DTR_CPU_THREADS", "1"))
+        if threads > 0:
             torch.set_num_threads(threads)
         self.spec = spec
         self.N = batch_size

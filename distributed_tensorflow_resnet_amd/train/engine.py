@@ -16,15 +16,17 @@ step with all pointers bound:
             wgrad (MFMA, fused BN-ReLU recompute of its input) + deterministic
             reduce into the flat fp32 gradient; per BN one reduce / finalize /
             apply (ReLU mask and residual-gradient add fused);
-  allreduce cut points after the op that finalises each gradient bucket
-            (parallel/buckets.py) -> RCCL all-reduce on torch.distributed's
-            NCCL stream, overlapping the rest of backward;
+  allreduce after the op that finalises each gradient bucket
+            (parallel/buckets.py): a plan op on the comm stream -- the native
+            RCCL communicator (csrc/comm.h) all-reduces the bucket while the
+            compute streams continue the backward; the optimizer waits on it
+            (c10d all-reduces between plan segments for gloo rehearsals);
   optimizer one fused SGD-momentum + weight-decay + bf16 re-pack launch, LR from
             the device-resident global_step, then global_step += 1.
 
-The plan runs natively segment by segment (no Python per op) and the whole
-step is captured once into a hipGraph (torch.cuda.CUDAGraph), so a step costs
-one graph launch on the host.
+The plan runs natively segment by segment (no Python per op); `use_graph`
+captures the whole step into a hipGraph instead (measured slower than the eager
+native plan on this runtime, profiles/launch_mode_ab.md).
 """
 from __future__ import annotations
 
@@ -149,7 +151,7 @@ class Engine:
                  seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
                  use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None,
-                 allreduce_dtype: str = "fp32"):
+                 allreduce_dtype: str = "fp32", native_comm: bool | None = None):
         self.nat = native(required=True)
         self.spec = spec
         self.N = batch_size
@@ -185,18 +187,33 @@ class Engine:
         self.params = ParamStore(spec, device=dev)
         self.params.initialize(seed)
         self.grad = torch.zeros(self.params.n_train, device=dev)
-        self.grad_bf16 = (torch.zeros(self.params.n_train, dtype=BF16, device=dev)
-                          if self.allreduce_bf16 and self.world > 1 else None)
         self.mom = torch.zeros(self.params.n_train, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
         self.scalars = torch.zeros(8, device=dev)  # loss_sum, correct, lr, l2
         self.side = torch.cuda.Stream(device=dev)   # weight-gradient stream
+        self.comm_stream = torch.cuda.Stream(device=dev)   # RCCL all-reduces
+        # Native RCCL communicator: the bucket all-reduces are plan ops on the comm
+        # stream.  None: world 1 (nothing to reduce) or a gloo rehearsal (c10d
+        # all-reduces issued by the host between plan segments, _run_bwd).
+        # native_comm=True forces it on a single rank (tests of the comm path).
+        self.comm = None
+        didx = dev.index if dev.index is not None else torch.cuda.current_device()
+        if self.dist is not None and (self.world > 1 or native_comm):
+            if native_comm is not False:
+                self.comm = self.dist.native_comm(didx, force=bool(native_comm))
+        elif native_comm:
+            from ..parallel.dist import DistContext
+            self.comm = DistContext().native_comm(didx, force=True)
+        self.grad_bf16 = (torch.zeros(self.params.n_train, dtype=BF16, device=dev)
+                          if self.allreduce_bf16 and (self.world > 1 or self.comm is not None)
+                          else None)
         self._build_weight_layout()
         self._alloc_activations()
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
-        if self.dist is not None and self.world > 1:
+        self.reduce_buckets = self.world > 1 or self.comm is not None
+        if self.reduce_buckets:
             if not bucket_mb:
                 # ~4 buckets, at most 25 MB each: ImageNet RN50's 97 MB of gradients in
                 # 25 MB all-reduces overlapping the backward; CIFAR RN50's 2.9 MB in four,
@@ -223,10 +240,15 @@ class Engine:
             sub = assign_buckets([slot_of[n] for n in names], int(reduce_mb * 2 ** 20))
             self.reduce_groups.append([g[2] for g in sub])
         self._build_train_plan()
-        if self.dist is not None and self.world > 1:
+        if self.reduce_buckets and self.comm is None:
+            # gloo rehearsal: the host issues each bucket's c10d all-reduce at its
+            # ready index, between Plan.run calls (_run_bwd)
             self.bucket_sched = schedule_buckets(self.buckets, self.ready_index)
         else:
             self.bucket_sched = []
+        errs = check_plan(self.plan, self.seg, barriers=[i for i, _, _ in self.bucket_sched])
+        if errs:   # fork/join structure of the three streams (race check)
+            raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
         self.graph = None
         self._captured = False
         self.eval_plans = {}
@@ -741,7 +763,7 @@ class Engine:
                 self._reduced.add((bi, gi))
             if not all((bi, gi) in self._reduced for gi in range(len(self.reduce_groups[bi]))):
                 continue
-            if self.world > 1 or force:
+            if self.reduce_buckets or force:
                 if self.fork_wgrad:
                     # join: the main stream (and the bucket's all-reduce) waits for the side stream
                     ev = plan.new_event()
@@ -751,6 +773,39 @@ class Engine:
                     plan.wait(ev)
                 self._mark(plan, *names)
                 self._flushed.add(bi)
+                if self.comm is not None:
+                    self._emit_allreduce(plan, lo, hi)
+
+    def _emit_allreduce(self, plan, lo: int, hi: int):
+        """Fork the comm stream off the main stream at the bucket's ready point and
+        all-reduce grad[lo:hi) there (bf16 exchange: cast kernels on the comm
+        stream around a bf16 all-reduce), while the compute streams continue."""
+        ev = plan.new_event()
+        plan.record(ev)
+        plan.use_stream(2)
+        plan.wait(ev)
+        n = hi - lo
+        g = self.grad.data_ptr() + 4 * lo
+        if self.grad_bf16 is not None:
+            gb = self.grad_bf16.data_ptr() + 2 * lo
+            plan.cast_f32_bf16(g, gb, n)
+            plan.all_reduce(self.comm, gb, n, self.nat.COMM_BF16)
+            plan.cast_bf16_f32(gb, g, n)
+        else:
+            plan.all_reduce(self.comm, g, n, self.nat.COMM_F32)
+        self._n_allreduce += 1
+        self._allreduce_bytes += n * (2 if self.grad_bf16 is not None else 4)
+        plan.use_stream(0)
+
+    def _join_comm(self, plan):
+        """The optimizer (main stream) waits for every bucket's all-reduce."""
+        if self.comm is None or not self._n_allreduce:
+            return
+        ev = plan.new_event()
+        plan.use_stream(2)
+        plan.record(ev)
+        plan.use_stream(0)
+        plan.wait(ev)
 
     def _emit_reduce(self, plan, names):
         descs = [self._pending.pop(n) for n in names if n in self._pending]
@@ -783,7 +838,9 @@ class Engine:
             e.fused_fwd = False
             e.pending = None
         self._cnt_next = 0
+        self._n_allreduce, self._allreduce_bytes = 0, 0
         b0 = plan.size()
+        self._t_fwd0 = plan.timing_point("fwd_begin")
         # the step's BN accumulators start at zero: cleared by the CIFAR augmentation
         # kernel (no extra launch), else by a memset
         zero = (self.bn_acc.data_ptr(), self.bn_acc.numel() * 8) \
@@ -881,6 +938,7 @@ class Engine:
 
         # ---- backward
         b1 = plan.size()
+        self._t_bwd0 = plan.timing_point("bwd_begin")
         self._pending, self._produced, self._flushed = {}, {"dense/bias"}, set()
         self._reduced = set()
         self._side_q, self._side_blocks = [], 0
@@ -985,6 +1043,9 @@ class Engine:
         self._conv_bwd(plan, stem, dstem_src, self.x_in, N, None, side=False)
         self._flush_side(plan, force=True)
         self._flush_buckets(plan, force=True)
+        self._t_bwd_done = plan.timing_point("bwd_compute_done")
+        self._join_comm(plan)
+        self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
 
         # ---- optimizer
@@ -999,12 +1060,10 @@ class Engine:
         plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
                        self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr(),
                        self.gstep.data_ptr())   # + global_step += 1
+        self._t_opt_end = plan.timing_point("opt_end")
         self.seg["opt"] = (b2, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
         assert not missing, f"gradients never produced: {missing[:4]}"
-        errs = check_plan(plan, self.seg)   # fork/join of the two streams (race check)
-        if errs:
-            raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
 
     # ------------------------------------------------------------------ running
     def repack(self):
@@ -1020,7 +1079,7 @@ class Engine:
 
     def _run(self, name, stream):
         a, b = self.seg[name]
-        self.plan.run(a, b, stream, self.side.cuda_stream)
+        self.plan.run(a, b, stream, self.side.cuda_stream, self.comm_stream.cuda_stream)
 
     def _step_eager(self):
         st = torch.cuda.current_stream().cuda_stream
@@ -1042,46 +1101,89 @@ class Engine:
             nvtx.range_pop()
         nvtx.range_pop()
 
+    def _host_allreduce(self, lo, hi):
+        """gloo rehearsal: a c10d all-reduce of grad[lo:hi) issued by the host."""
+        if self.grad_bf16 is not None:
+            buf = self.grad_bf16[lo:hi]
+            buf.copy_(self.grad[lo:hi])
+            return self.dist.all_reduce_async(buf), lo, hi
+        return self.dist.all_reduce_async(self.grad[lo:hi]), lo, hi
+
+    def _host_allreduce_wait(self, works):
+        for w, lo, hi in works:
+            w.wait()
+            if self.grad_bf16 is not None:
+                self.grad[lo:hi].copy_(self.grad_bf16[lo:hi])
+
     def _run_bwd(self, st):
         a, b = self.seg["bwd"]
-        works = []
+        side, comm = self.side.cuda_stream, self.comm_stream.cuda_stream
         if self.bucket_sched:
-            side = self.side.cuda_stream
-            prev = a
+            works, prev = [], a
             for idx, lo, hi in self.bucket_sched:
                 if idx > prev:
-                    self.plan.run(prev, idx, st, side)
+                    self.plan.run(prev, idx, st, side, comm)
                     prev = idx
-                if self.grad_bf16 is not None:
-                    buf = self.grad_bf16[lo:hi]
-                    buf.copy_(self.grad[lo:hi])
-                    works.append((self.dist.all_reduce_async(buf), lo, hi))
-                else:
-                    works.append((self.dist.all_reduce_async(self.grad[lo:hi]), lo, hi))
+                works.append(self._host_allreduce(lo, hi))
             if b > prev:
-                self.plan.run(prev, b, st, side)
-            for w, lo, hi in works:
-                w.wait()
-                if self.grad_bf16 is not None:
-                    self.grad[lo:hi].copy_(self.grad_bf16[lo:hi])
+                self.plan.run(prev, b, st, side, comm)
+            self._host_allreduce_wait(works)
         else:
-            self.plan.run(a, b, st, self.side.cuda_stream)
+            self.plan.run(a, b, st, self.side.cuda_stream, self.comm_stream.cuda_stream)
 
     def step_timed(self) -> dict:
-        """One eager step with HIP-event timing per phase (ProfilerHook)."""
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        """One eager step with HIP-event timing per phase (ProfilerHook, bench.py):
+        forward, backward compute, the exposed all-reduce tail (from the end of
+        the backward's compute to the optimizer's join of the last bucket's
+        all-reduce; for gloo rehearsals, the host's c10d waits) and the optimizer."""
         st = torch.cuda.current_stream().cuda_stream
-        ev[0].record()
-        self._run("fwd", st)
-        ev[1].record()
-        self._run_bwd(st)
-        ev[2].record()
-        self._run("opt", st)
-        ev[3].record()
-        torch.cuda.synchronize()
-        return {"forward": ev[0].elapsed_time(ev[1]),
-                "backward+allreduce": ev[1].elapsed_time(ev[2]),
-                "optimizer": ev[2].elapsed_time(ev[3])}
+        p = self.plan
+        if self.bucket_sched:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            ev[0].record()
+            self._run("fwd", st)
+            ev[1].record()
+            a, b = self.seg["bwd"]
+            works, prev = [], a
+            for idx, lo, hi in self.bucket_sched:
+                self.plan.run(prev, idx, st, self.side.cuda_stream, self.comm_stream.cuda_stream)
+                prev = idx
+                works.append(self._host_allreduce(lo, hi))
+            self.plan.run(prev, b, st, self.side.cuda_stream, self.comm_stream.cuda_stream)
+            ev[2].record()
+            self._host_allreduce_wait(works)
+            ev[3].record()
+            self._run("opt", st)
+            ev[4].record()
+            torch.cuda.synchronize()
+            return {"forward": ev[0].elapsed_time(ev[1]), "backward": ev[1].elapsed_time(ev[2]),
+                    "allreduce_exposed": ev[2].elapsed_time(ev[3]),
+                    "backward+allreduce": ev[1].elapsed_time(ev[3]),
+                    "optimizer": ev[3].elapsed_time(ev[4])}
+        p.set_timing(True)
+        try:
+            self._run("fwd", st)
+            self._run_bwd(st)
+            self._run("opt", st)
+            torch.cuda.synchronize()
+        finally:
+            p.set_timing(False)
+        bwd = p.elapsed_ms(self._t_bwd0, self._t_bwd_done)
+        exposed = p.elapsed_ms(self._t_bwd_done, self._t_joined)
+        return {"forward": p.elapsed_ms(self._t_fwd0, self._t_bwd0), "backward": bwd,
+                "allreduce_exposed": exposed, "backward+allreduce": bwd + exposed,
+                "optimizer": p.elapsed_ms(self._t_joined, self._t_opt_end)}
+
+    def comm_info(self) -> dict:
+        """How the gradients are exchanged (bench.py JSON)."""
+        nat = self.comm is not None
+        per = 2 if self.grad_bf16 is not None else 4
+        return {"native_rccl": nat,
+                "buckets": len(self.buckets) if self.reduce_buckets else 0,
+                "allreduce_ops": self._n_allreduce if nat else len(self.bucket_sched),
+                "allreduce_bytes": (self._allreduce_bytes if nat else
+                                    sum((hi - lo) * per for _, lo, hi in self.bucket_sched)),
+                "rccl_library": self.nat.Comm.library() if nat else None}
 
     def capture(self, warmup: int = 2):
         """Run `warmup` real steps on a side stream, then capture one step."""
@@ -1157,8 +1259,14 @@ class Engine:
         BN moving statistics and global_step from `src` to every rank."""
         if self.dist is None or self.world == 1:
             return
-        for t in (self.params.master, self.params.stats, self.mom, self.gstep):
-            self.dist.broadcast(t, src)
+        if self.comm is not None:
+            st = torch.cuda.current_stream().cuda_stream
+            for t in (self.params.master, self.params.stats, self.mom, self.gstep):
+                code = self.nat.COMM_I64 if t.dtype == torch.int64 else self.nat.COMM_F32
+                self.comm.broadcast(t.data_ptr(), t.numel(), code, src, st)
+        else:
+            for t in (self.params.master, self.params.stats, self.mom, self.gstep):
+                self.dist.broadcast(t, src)
         self.repack()
 
     # ------------------------------------------------------------------ eval

@@ -1,61 +1,96 @@
 """Host-side stream-ordering check of a recorded native Plan (race detection).
 
-The training step is a static list of ops on two HIP streams (main = 0, side = 1)
-ordered only by event record/wait pairs (engine.py `_flush_side` / `_flush_buckets`).
-A missing fork or join is a data race that no GPU sanitizer on this pool can find
-(no XNACK / GPU ASan), and it usually shows up only as rare, non-reproducible
-gradient corruption.  This module checks the op list statically, once, when the
-engine builds the plan (SURVEY.md §5 "Race detection": stream-ordering asserts
-around comm/compute events; the reference has none -- its only checks are graph
-asserts, `/root/reference/vgg_preprocessing.py:67-84`, `cifar_input.py:110-115`).
+The training step is a static list of ops on three HIP streams (main = 0,
+side = 1 for weight gradients, comm = 2 for the RCCL all-reduces) ordered only
+by event record/wait pairs (engine.py `_flush_side` / `_flush_buckets` /
+`_emit_allreduce`).  A missing fork or join is a data race that no GPU
+sanitizer on this pool can find (no XNACK / GPU ASan), and it usually shows up
+only as rare, non-reproducible gradient corruption.  This module checks the op
+list statically, once, when the engine builds the plan (SURVEY.md §5 "Race
+detection": stream-ordering asserts around comm/compute events; the reference
+has none -- its only checks are graph asserts,
+`/root/reference/vgg_preprocessing.py:67-84`, `cifar_input.py:110-115`).
 
-Rules, per segment (a range of ops the host runs with one `Plan.run` call):
+It is a check of the fork/join STRUCTURE, with happens-before computed by
+vector clocks over the three streams; it does not know which buffers an op
+reads or writes, so its rules are stated conservatively in terms of "all work
+queued earlier".  Rules, per segment (a range of ops the host runs with one
+`Plan.run` call):
 
-R1  every wait names an event recorded earlier in the same segment, on the other
+R1  every wait names an event recorded earlier in the same segment, on another
     stream (a wait on a never-recorded event is a no-op: no ordering at all; a
     record from a previous segment may be a previous step's);
-R2  fork: every side-stream launch follows a side-stream wait on an event the main
-    stream recorded in the same segment (otherwise it races with the work the host
-    queued before the segment, e.g. the previous step's optimizer);
-R3  join: if the segment launched anything on the side stream, the main stream
-    waits, before the segment ends, on an event the side stream recorded after its
-    last launch (otherwise the next segment / all-reduce / optimizer reads
-    gradients that are still being written).
+R2  fork: every side- or comm-stream launch follows a wait (directly or through
+    another stream) on an event the main stream recorded in the same segment
+    (otherwise it races with the work the host queued before the segment, e.g.
+    the previous step's optimizer);
+R3  join: everything a segment launched on the side and comm streams is ordered
+    before the main stream's end of the segment (otherwise the next segment /
+    optimizer reads gradients that are still being written or all-reduced);
+R4  collectives: an all-reduce (or a host split point, `barriers`: an index
+    where the host issues a c10d all-reduce on the main stream between two
+    `Plan.run` calls) is ordered after EVERY launch queued before it in the
+    plan, on every stream -- the bucket it reads is complete, whichever stream
+    produced its gradients.
 
 Op encoding (`Plan.op_kinds` / `op_streams` / `op_events`): kind 0 launch,
-1 record, 2 wait; stream 0 main, 1 side.
+1 record, 2 wait, 3 timing probe (ignored); stream 0 main, 1 side, 2 comm.
 """
 from __future__ import annotations
 
 from typing import Dict, Iterable, List, Sequence, Tuple
 
-LAUNCH, RECORD, WAIT = 0, 1, 2
+LAUNCH, RECORD, WAIT, TIMING = 0, 1, 2, 3
+NSTREAMS = 3
+_COLLECTIVES = ("all_reduce",)
 
 
 def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Sequence[int],
                      segments: Iterable[Tuple[str, int, int]],
-                     names: Sequence[str] | None = None) -> List[str]:
-    """Return a list of human-readable violations (empty = ordering is sound)."""
+                     names: Sequence[str] | None = None,
+                     barriers: Sequence[int] = ()) -> List[str]:
+    """Return a list of human-readable violations (empty = ordering is sound).
+
+    ``barriers``: plan indices where the host runs a collective on the main
+    stream between two Plan.run calls (the op at that index has not been issued
+    yet); checked with rule R4 like an all-reduce op at that position."""
     n = len(kinds)
     if len(streams) != n or len(events) != n:
         raise ValueError("kinds/streams/events length mismatch")
     errs: List[str] = []
+    barrier_set = set(barriers)
 
     def op(i: int) -> str:
-        return f"op {i}" + (f" ({names[i]})" if names is not None else "")
+        return f"op {i}" + (f" ({names[i]})" if names is not None and i < n else "")
 
     for seg, a, b in segments:
         if not (0 <= a <= b <= n):
             errs.append(f"{seg}: bad range [{a}, {b}) for a plan of {n} ops")
             continue
-        rec: Dict[int, Tuple[int, int]] = {}   # event -> (stream, index) of latest record
-        forked = False                         # side stream ordered after main in this segment
-        last_side_launch = -1
-        joined_after = -1                      # latest side index a main wait has joined
+        # clock[s][t]: latest plan index of a launch on stream t known to complete
+        # before the current point of stream s (-1: none); launched[t]: latest
+        # launch on t so far.  fork[s]: stream s is ordered after a main record.
+        clock = [[-1] * NSTREAMS for _ in range(NSTREAMS)]
+        rec: Dict[int, Tuple[int, List[int], bool]] = {}   # event -> (stream, clock, forked)
+        forked = [True, False, False]
+        launched = [-1] * NSTREAMS
+        reported_fork = [False] * NSTREAMS
+
+        def r4(i: int, s: int, what: str):
+            for t in range(NSTREAMS):
+                if t != s and launched[t] > clock[s][t]:
+                    errs.append(f"{seg}: {what} at {op(i)} is not ordered after {op(launched[t])} "
+                                f"on stream {t} (R4)")
+
         for i in range(a, b):
+            if i in barrier_set:
+                r4(i, 0, "host all-reduce split")
             k, s, e = kinds[i], streams[i], events[i]
+            if not 0 <= s < NSTREAMS:
+                errs.append(f"{seg}: {op(i)} on unknown stream {s}")
+                continue
             if k == RECORD:
-                rec[e] = (s, i)
+                rec[e] = (s, list(clock[s]), forked[s])
             elif k == WAIT:
                 src = rec.get(e)
                 if src is None:
@@ -66,23 +101,28 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
                     errs.append(f"{seg}: {op(i)} waits on event {e} recorded on its own "
                                 f"stream (R1: no cross-stream ordering)")
                     continue
-                if s == 1:
-                    forked = True
-                else:
-                    joined_after = max(joined_after, src[1])
-            elif k == LAUNCH and s == 1:
-                if not forked:
-                    errs.append(f"{seg}: side-stream {op(i)} before any fork from the main "
+                clock[s] = [max(x, y) for x, y in zip(clock[s], src[1])]
+                forked[s] = forked[s] or src[2]
+            elif k == LAUNCH:
+                if s != 0 and not forked[s] and not reported_fork[s]:
+                    errs.append(f"{seg}: stream-{s} {op(i)} before any fork from the main "
                                 f"stream (R2)")
-                    forked = True   # report once per segment
-                last_side_launch = i
-        if last_side_launch >= 0 and joined_after < last_side_launch:
-            errs.append(f"{seg}: side-stream work up to {op(last_side_launch)} is never "
-                        f"joined into the main stream before the segment ends (R3)")
+                    reported_fork[s] = True
+                if names is not None and names[i] in _COLLECTIVES:
+                    r4(i, s, names[i])
+                clock[s][s] = i
+                launched[s] = i
+        if b in barrier_set:
+            r4(b, 0, "host all-reduce split")
+        for t in (1, 2):
+            if launched[t] > clock[0][t]:
+                errs.append(f"{seg}: stream-{t} work up to {op(launched[t])} is never "
+                            f"joined into the main stream before the segment ends (R3)")
     return errs
 
 
-def check_plan(plan, segments: Dict[str, Tuple[int, int]]) -> List[str]:
+def check_plan(plan, segments: Dict[str, Tuple[int, int]], barriers: Sequence[int] = ()) -> List[str]:
     """`check_plan_order` over a native `_C.Plan` and the engine's {name: (a, b)}."""
     return check_plan_order(plan.op_kinds(), plan.op_streams(), plan.op_events(),
-                            [(k, a, b) for k, (a, b) in segments.items()], plan.names())
+                            [(k, a, b) for k, (a, b) in segments.items()], plan.names(),
+                            barriers=barriers)
