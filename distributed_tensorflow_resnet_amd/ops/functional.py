@@ -16,6 +16,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import native
+from .reference import BN_EPS
 
 BF16 = torch.bfloat16
 
@@ -109,7 +110,7 @@ def conv2d_fwd(x, w_ohwi, stride: int, *, pre_scale=None, pre_shift=None, residu
                        0 if out_f32 else out.data_ptr(), out.data_ptr() if out_f32 else 0,
                        _ptr(residual), _ptr(pre_scale), _ptr(pre_shift), _ptr(bias),
                        0 if bias is None else bias.numel(), _ptr(stat_part), int(accumulate),
-                       g.as_list(), [], _ptrs(fin), [], _ptrs(pfin), [], 0.997, 1e-5, 1, _stream())
+                       g.as_list(), [], _ptrs(fin), [], _ptrs(pfin), [], 0.997, BN_EPS, 1, _stream())
     return out
 
 
@@ -137,7 +138,7 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
         out = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
     bl = [] if bnb is None else [t.data_ptr() for t in bnb]
     native().conv_gemm(1, dy.data_ptr(), w_hwio.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0,
-                       int(accumulate), g.as_list(), bl, [], _ptrs(bfin), [], _ptrs(abwd), 0.997, 1e-5, 1,
+                       int(accumulate), g.as_list(), bl, [], _ptrs(bfin), [], _ptrs(abwd), 0.997, BN_EPS, 1,
                        _stream())
     return out
 
@@ -166,7 +167,7 @@ def conv2d_wgrad(dy, x, kh: int, kw: int, stride: int, *, pre_scale=None, pre_sh
 
 
 def bn_finalize(stat_part, tiles, tile_rows, M, gamma, beta, moving_mean, moving_var,
-                momentum=0.997, eps=1e-5, update_moving=True):
+                momentum=0.997, eps=BN_EPS, update_moving=True):
     C = gamma.numel()
     dev = gamma.device
     mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))

@@ -11,7 +11,12 @@ import torch
 import torch.nn.functional as F
 
 BN_DECAY = 0.997   # _BATCH_NORM_DECAY, resnet_model_official.py:37
-BN_EPS = 1e-5      # _BATCH_NORM_EPSILON, resnet_model_official.py:38
+# _BATCH_NORM_EPSILON = 1e-5 (resnet_model_official.py:38), but tf.layers' fused batch
+# norm raises any epsilon below 1.001e-5 to 1.001e-5 (cuDNN's minimum): every
+# FusedBatchNorm/FusedBatchNormGrad node in the reference's graphs carries
+# epsilon = float32(1.001e-5) (model.ckpt-107738.meta, resnet50_cifar_frozen_model_eval.pb;
+# tests/test_graphdef_cpu.py pins it).  This is the value the math uses.
+BN_EPS = 1.001e-5
 
 
 def fixed_pads(kernel_size: int) -> tuple[int, int]:

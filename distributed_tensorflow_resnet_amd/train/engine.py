@@ -47,7 +47,7 @@ BF16 = torch.bfloat16
 BN_DECAY = 0.997
 # Diagnostics: DTR_DIAG_SKIP=wgrad,dgrad,... drops those launches (wrong math; timing only)
 _DIAG_SKIP = set(filter(None, os.environ.get("DTR_DIAG_SKIP", "").split(",")))
-BN_EPS = 1e-5
+from ..ops.reference import BN_EPS  # noqa: E402  (TF's effective 1.001e-5)
 
 WGD_DTYPE = np.dtype([
     ("part", "<u8"), ("grad", "<u8"), ("splits", "<i4"), ("K", "<i4"), ("Kv", "<i4"),

@@ -2,10 +2,11 @@
 """Freeze a checkpoint into a self-contained inference artifact and run it
 (reference resnet_cifar_frozen_model.py: export_meta_graph + freeze_graph ->
 .pb with outputs `predictions,precision`, then feed-dict inference on 100
-test images).  Our artifact is a safetensors file (utils/frozen.py).
+test images).  utils/frozen.py writes the same TensorFlow GraphDef (node for
+node the reference's resnet50_cifar_frozen_model_eval.pb), without TensorFlow.
 
     python resnet_cifar_frozen_model.py --checkpoint_path /tmp/ckpt/model.ckpt-1000 \
-        --output resnet50_cifar_frozen_model_eval.safetensors [--eval_data_path DIR]
+        --output resnet50_cifar_frozen_model_eval.pb [--eval_data_path DIR]
 """
 import argparse
 import os
@@ -21,11 +22,11 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--checkpoint_path", default="")
     ap.add_argument("--train_dir", default="")
-    ap.add_argument("--output", default="resnet50_cifar_frozen_model_eval.safetensors")
+    ap.add_argument("--output", default="resnet50_cifar_frozen_model_eval.pb")
     ap.add_argument("--dataset", default="cifar10")
     ap.add_argument("--resnet_size", type=int, default=50)
     ap.add_argument("--eval_data_path", default="")
-    ap.add_argument("--device", default="auto")
+    ap.add_argument("--device", default="auto", choices=("auto", "gpu", "cpu", "interp"))
     a = ap.parse_args(argv)
     prefix = a.checkpoint_path or tb.latest_checkpoint(a.train_dir)
     if not prefix:

@@ -3,7 +3,14 @@
 resnet_cifar_predict_from_pd.py: load_graph(.pb) + feed-dict run of
 `predictions` on 100 standardized test images).
 
-    python resnet_cifar_predict_from_pd.py --frozen model.safetensors [--eval_data_path DIR]
+    python resnet_cifar_predict_from_pd.py --frozen resnet50_cifar_frozen_model_eval.pb \
+        [--eval_data_path DIR] [--device auto|gpu|cpu|interp]
+
+Any frozen ResNet v2 GraphDef works -- ours (resnet_cifar_frozen_model.py) or
+TensorFlow's, e.g. the reference's test/resnet50-cifar-ckpt-20190218/
+resnet50_cifar_frozen_model_eval.pb.  `--device interp` runs the graph itself
+op by op (utils/tf_interp.py); the other devices load its weights into our
+GPU inference plan or CPU model.
 """
 import argparse
 import os
@@ -21,7 +28,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--frozen", required=True)
     ap.add_argument("--eval_data_path", default="")
-    ap.add_argument("--device", default="auto")
+    ap.add_argument("--device", default="auto", choices=("auto", "gpu", "cpu", "interp"))
     a = ap.parse_args(argv)
     from distributed_tensorflow_resnet_amd.utils.frozen import read_frozen
 

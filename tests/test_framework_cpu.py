@@ -186,11 +186,15 @@ def test_driver_train_resume_eval_cpu(tmp_path):
     # tools on the produced checkpoint
     r = run(["tf_saver.py", "--checkpoint_dir", td, "--restore", "--resnet_size", "8"])
     assert r.returncode == 0 and "dense/bias" in r.stdout, r.stderr[-2000:]
-    fz = str(tmp_path / "frozen.safetensors")
+    fz = str(tmp_path / "frozen.pb")
     r = run(["resnet_cifar_frozen_model.py", "--train_dir", td, "--output", fz, "--resnet_size",
              "8", "--eval_data_path", root, "--device", "cpu"])
     assert r.returncode == 0 and "precision:" in r.stdout, r.stderr[-2000:]
-    assert os.path.exists(fz)
+    p_cpu = r.stdout.split("predictions:")[1].splitlines()[0]
+    r = run(["resnet_cifar_predict_from_pd.py", "--frozen", fz, "--eval_data_path", root,
+             "--device", "interp"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split("predictions:")[1].splitlines()[0] == p_cpu   # graph == our model
 
 
 def test_resnet_single_config1():

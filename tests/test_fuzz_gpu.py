@@ -106,4 +106,4 @@ def test_fuzz_bn_stat_accumulators(gpu, shape, shifted):
     yf = y.float().reshape(M, K)
     var = yf.var(0, unbiased=False)
     assert _rel(mean, yf.mean(0)) < 1e-4, shape
-    assert _rel(1.0 / rstd ** 2 - 1e-5, var) < 1e-3, shape
+    assert _rel(1.0 / rstd ** 2 - 1.001e-5, var) < 1e-3, shape
