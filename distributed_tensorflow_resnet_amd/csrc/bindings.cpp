@@ -16,11 +16,16 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "comm.h"
@@ -482,6 +487,64 @@ struct PlanOp {
   int ev;          // event index (record / wait), timing-event index (OP_TIMING)
 };
 
+// One host thread per stream (Plan::run, threaded mode).  hipLaunchKernel costs
+// ~3 us of host time; issued from one thread, the side stream's weight-gradient
+// launches sit between the main stream's dgrad launches, and at small batch
+// (CIFAR, 16-32 images per rank) the main stream drains while the host is busy
+// with the side stream (rocprofv3 timeline: ~35 us main-stream gaps every two
+// residual blocks).  Each stream's ops are instead issued, in plan order, by its
+// own thread; a cross-stream wait is issued only once the matching record has
+// been issued in THIS run (per-op generation stamps), so the device-side
+// fork/join graph is exactly the single-threaded one.
+struct IssueWorker {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool has_job = false, quit = false, done = true;
+  IssueWorker() {
+    th = std::thread([this] {
+      for (;;) {
+        std::function<void()> j;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [this] { return has_job || quit; });
+          if (quit) return;
+          j = std::move(job);
+          has_job = false;
+        }
+        j();
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done = true;
+        }
+        cv.notify_all();
+      }
+    });
+  }
+  void start(std::function<void()> j) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = std::move(j);
+      has_job = true;
+      done = false;
+    }
+    cv.notify_all();
+  }
+  void join() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return done; });
+  }
+  ~IssueWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+    }
+    cv.notify_all();
+    if (th.joinable()) th.join();
+  }
+};
+
 struct Plan {
   std::vector<PlanOp> ops;
   std::vector<std::string> names;
@@ -491,8 +554,19 @@ struct Plan {
   std::vector<double> host_us;   // per-op host issue time (profile mode only)
   bool profile = false;
   bool timing = false;           // OP_TIMING ops record only when enabled
+  int threaded = -1;             // -1: DTR_PLAN_THREADS (default 1); 0 / 1
   int cur = 0;
+  // threaded issue state
+  std::unique_ptr<IssueWorker> workers[PLAN_STREAMS];
+  std::unique_ptr<std::atomic<unsigned>[]> stamp;   // generation at which op i was issued
+  size_t stamp_n = 0;
+  std::vector<int> rec_of;       // WAIT op -> latest RECORD op of its event before it (-1)
+  size_t rec_of_n = 0;
+  unsigned gen = 0;
+  std::atomic<bool> abort_run{false};
+
   ~Plan() {
+    for (auto& w : workers) w.reset();
     for (auto e : events) (void)hipEventDestroy(e);
     for (auto e : tevents) (void)hipEventDestroy(e);
   }
@@ -540,32 +614,118 @@ struct Plan {
       throw std::runtime_error(std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
     return ms;
   }
+
+  hipError_t issue(int i, hipStream_t s) {
+    const PlanOp& o = ops[i];
+    if (o.kind == OP_LAUNCH) {
+      o.fn(s);
+      return hipSuccess;
+    }
+    if (o.kind == OP_RECORD) return hipEventRecord(events[o.ev], s);
+    if (o.kind == OP_WAIT) return hipStreamWaitEvent(s, events[o.ev], 0);
+    if (timing) return hipEventRecord(tevents[o.ev], s);
+    return hipSuccess;
+  }
+
+  bool use_threads(int begin, int end) {
+    if (threaded < 0) {
+      const char* e = std::getenv("DTR_PLAN_THREADS");
+      threaded = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    if (!threaded || profile) return false;
+    bool multi = false;
+    for (int i = begin; i < end && !multi; ++i) multi = ops[i].stream != ops[begin].stream;
+    return multi;
+  }
+
+  void prepare_threads() {
+    if (stamp_n != ops.size()) {
+      stamp.reset(new std::atomic<unsigned>[ops.size()]);
+      for (size_t i = 0; i < ops.size(); ++i) stamp[i].store(0u);
+      stamp_n = ops.size();
+    }
+    if (rec_of_n != ops.size()) {
+      rec_of.assign(ops.size(), -1);
+      std::vector<int> last(events.size(), -1);
+      for (size_t i = 0; i < ops.size(); ++i) {
+        if (ops[i].kind == OP_RECORD) last[ops[i].ev] = (int)i;
+        else if (ops[i].kind == OP_WAIT) rec_of[i] = last[ops[i].ev];
+      }
+      rec_of_n = ops.size();
+    }
+    for (int s = 1; s < PLAN_STREAMS; ++s)
+      if (!workers[s]) workers[s].reset(new IssueWorker());
+  }
+
+  // Issue stream `sid`'s ops of [begin, end) in order; returns the first failure.
+  std::pair<int, hipError_t> issue_stream(int sid, int begin, int end, hipStream_t s, unsigned g) {
+    if (sid != 0) {   // the current device is per host thread: use the stream's
+      int dev = -1, curdev = -1;
+      if (hipStreamGetDevice(s, &dev) == hipSuccess && hipGetDevice(&curdev) == hipSuccess &&
+          dev >= 0 && dev != curdev)
+        (void)hipSetDevice(dev);
+    }
+    for (int i = begin; i < end; ++i) {
+      if (ops[i].stream != sid) continue;
+      if (ops[i].kind == OP_WAIT) {
+        const int r = rec_of[i];
+        if (r >= begin) {   // recorded in this range: wait until it is issued in this run
+          unsigned spins = 0;
+          while (stamp[r].load(std::memory_order_acquire) != g) {
+            if (abort_run.load(std::memory_order_relaxed)) return {i, hipErrorUnknown};
+            if (++spins > 64) std::this_thread::yield();
+          }
+        }
+      }
+      hipError_t e = issue(i, s);
+      if (e == hipSuccess && ops[i].kind == OP_LAUNCH) e = hipGetLastError();  // per thread
+      if (e != hipSuccess) {
+        abort_run.store(true);
+        return {i, e};
+      }
+      stamp[i].store(g, std::memory_order_release);
+    }
+    return {-1, hipSuccess};
+  }
+
   void run(int begin, int end, ptr_t main_stream, ptr_t side_stream, ptr_t comm_stream) {
     if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
     hipStream_t st[PLAN_STREAMS] = {S(main_stream), S(side_stream ? side_stream : main_stream),
                                     S(comm_stream ? comm_stream : main_stream)};
     int bad_op = -1;
     hipError_t bad = hipSuccess;
-    {
+    if (use_threads(begin, end) && st[1] != st[0] && st[2] != st[0] && st[1] != st[2]) {
+      py::gil_scoped_release nogil;
+      prepare_threads();
+      const unsigned g = ++gen == 0 ? ++gen : gen;   // 0 = never issued
+      abort_run.store(false);
+      std::pair<int, hipError_t> res[PLAN_STREAMS];
+      bool used[PLAN_STREAMS] = {false, false, false};
+      for (int i = begin; i < end; ++i) used[ops[i].stream] = true;
+      for (int sid = 1; sid < PLAN_STREAMS; ++sid) {
+        res[sid] = {-1, hipSuccess};
+        if (used[sid])
+          workers[sid]->start([this, sid, begin, end, &st, g, &res] {
+            res[sid] = issue_stream(sid, begin, end, st[sid], g);
+          });
+      }
+      res[0] = issue_stream(0, begin, end, st[0], g);
+      for (int sid = 1; sid < PLAN_STREAMS; ++sid)
+        if (used[sid]) workers[sid]->join();
+      for (auto& r : res)
+        if (r.second != hipSuccess && (bad_op < 0 || r.first < bad_op)) {
+          bad_op = r.first;
+          bad = r.second;
+        }
+    } else {
       py::gil_scoped_release nogil;
       if (profile && host_us.size() != ops.size()) host_us.assign(ops.size(), 0.0);
       for (int i = begin; i < end; ++i) {
-        const PlanOp& o = ops[i];
-        hipStream_t s = st[o.stream];
         const auto t0 = profile ? std::chrono::steady_clock::now()
                                 : std::chrono::steady_clock::time_point();
-        hipError_t e = hipSuccess;
-        if (o.kind == OP_LAUNCH) {
-          o.fn(s);
-        } else if (o.kind == OP_RECORD) {
-          e = hipEventRecord(events[o.ev], s);
-        } else if (o.kind == OP_WAIT) {
-          e = hipStreamWaitEvent(s, events[o.ev], 0);
-        } else if (timing) {
-          e = hipEventRecord(tevents[o.ev], s);
-        }
         // A failed record/wait silently drops a fork or join the stream check
         // certified: remember the first failure and stop issuing.
+        const hipError_t e = issue(i, st[ops[i].stream]);
         if (e != hipSuccess) {
           bad_op = i;
           bad = e;
@@ -632,6 +792,7 @@ PYBIND11_MODULE(_C, m) {
       .def("current_stream", [](const Plan& p) { return p.cur; })
       .def("timing_point", &Plan::timing_point)
       .def("set_timing", [](Plan& p, bool on) { p.timing = on; })
+      .def("set_threaded", [](Plan& p, bool on) { p.threaded = on ? 1 : 0; })
       .def("elapsed_ms", &Plan::elapsed_ms)
       // in-place SUM all-reduce of `count` elements at `ptr` on the plan's current
       // stream through the native RCCL communicator (dtype: 7 fp32, 9 bf16)

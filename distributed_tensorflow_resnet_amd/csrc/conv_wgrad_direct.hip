@@ -195,6 +195,32 @@ static int g_wgd_enabled = -1;
 
 void set_wgrad_direct(int enabled) { g_wgd_enabled = enabled ? 1 : 0; }
 
+// Workgroups the direct kernel should at least launch (DTR_WGD_TARGET, default
+// 96): below it the tile shrinks (fewer pixels per split, then fewer taps per
+// workgroup).  At 16-32 images per rank (the 8-GPU strong-scaling share of the
+// global batch 128) the bs128-tuned tiles left 12-32 workgroups per stage-3/2
+// wgrad, ~10 us each, and the side stream became the backward's critical path.
+static int wgd_target() {
+  static int t = -1;
+  if (t < 0) {
+    const char* e = std::getenv("DTR_WGD_TARGET");
+    t = e ? std::atoi(e) : 96;
+  }
+  return t;
+}
+
+// smallest pixel tile instantiated per channel count
+static int wgd_min_bmp(int C) { return C == 16 ? 128 : 64; }
+
+// Taps per workgroup for this tile: the bs128 default (9 for C 16, 3 otherwise),
+// or 1 when even the smallest tile leaves fewer workgroups than the target.
+static int wgd_taps(const ConvGeom& g, int bmp) {
+  const long P = (long)g.N * g.H * g.W;
+  const int tj = g.C == 16 ? 9 : 3;
+  if (g.C != 16 && bmp == wgd_min_bmp(g.C) && (P / bmp) * (9 / tj) < wgd_target()) return 1;
+  return tj;
+}
+
 // Pixels per split of the direct kernel for this conv, 0 if not covered.
 int wgrad_direct_bmp(const ConvGeom& g) {
   if (g_wgd_enabled < 0) {
@@ -219,11 +245,13 @@ int wgrad_direct_bmp(const ConvGeom& g) {
   else if (g.C == 32 && g.W == 16) bmp = bm32;
   else if (g.C == 64 && g.W == 8) bmp = bm64;
   const long P = (long)g.N * g.H * g.W;
-  const int lo = g.C == 64 ? 128 : 256;          // smallest instantiated tile
+  const int lo = wgd_min_bmp(g.C);               // smallest instantiated tile
   const int hi = g.C == 16 ? 1024 : g.C == 32 ? 512 : 256;
   if (bmp < lo || bmp > hi || (bmp & (bmp - 1))) return 0;
   while (bmp > lo && P % bmp != 0) bmp >>= 1;     // the largest tile that divides P
   if (P % bmp != 0) return 0;
+  const int tj0 = g.C == 16 ? 9 : 3;
+  while (bmp > lo && (P / bmp) * (9 / tj0) < wgd_target() && P % (bmp >> 1) == 0) bmp >>= 1;
   return bmp;
 }
 
@@ -231,16 +259,23 @@ bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) {
   const int bmp = wgrad_direct_bmp(a.g);
   if (bmp == 0 || a.px_per_split != bmp) return false;
   const ConvGeom& g = a.g;
+  const int tj = wgd_taps(g, bmp);
   if (g.C == 16) {
     if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s);
     else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s);
-    else wgd_launch<16, 32, 32, 256, 9>(a, s);
+    else if (bmp == 256) wgd_launch<16, 32, 32, 256, 9>(a, s);
+    else wgd_launch<16, 32, 32, 128, 9>(a, s);
   } else if (g.C == 32) {
     if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s);
-    else wgd_launch<32, 16, 16, 256, 3>(a, s);
+    else if (bmp == 256) wgd_launch<32, 16, 16, 256, 3>(a, s);
+    else if (bmp == 128) wgd_launch<32, 16, 16, 128, 3>(a, s);
+    else if (tj == 3) wgd_launch<32, 16, 16, 64, 3>(a, s);
+    else wgd_launch<32, 16, 16, 64, 1>(a, s);
   } else {
     if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s);
-    else wgd_launch<64, 8, 8, 128, 3>(a, s);
+    else if (bmp == 128) wgd_launch<64, 8, 8, 128, 3>(a, s);
+    else if (tj == 3) wgd_launch<64, 8, 8, 64, 3>(a, s);
+    else wgd_launch<64, 8, 8, 64, 1>(a, s);
   }
   return true;
 }
