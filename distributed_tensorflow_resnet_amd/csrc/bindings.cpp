@@ -455,6 +455,16 @@ static Launch mk_cifar_augment(ptr_t img, ptr_t out, int N, int H, int W, int Cp
   };
 }
 
+static Launch mk_imagenet_u8_pack(ptr_t img, ptr_t out, int N, int H, int W,
+                                  unsigned long long seed, ptr_t gstep, int train, ptr_t zero,
+                                  long zero_bytes) {
+  if (zero_bytes % 16) throw std::invalid_argument("imagenet_u8_pack: zero_bytes % 16 != 0");
+  return [=](hipStream_t s) {
+    imagenet_u8_pack(P<const uint8_t>(img), P<bf16>(out), N, H, W, seed,
+                     P<const long long>(gstep), train, P<void>(zero), zero_bytes, s);
+  };
+}
+
 static Launch mk_pad_channels(ptr_t x, ptr_t out, long npix, int C, int Cpad) {
   return [=](hipStream_t s) { nhwc_pad_channels(P<const float>(x), P<bf16>(out), npix, C, Cpad, s); };
 }
@@ -886,6 +896,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "fill", mk_fill);
   def_op(m, plan, "memset", mk_memset);
   def_op(m, plan, "cifar_augment", mk_cifar_augment);
+  def_op(m, plan, "imagenet_u8_pack", mk_imagenet_u8_pack);
   def_op(m, plan, "pad_channels", mk_pad_channels);
   def_op(m, plan, "synthetic_images", mk_synthetic);
   def_op(m, plan, "cast_f32_bf16", mk_cast_f2b);

@@ -233,7 +233,12 @@ template <int BM, int BN, int WM, int WN, int FLAGS, bool XO = false>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                               char* smem, const int m0, const int n0,
-                                              const EpiPre<BM, BN, WM, XO>* pre = nullptr) {
+                                              const EpiPre<BM, BN, WM, XO>* pre = nullptr,
+                                              int tile_m = -1, int tile_n = -1) {
+  // (tile_m, tile_n): this workgroup's logical tile when the kernel remaps blockIdx
+  // (XCD swizzle, conv_gemm.hip); -1 = blockIdx.x / blockIdx.y.
+  if (tile_m < 0) tile_m = blockIdx.x;
+  if (tile_n < 0) tile_n = blockIdx.y;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -473,7 +478,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
 
   if constexpr (STATS) {
     if (tid < BN && n0 + tid < NC) {
-      float* tile_out = args.stat_part + (long)blockIdx.x * 2 * NC;
+      float* tile_out = args.stat_part + (long)tile_m * 2 * NC;
       if (args.stat_acc != nullptr) {       // accumulator mode: sum y, sum y^2 of the tile
         const double n = wn_run, mu = wmean_run;
         bn_acc_add(args.stat_acc, NC, n0 + tid, n * mu, (double)wm2_run + n * mu * mu);
@@ -492,13 +497,13 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       bool last;
       float fn_ = 0.f, fmu = 0.f, fm2 = 0.f;
       if (F.group == 0) {          // single level: combine every tile
-        last = last_arriver(F.counters + blockIdx.y, T, flag);
+        last = last_arriver(F.counters + tile_n, T, flag);
         if (last) welford_combine<BN>(args.stat_part, NC, n0, 0, T, BM, M, red, red2, cs,
                                       fn_, fmu, fm2);
       } else {                     // two levels: groups of F.group tiles, then the groups
-        const int GS = F.group, ng = (T + GS - 1) / GS, gi = blockIdx.x / GS;
+        const int GS = F.group, ng = (T + GS - 1) / GS, gi = tile_m / GS;
         const int gsize = min(GS, T - gi * GS);
-        last = last_arriver(F.counters + gridDim.y + blockIdx.y * ng + gi, gsize, flag);
+        last = last_arriver(F.counters + gridDim.y + tile_n * ng + gi, gsize, flag);
         if (last) {
           welford_combine<BN>(args.stat_part, NC, n0, gi * GS, gsize, BM, M - gi * GS * BM,
                               red, red2, cs, fn_, fmu, fm2);
@@ -506,11 +511,11 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
             publish_f32(F.gpart + (long)gi * 2 * NC + n0 + tid, fmu);
             publish_f32(F.gpart + (long)gi * 2 * NC + NC + n0 + tid, fm2);
           }
-          reset_counter(F.counters + gridDim.y + blockIdx.y * ng + gi);
+          reset_counter(F.counters + gridDim.y + tile_n * ng + gi);
           if (F.groups_only) {
             last = false;   // a consumer's BnPreFin combines the group partials
           } else {
-            last = last_arriver(F.counters + blockIdx.y, ng, flag);
+            last = last_arriver(F.counters + tile_n, ng, flag);
             if (last) welford_combine<BN>(F.gpart, NC, n0, 0, ng, GS * BM, M, red, red2, cs,
                                           fn_, fmu, fm2);
           }
@@ -532,14 +537,14 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
             F.mvar[col] -= (1.f - F.momentum) * (F.mvar[col] - uvar);
           }
         }
-        reset_counter(F.counters + blockIdx.y);
+        reset_counter(F.counters + tile_n);
       }
     }
   }
   if constexpr (BNB) {
     if (tid < BN && n0 + tid < NC) {
       const float t1 = bnb_t1, t2 = bnb_t2;
-      float* tile_out = args.bnb_part + (long)blockIdx.x * 2 * NC;
+      float* tile_out = args.bnb_part + (long)tile_m * 2 * NC;
       if (args.bnb_acc != nullptr) {        // accumulator mode
         bn_acc_add(args.bnb_acc, NC, n0 + tid, (double)t1, (double)t2);
       } else if (args.bfin.counters != nullptr) {
@@ -557,23 +562,23 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       bool last;
       float sg = 0.f, sgx = 0.f;
       if (F.group == 0) {
-        last = last_arriver(F.counters + blockIdx.y, T, flag);
+        last = last_arriver(F.counters + tile_n, T, flag);
         if (last) sum_combine<BN>(args.bnb_part, NC, n0, 0, T, red, red2, sg, sgx);
       } else {
-        const int GS = F.group, ng = (T + GS - 1) / GS, gi = blockIdx.x / GS;
+        const int GS = F.group, ng = (T + GS - 1) / GS, gi = tile_m / GS;
         const int gsize = min(GS, T - gi * GS);
-        last = last_arriver(F.counters + gridDim.y + blockIdx.y * ng + gi, gsize, flag);
+        last = last_arriver(F.counters + gridDim.y + tile_n * ng + gi, gsize, flag);
         if (last) {
           sum_combine<BN>(args.bnb_part, NC, n0, gi * GS, gsize, red, red2, sg, sgx);
           if (tid < BN && n0 + tid < NC) {
             publish_f32(F.gpart + (long)gi * 2 * NC + n0 + tid, sg);
             publish_f32(F.gpart + (long)gi * 2 * NC + NC + n0 + tid, sgx);
           }
-          reset_counter(F.counters + gridDim.y + blockIdx.y * ng + gi);
+          reset_counter(F.counters + gridDim.y + tile_n * ng + gi);
           if (F.groups_only) {
             last = false;   // the consumer dgrad's BnBwdPre combines the group sums
           } else {
-            last = last_arriver(F.counters + blockIdx.y, ng, flag);
+            last = last_arriver(F.counters + tile_n, ng, flag);
             if (last) sum_combine<BN>(F.gpart, NC, n0, 0, ng, red, red2, sg, sgx);
           }
         }
@@ -588,7 +593,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
           F.coef[NC + col] = a * sg / (float)M;
           F.coef[2 * NC + col] = a * sgx / (float)M;
         }
-        reset_counter(F.counters + blockIdx.y);
+        reset_counter(F.counters + tile_n);
       }
     }
   }

@@ -80,8 +80,22 @@ conv_gemm_kernel(GemmArgs args) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // Tile order.  Workgroups are dispatched x-fastest and dealt round-robin to the 8
+  // XCDs, each with its own L2; with `swz` the logical tile of linear id L is
+  // chunk (L % 8) of the tile list, walked N-fastest, so the workgroups resident on
+  // one XCD at a time cover a few A row blocks with ALL their column tiles (A read
+  // once per XCD from HBM instead of once per column tile).
+  int tm = blockIdx.x, tn = blockIdx.y;
+  if (args.swz) {
+    const int TMn = gridDim.x, TNn = gridDim.y;
+    const int L = blockIdx.x + TMn * blockIdx.y;
+    const int full = (TMn * TNn) & ~7;
+    const int lg = L < full ? (L & 7) * (full >> 3) + (L >> 3) : L;
+    tm = lg / TNn;
+    tn = lg - tm * TNn;
+  }
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
 
   // Input-channel count of the A operand's gather (C for fwd, K for dgrad).
   const int Acin = (MODE == MODE_FWD) ? g.C : g.K;
@@ -460,9 +474,9 @@ conv_gemm_kernel(GemmArgs args) {
   }
 
   if constexpr (BNB && EP::ON)
-    conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre);
+    conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre, tm, tn);
   else
-    conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0);
+    conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0, nullptr, tm, tn);
 }
 
 // ---------------------------------------------------------------------------
@@ -497,9 +511,17 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   return mode == MODE_FWD ? a.Ncol >= 128 : a.M >= 16384;
 }
 
+static int g_xcd_swz = -1;   // DTR_XCD_SWZ: 0 off, 1 on (default: see launch_cfg)
+
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>
-static void launch_cfg(const GemmArgs& a, hipStream_t s) {
+static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   constexpr int NBUF = 2;   // 1 measured neutral on the ImageNet 128x128 tiles
+  if (g_xcd_swz < 0) {
+    const char* e = std::getenv("DTR_XCD_SWZ");
+    g_xcd_swz = e ? std::atoi(e) : 0;
+  }
+  GemmArgs a = a0;
+  a.swz = (g_xcd_swz && (a.Ncol + BN - 1) / BN > 1) ? 1 : 0;
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)NBUF * (BM + BN) * 64 * sizeof(bf16);
   if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);

@@ -7,6 +7,9 @@ namespace dtr {
 void cifar_augment(const uint8_t* img, bf16* out, int N, int H, int W, int Cpad, int pad,
                    unsigned long long seed, const long long* gstep, int train, int* crop_log,
                    void* zero, long zero_bytes, hipStream_t s);   // zero: optional buffer to clear
+void imagenet_u8_pack(const uint8_t* img, bf16* out, int N, int H, int W,
+                      unsigned long long seed, const long long* gstep, int train, void* zero,
+                      long zero_bytes, hipStream_t s);   // uint8 HWC crops -> bf16 NHWC-8
 void nhwc_pad_channels(const float* x, bf16* out, long npix, int C, int Cpad, hipStream_t s);
 void synthetic_images(bf16* out, long npix, int C, int Cpad, unsigned long long seed,
                       hipStream_t s);

@@ -220,3 +220,55 @@ void synthetic_images(bf16* out, long npix, int C, int Cpad, unsigned long long 
 }
 
 }  // namespace dtr
+
+namespace dtr {
+
+// ImageNet real-data feed (resnet_imagenet_main.py:122-192 with VGG preprocessing,
+// vgg_preprocessing.py:284-333): CPU workers decode the JPEG, do the
+// aspect-preserving resize and the random (train) / central (eval) 224x224 crop
+// and ship the crop as uint8 HWC -- 4x fewer host->device bytes than float32.
+// This kernel does the rest on the device: the random left-right flip (hash of
+// (seed, global_step, image), like cifar_augment), the per-channel mean
+// subtraction (R,G,B = 123.68, 116.78, 103.94, vgg_preprocessing.py:37-39) and the
+// bf16 NHWC packing with the channel dim padded to 8 (one 16-B row per pixel,
+// the stem conv's operand layout).  Optionally clears a buffer in the same launch
+// (the step's BatchNorm accumulators).  One thread per output pixel.
+__global__ void __launch_bounds__(256)
+imagenet_u8_pack_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int H, int W,
+                        unsigned long long seed, const long long* gstep, int train,
+                        uint4* __restrict__ zero, long zero_vec, long npix) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < zero_vec; i += (long)gridDim.x * 256)
+    zero[i] = make_uint4(0u, 0u, 0u, 0u);
+  const long p = blockIdx.x * 256L + threadIdx.x;
+  if (p >= npix) return;
+  const long HW = (long)H * W;
+  const long n = p / HW;
+  const int rem = (int)(p - n * HW);
+  const int y = rem / W, x = rem - y * W;
+  int flip = 0;
+  if (train) {
+    const unsigned long long step = gstep ? (unsigned long long)*gstep : 0ull;
+    flip = (int)((splitmix(seed ^ splitmix(step * 0x100000001B3ull + (unsigned long long)n)) >> 32) & 1);
+  }
+  const int xs = flip ? W - 1 - x : x;
+  const uint8_t* src = img + ((n * H + y) * (long)W + xs) * 3;
+  bf16x8 r = {};
+  r[0] = (bf16)((float)src[0] - 123.68f);
+  r[1] = (bf16)((float)src[1] - 116.78f);
+  r[2] = (bf16)((float)src[2] - 103.94f);
+  *reinterpret_cast<bf16x8*>(out + p * 8) = r;
+}
+
+void imagenet_u8_pack(const uint8_t* img, bf16* out, int N, int H, int W,
+                      unsigned long long seed, const long long* gstep, int train, void* zero,
+                      long zero_bytes, hipStream_t s) {
+  if (zero_bytes % 16 != 0) throw std::invalid_argument("imagenet_u8_pack: zero_bytes % 16");
+  const long npix = (long)N * H * W;
+  const int grid = (int)((npix + 255) / 256);
+  hipLaunchKernelGGL(imagenet_u8_pack_kernel, dim3(grid), dim3(256), 0, s, img, out, H, W, seed,
+                     gstep, train, reinterpret_cast<uint4*>(zero), zero ? zero_bytes / 16 : 0,
+                     npix);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

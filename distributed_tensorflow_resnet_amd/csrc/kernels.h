@@ -126,6 +126,7 @@ struct GemmArgs {
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;
+  int swz = 0;              // conv_gemm: XCD-grouped tile order (set by the launcher)
 };
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);

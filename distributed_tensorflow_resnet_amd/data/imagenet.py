@@ -33,14 +33,19 @@ def filenames(is_training: bool, data_dir: str) -> list[str]:
 
 
 def record_parser(raw: bytes, is_training: bool, rng=None, label_offset: int = 1,
-                  image_size: int = 224):
-    """-> (float32 HWC image, int label)."""
+                  image_size: int = 224, u8: bool = False):
+    """-> (float32 HWC image, int label); u8=True: the uint8 HWC crop for the GPU feed
+    (flip + mean subtraction left to imagenet_u8_pack on the device)."""
     from PIL import Image
 
     ex = parse_example(raw)
     jpeg = ex["image/encoded"][0]
     label = int(ex["image/class/label"][0]) - label_offset
-    img = Image.open(io.BytesIO(jpeg)).convert("RGB")
+    img = Image.open(io.BytesIO(jpeg))
+    img.draft("RGB", (image_size * 2, image_size * 2))   # JPEG DCT-domain downscale when large
+    img = img.convert("RGB")
+    if u8:
+        return vgg.crop_u8(img, image_size, image_size, is_training, rng=rng), label
     x = vgg.preprocess_image(img, image_size, image_size, is_training, rng=rng)
     return x.astype(np.float32), label
 
@@ -49,7 +54,7 @@ class TFRecordImages(torch.utils.data.IterableDataset):
     """Streams records of the shards assigned to (rank, dataloader worker)."""
 
     def __init__(self, files, is_training, rank=0, world=1, seed=0, label_offset=1,
-                 image_size=224, shuffle_buffer=1024):
+                 image_size=224, shuffle_buffer=1024, u8=False):
         self.files = [f for f in files if os.path.exists(f)]
         if not self.files:
             raise FileNotFoundError(f"no TFRecord shards found (e.g. {files[:1]})")
@@ -59,6 +64,7 @@ class TFRecordImages(torch.utils.data.IterableDataset):
         self.label_offset = label_offset
         self.image_size = image_size
         self.shuffle_buffer = shuffle_buffer
+        self.u8 = u8
 
     def __iter__(self):
         wi = torch.utils.data.get_worker_info()
@@ -72,7 +78,7 @@ class TFRecordImages(torch.utils.data.IterableDataset):
         for f in mine:
             for raw in read_records(f):
                 item = record_parser(raw, self.is_training, rng, self.label_offset,
-                                     self.image_size)
+                                     self.image_size, self.u8)
                 if not self.is_training:
                     yield item
                     continue
@@ -84,15 +90,17 @@ class TFRecordImages(torch.utils.data.IterableDataset):
 
 
 def input_fn(is_training, data_dir, batch_size, num_epochs=1, rank=0, world=1, workers=5, seed=0,
-             label_offset=1, image_size=224):
-    """Yields (float NHWC [B,224,224,3], int64 [B]) for num_epochs passes."""
+             label_offset=1, image_size=224, u8=False, pin_memory=False):
+    """Yields (NHWC [B,224,224,3], int64 [B]) for num_epochs passes: float32 VGG-
+    preprocessed, or (u8=True) uint8 crops for the device-side flip/mean/pack."""
     ds = TFRecordImages(filenames(is_training, data_dir), is_training, rank, world, seed,
-                        label_offset, image_size)
+                        label_offset, image_size, u8=u8)
     for ep in range(num_epochs):
         ds.seed = seed + ep
         dl = torch.utils.data.DataLoader(ds, batch_size=batch_size, num_workers=workers,
-                                         drop_last=is_training,
-                                         collate_fn=_collate, persistent_workers=False)
+                                         drop_last=is_training, pin_memory=pin_memory,
+                                         collate_fn=_collate, persistent_workers=False,
+                                         prefetch_factor=4 if workers else None)
         yield from dl
 
 

@@ -71,6 +71,40 @@ def preprocess_for_eval(img, out_h=224, out_w=224, resize_side=_RESIZE_SIDE_MIN)
     return mean_image_subtraction(np.ascontiguousarray(x))
 
 
+def crop_u8(img, out_h=224, out_w=224, is_training=False, resize_side_min=_RESIZE_SIDE_MIN,
+            resize_side_max=_RESIZE_SIDE_MAX, rng=None) -> np.ndarray:
+    """The CPU half of preprocess_image for the GPU feed: aspect-preserving resize +
+    random (train) / central (eval) crop, returned as uint8 HWC.  The random flip
+    and the mean subtraction run on the device (imagenet_u8_pack, csrc/data.hip),
+    so the host ships 1 byte per value instead of 4."""
+    from PIL import Image
+
+    pil = img if isinstance(img, Image.Image) else Image.fromarray(np.asarray(img, dtype=np.uint8))
+    pil = pil.convert("RGB")
+    w, h = pil.size
+    if is_training:
+        rng = rng or np.random.default_rng()
+        side = int(rng.integers(resize_side_min, resize_side_max + 1))
+    else:
+        side = resize_side_min
+    nh, nw = smallest_size_at_least(h, w, side)
+    if nh < out_h or nw < out_w:
+        raise ValueError("Crop size greater than the image size.")
+    if is_training:   # the same draws as random_crop on the resized image
+        oy = int(rng.integers(0, nh - out_h + 1))
+        ox = int(rng.integers(0, nw - out_w + 1))
+    else:
+        oy, ox = (nh - out_h) // 2, (nw - out_w) // 2
+    # resize only the crop's source window: PIL samples output pixel i of the box at
+    # box0 + (i + 0.5) * scale - 0.5 with the full-image filter support, i.e. exactly
+    # pixel ox + i of the resized image (tests/test_framework_cpu.py), at a fraction
+    # of the work (224x224 instead of up to 512x683 resized pixels)
+    sx, sy = w / nw, h / nh
+    box = (ox * sx, oy * sy, (ox + out_w) * sx, (oy + out_h) * sy)
+    x = np.asarray(pil.resize((out_w, out_h), Image.BILINEAR, box=box), dtype=np.uint8)
+    return np.ascontiguousarray(x)
+
+
 def preprocess_image(image, output_height, output_width, is_training=False,
                      resize_side_min=_RESIZE_SIDE_MIN, resize_side_max=_RESIZE_SIDE_MAX, rng=None):
     """vgg_preprocessing.preprocess_image (vgg_preprocessing.py:336-363)."""

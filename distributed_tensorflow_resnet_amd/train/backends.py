@@ -40,10 +40,10 @@ class GPUBackend:
     def set_batch(self, images, labels):
         self.engine.set_batch(images, labels)
 
-    def step(self):
+    def step(self, need_cost: bool = False):
         eng = self.engine
         if self.profile_phases:
-            self.last_phase_ms = eng.step_timed()
+            self.last_phase_ms = eng.step_timed(need_cost)
         elif self.use_graph:
             # first step eager (initialises RCCL communicators), second step
             # captures the hipGraph (capture executes nothing) and replays it:
@@ -51,10 +51,10 @@ class GPUBackend:
             if self._eager_done and not self._captured:
                 eng.capture(warmup=0)
                 self._captured = True
-            eng.step()
+            eng.step(need_cost)
             self._eager_done = True
         else:
-            eng.step()
+            eng.step(need_cost)
         self._host_step += 1
 
     def metrics(self):
@@ -124,7 +124,7 @@ class CPUBackend:
         self._x = images.float()
         self._y = labels.long()
 
-    def step(self):
+    def step(self, need_cost: bool = False):   # the CPU loss always includes the l2 term
         m = self.model
         master = self.store.master
         if master.grad is not None:

@@ -27,7 +27,7 @@ from ..utils.flags import build_parser, warn_unsupported
 from ..utils.records import EventWriter
 from . import hooks as H
 from .backends import make_backend
-from .engine import cifar_lr_schedule, imagenet_lr_schedule
+from .engine import cifar_lr_schedule, imagenet_lr_schedule, scaled
 from .evaluator import SidecarEvaluator, make_inference
 from .session import TrainingSession, run_training
 
@@ -63,7 +63,7 @@ class Prefetcher:
         return item
 
 
-def _train_batches(flags, spec, rank, world):
+def _train_batches(flags, spec, rank, world, u8=False):
     if flags.synthetic:
         return None
     if spec.dataset.startswith("cifar"):
@@ -76,7 +76,7 @@ def _train_batches(flags, spec, rank, world):
 
     return imagenet.input_fn(True, flags.train_data_path, flags.batch_size,
                              num_epochs=flags.num_epochs, rank=rank, world=world,
-                             workers=flags.num_parallel_calls, seed=flags.seed)
+                             workers=flags.num_parallel_calls, seed=flags.seed, u8=u8)
 
 
 def _eval_batches_factory(flags, spec):
@@ -130,11 +130,15 @@ def main(argv=None, kind: str = "cifar") -> int:
     dp_ctx = None if flags.variable_update == "independent" else ctx
     rank, world = ctx.rank, ctx.world_size
     sched = cifar_lr_schedule() if spec.dataset.startswith("cifar") else imagenet_lr_schedule()
+    sched = scaled(sched, flags.lr_schedule_scale)
+    # real ImageNet on the GPU: uint8 crops from the workers, flip/mean/bf16 pack on device
+    u8 = device == "gpu" and spec.dataset == "imagenet" and not flags.synthetic
     backend = make_backend(spec, flags.batch_size, device=device, weight_decay=flags.weight_decay,
                            lr_schedule=sched, optimizer=flags.optimizer, seed=flags.seed,
                            dist_ctx=dp_ctx, bucket_mb=flags.bucket_mb, use_graph=flags.use_graph,
-                           data_seed=1234 + rank, allreduce_dtype=flags.allreduce_dtype)
-    it = _train_batches(flags, spec, rank, world)
+                           data_seed=1234 + rank, allreduce_dtype=flags.allreduce_dtype,
+                           input_mode="imagenet_u8" if u8 else "auto")
+    it = _train_batches(flags, spec, rank, world, u8=u8)
     feeder = None
     if it is None:
         if device == "gpu":

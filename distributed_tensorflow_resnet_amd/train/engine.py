@@ -94,6 +94,14 @@ def imagenet_lr_schedule() -> LRSchedule:
                       warm_steps=6240, warm_from=0.1, warm_to=0.4)
 
 
+def scaled(s: LRSchedule, factor: float) -> LRSchedule:
+    """The same schedule with its step boundaries (and warm-up length) x factor."""
+    if factor == 1.0:
+        return s
+    return LRSchedule(s.init, [max(1, int(round(b * factor))) for b in s.bounds], list(s.values),
+                      int(round(s.warm_steps * factor)), s.warm_from, s.warm_to)
+
+
 def constant_lr(lr: float) -> LRSchedule:
     return LRSchedule(lr, [], [lr])
 
@@ -251,6 +259,7 @@ class Engine:
             raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
         self.graph = None
         self._captured = False
+        self._steps_run, self._cost_at = 0, -1
         self.eval_plans = {}
         self.repack()
 
@@ -355,6 +364,8 @@ class Engine:
         H, W = spec.image_h, spec.image_w
         if self.input_mode == "cifar_u8":
             self.img_u8 = torch.zeros((N, 3, H, W), dtype=torch.uint8, device=dev)
+        elif self.input_mode == "imagenet_u8":   # VGG crops, HWC (imagenet_u8_pack)
+            self.img_u8 = torch.zeros((N, H, W, 3), dtype=torch.uint8, device=dev)
         self.x_in = torch.zeros((N, H, W, self.cpad_in), dtype=BF16, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
         st = spec.stem
@@ -845,13 +856,16 @@ class Engine:
         # kernel (no extra launch), else by a memset
         zero = (self.bn_acc.data_ptr(), self.bn_acc.numel() * 8) \
             if (self.bn_acc_on or self.bn_bacc_on) else (0, 0)
-        if zero[0] and self.input_mode != "cifar_u8":
+        if zero[0] and self.input_mode not in ("cifar_u8", "imagenet_u8"):
             plan.memset(*zero)
         # ---- input
         if self.input_mode == "cifar_u8":
             plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
                                spec.image_w, self.cpad_in, 4, self.data_seed,
                                self.gstep.data_ptr(), 1, 0, *zero)
+        elif self.input_mode == "imagenet_u8":
+            plan.imagenet_u8_pack(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
+                                  spec.image_w, self.data_seed, self.gstep.data_ptr(), 1, *zero)
         # ---- forward
         stem = self.convs[spec.stem.name]
         blocks = spec.blocks
@@ -944,15 +958,6 @@ class Engine:
         self._side_q, self._side_blocks = [], 0
         # the dense wgrad below runs on the main stream (unless the head is fused)
         self._main_wgrad = self.fork_wgrad and not self._head_fused
-        # 1/2 sum v^2 of the (pre-update) weights for the reported `cost` only: it
-        # rides in the first side-stream batch, off the critical path (ImageNet:
-        # 25.5 M floats, ~80 us on the main stream).
-        l2 = lambda: plan.l2_half_sum(self.params.master.data_ptr(),  # noqa: E731
-                                      self.params.n_train, self.l2_ws.data_ptr(), sp + 12)
-        if self.fork_wgrad:
-            self._side_q.append(l2)
-        else:
-            l2()
         self._pending_bwd, self._bnb_src = None, None
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
@@ -1062,6 +1067,15 @@ class Engine:
                        self.gstep.data_ptr())   # + global_step += 1
         self._t_opt_end = plan.timing_point("opt_end")
         self.seg["opt"] = (b2, plan.size())
+        # 1/2 sum v^2 of the weights, which only feeds the logged `cost`
+        # (resnet_model.py:85-86; the gradient's wd*v is fused into the optimizer):
+        # its own segment, run before the forward of the steps whose metrics are read
+        # (step(need_cost=True); ImageNet RN50: 25.5 M floats, ~0.1 ms per step saved
+        # on every other step).
+        b3 = plan.size()
+        plan.l2_half_sum(self.params.master.data_ptr(), self.params.n_train,
+                         self.l2_ws.data_ptr(), sp + 12)
+        self.seg["cost"] = (b3, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
         assert not missing, f"gradients never produced: {missing[:4]}"
 
@@ -1081,8 +1095,10 @@ class Engine:
         a, b = self.seg[name]
         self.plan.run(a, b, stream, self.side.cuda_stream, self.comm_stream.cuda_stream)
 
-    def _step_eager(self):
+    def _step_eager(self, need_cost: bool = False):
         st = torch.cuda.current_stream().cuda_stream
+        if need_cost:
+            self._run("cost", st)
         if self.markers:
             return self._step_marked(st)
         self._run("fwd", st)
@@ -1131,13 +1147,17 @@ class Engine:
         else:
             self.plan.run(a, b, st, self.side.cuda_stream, self.comm_stream.cuda_stream)
 
-    def step_timed(self) -> dict:
+    def step_timed(self, need_cost: bool = False) -> dict:
         """One eager step with HIP-event timing per phase (ProfilerHook, bench.py):
         forward, backward compute, the exposed all-reduce tail (from the end of
         the backward's compute to the optimizer's join of the last bucket's
         all-reduce; for gloo rehearsals, the host's c10d waits) and the optimizer."""
         st = torch.cuda.current_stream().cuda_stream
         p = self.plan
+        self._steps_run += 1
+        if need_cost:
+            self._run("cost", st)
+            self._cost_at = self._steps_run
         if self.bucket_sched:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
             ev[0].record()
@@ -1192,6 +1212,7 @@ class Engine:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._step_eager()
+                self._steps_run += 1
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -1201,17 +1222,23 @@ class Engine:
         self._captured = True
         return warmup
 
-    def step(self):
-        """One training step (global_step += 1 on the device)."""
+    def step(self, need_cost: bool = False):
+        """One training step (global_step += 1 on the device).  ``need_cost``: also
+        compute 1/2 sum v^2 of this step's (pre-update) weights for the logged cost."""
         if self.graph is not None:
+            if need_cost:
+                self._run("cost", torch.cuda.current_stream().cuda_stream)
             self.graph.replay()
         else:
-            self._step_eager()
+            self._step_eager(need_cost)
+        self._steps_run += 1
+        if need_cost:
+            self._cost_at = self._steps_run
 
     # ------------------------------------------------------------------ io
     def set_batch(self, images, labels):
         """Copy a host/device batch into the static input buffers."""
-        if self.input_mode == "cifar_u8":
+        if self.input_mode in ("cifar_u8", "imagenet_u8"):
             self.img_u8.copy_(images, non_blocking=True)
         else:
             x = images
@@ -1224,7 +1251,7 @@ class Engine:
 
     def fill_synthetic(self, seed: int = 0):
         g = torch.Generator(device="cpu").manual_seed(seed)
-        if self.input_mode == "cifar_u8":
+        if self.input_mode in ("cifar_u8", "imagenet_u8"):
             self.img_u8.copy_(torch.randint(0, 256, tuple(self.img_u8.shape), generator=g,
                                             dtype=torch.uint8))
         else:
@@ -1235,7 +1262,12 @@ class Engine:
                                         dtype=torch.int32))
 
     def metrics(self) -> dict:
-        """Host read of the last step's scalars (synchronises)."""
+        """Host read of the last step's scalars (synchronises).  The `cost` term
+        wd * 1/2 sum v^2 is exact (pre-update weights) when the step ran with
+        need_cost=True; otherwise it is computed now from the updated weights."""
+        if self._cost_at != self._steps_run:
+            self._run("cost", torch.cuda.current_stream().cuda_stream)
+            self._cost_at = self._steps_run
         v = self.scalars.detach().cpu().tolist()
         loss_sum, correct, lr, l2 = v[0], v[1], v[2], v[3]
         if self.dist is not None and self.world > 1:

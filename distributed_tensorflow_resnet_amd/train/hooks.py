@@ -33,8 +33,18 @@ class Hook:
     def after_run(self, session, step: int):
         """`step` = global_step after this run."""
 
+    def wants_metrics(self, session, step: int) -> bool:
+        """Will after_run(step) read session.metrics()?  The session then asks the
+        backend for the exact `cost` of that step (its weight-decay term is only
+        computed on such steps)."""
+        return False
+
     def end(self, session):
         pass
+
+
+def _every(n: int, step: int) -> bool:
+    return n > 0 and step % n == 0
 
 
 def log(msg: str):
@@ -57,6 +67,9 @@ class LoggingTensorHook(Hook):
     def __init__(self, every_n_iter: int = 20, precision_key: str = "precision"):
         self.n = every_n_iter
         self.key = precision_key
+
+    def wants_metrics(self, session, step):
+        return _every(self.n, step) and session.is_chief
 
     def after_run(self, session, step):
         if self.n > 0 and step % self.n == 0 and session.is_chief:
@@ -100,6 +113,9 @@ class SummarySaverHook(Hook):
         self.n = save_steps
         self.tag = precision_tag
 
+    def wants_metrics(self, session, step):
+        return self.writer is not None and _every(self.n, step) and session.is_chief
+
     def after_run(self, session, step):
         if self.writer is not None and self.n > 0 and step % self.n == 0 and session.is_chief:
             m = session.metrics()
@@ -118,6 +134,9 @@ class JsonlMetricsHook(Hook):
     def __init__(self, path: str, every: int = 100):
         self.path = path
         self.n = every
+
+    def wants_metrics(self, session, step):
+        return _every(self.n, step) and session.is_chief
 
     def after_run(self, session, step):
         if self.n > 0 and step % self.n == 0 and session.is_chief:
@@ -177,6 +196,9 @@ class NanGuardHook(Hook):
 
     def __init__(self, every: int = 1):
         self.n = every
+
+    def wants_metrics(self, session, step):
+        return _every(self.n, step)
 
     def after_run(self, session, step):
         if step % self.n == 0:

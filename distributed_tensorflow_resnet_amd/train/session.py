@@ -82,7 +82,8 @@ class TrainingSession:
                 self.request_stop()
                 return
             self.backend.set_batch(images, labels)
-        self.backend.step()
+        nxt = self.global_step + 1
+        self.backend.step(need_cost=any(h.wants_metrics(self, nxt) for h in self.hooks))
         step = self.global_step
         for h in self.hooks:
             h.after_run(self, step)

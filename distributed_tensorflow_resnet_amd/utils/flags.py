@@ -157,6 +157,9 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_argument("--comm_timeout_secs", type=float, default=600.0,
                    help="Collective timeout of the process group (RCCL watchdog aborts the "
                         "communicator after it).")
+    p.add_argument("--lr_schedule_scale", type=float, default=1.0,
+                   help="Multiply the LR schedule's step boundaries (and warm-up) by this "
+                        "factor: compressed schedules for short runs (convergence tests).")
     p.add_argument("--allreduce_dtype", default="fp32", choices=("fp32", "bf16"),
                    help="Gradient all-reduce precision: bf16 halves the bytes on xGMI (fp32 "
                         "master weights and optimizer are unchanged).")

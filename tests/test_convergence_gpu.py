@@ -1,0 +1,69 @@
+"""Convergence proxy: ResNet-20 learns a held-out task on the GPU (bf16 engine)
+as well as the fp32 CPU trainer does.
+
+The reference's accuracy claim (93.3 % / 93.6 % CIFAR-10 "Best Precision",
+README.md:22-28) needs the real CIFAR-10, which is not available offline, so its
+parity stays unpinned.  Instead data/learnable.py writes a 10-class
+CIFAR-shaped task in the CIFAR-10 binary layout (class colour templates under
+random shift / brightness / noise / distractors, 10k train + 2k held-out), and
+both trainers run the full stack the reference runs: resnet_cifar_main.py
+(records -> augmentation -> ResNet-20 v2 -> momentum SGD with wd, the CIFAR LR
+schedule compressed 50x: 0.1 / 0.01 / 0.001 / 1e-4 from steps 800 / 1200 / 1600) and the
+side-car evaluator resnet_cifar_eval.py (Precision / Best_Precision events,
+resnet_cifar_main.py:361-421) on the held-out split."""
+import glob
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from distributed_tensorflow_resnet_amd.data.learnable import make_learnable_cifar
+from distributed_tensorflow_resnet_amd.utils import records
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS = 1600
+
+
+def _train_cmd(device, data, td):
+    return [sys.executable, os.path.join(ROOT, "resnet_cifar_main.py"), "--device", device,
+            "--resnet_size", "20", "--batch_size", "32", "--train_steps", str(STEPS),
+            "--lr_schedule_scale", "0.02", "--train_data_path", data, "--train_dir", td,
+            "--log_every", "400", "--save_checkpoint_steps", str(STEPS)]
+
+
+def _eval(device, data, td, ed):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "resnet_cifar_eval.py"), "--device",
+                        device, "--resnet_size", "20", "--train_dir", td, "--eval_dir", ed,
+                        "--eval_data_path", data, "--eval_once", "--eval_batch_size", "100",
+                        "--eval_batch_count", "20"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, DTR_CPU_THREADS="8"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    m = re.search(r"precision: ([0-9.]+), best precision: ([0-9.]+)", r.stdout)
+    assert m, r.stdout[-2000:]
+    evs = records.read_events(glob.glob(os.path.join(ed, "events.out.tfevents.*"))[0])
+    best = [e for e in evs if "Best_Precision" in e["scalars"]]
+    assert best and best[-1]["step"] == STEPS
+    return float(m.group(1)), best[-1]["scalars"]["Best_Precision"]
+
+
+def test_resnet20_gpu_bf16_matches_cpu_fp32_on_learnable_task(gpu, tmp_path):
+    data = str(tmp_path / "data")
+    make_learnable_cifar(data, 10000, 2000, seed=0)
+    runs = {}
+    env = dict(os.environ, DTR_CPU_THREADS="8")
+    procs = {d: subprocess.Popen(_train_cmd(d, data, str(tmp_path / f"train_{d}")),
+                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                 env=env) for d in ("gpu", "cpu")}
+    for d, p in procs.items():
+        out, _ = p.communicate(timeout=600)
+        assert p.returncode == 0, out[-3000:]
+        print(d, "\n".join(line for line in out.splitlines() if "step =" in line))
+    for d in ("gpu", "cpu"):
+        runs[d] = _eval(d, data, str(tmp_path / f"train_{d}"), str(tmp_path / f"eval_{d}"))
+    print("held-out precision (gpu bf16, cpu fp32):", runs["gpu"], runs["cpu"])
+    assert runs["gpu"][0] >= 0.90 and runs["cpu"][0] >= 0.90, runs
+    assert abs(runs["gpu"][0] - runs["cpu"][0]) <= 0.02, runs
+    assert abs(runs["gpu"][1] - runs["gpu"][0]) < 1e-6   # first evaluation = best so far

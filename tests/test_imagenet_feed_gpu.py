@@ -1,0 +1,59 @@
+"""Real-data ImageNet feed, device half: imagenet_u8_pack (csrc/data.hip) turns
+the workers' uint8 HWC crops into the stem's bf16 NHWC-8 operand with the VGG
+random flip and mean subtraction (vgg_preprocessing.py:37-39, 284-314), and the
+engine's imagenet_u8 input mode trains from it."""
+import pytest
+import torch
+
+from distributed_tensorflow_resnet_amd.models.spec import imagenet_spec
+from distributed_tensorflow_resnet_amd.train.engine import Engine, imagenet_lr_schedule
+
+pytestmark = pytest.mark.gpu
+MEANS = torch.tensor([123.68, 116.78, 103.94])
+
+
+def test_u8_pack_flip_and_mean(gpu):
+    import distributed_tensorflow_resnet_amd as dtr
+
+    nat = dtr.native(required=True)
+    N, H, W = 16, 20, 24
+    img = torch.randint(0, 256, (N, H, W, 3), dtype=torch.uint8, device=gpu)
+    out = torch.full((N, H, W, 8), 7.0, dtype=torch.bfloat16, device=gpu)
+    gstep = torch.tensor([5], dtype=torch.int64, device=gpu)
+    zero = torch.ones(64, device=gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    nat.imagenet_u8_pack(img.data_ptr(), out.data_ptr(), N, H, W, 99, gstep.data_ptr(), 1,
+                         zero.data_ptr(), zero.numel() * 4, st)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(zero) == 0
+    assert torch.count_nonzero(out[..., 3:]) == 0
+    ref = (img.float().cpu() - MEANS).to(torch.bfloat16).float()
+    got = out[..., :3].float().cpu()
+    flips = 0
+    for n in range(N):
+        if torch.equal(got[n], ref[n]):
+            continue
+        assert torch.equal(got[n], ref[n].flip(1)), n
+        flips += 1
+    assert 2 <= flips <= N - 2          # a fair coin per image
+    # eval (train=0): no flip; a different step reshuffles the flips
+    nat.imagenet_u8_pack(img.data_ptr(), out.data_ptr(), N, H, W, 99, gstep.data_ptr(), 0, 0, 0, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out[..., :3].float().cpu(), ref)
+
+
+def test_engine_trains_from_u8_crops(gpu):
+    spec = imagenet_spec(0, num_classes=10, image_hw=64, block="bottleneck", layers=[1, 1, 1, 1])
+    eng = Engine(spec, 8, weight_decay=1e-4, lr_schedule=imagenet_lr_schedule(), device=gpu,
+                 input_mode="imagenet_u8")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 256, (8, 64, 64, 3), generator=g, dtype=torch.uint8).pin_memory()
+    y = torch.randint(0, 10, (8,), generator=g)
+    eng.set_batch(x, y)
+    losses = []
+    for _ in range(12):
+        eng.step()
+        losses.append(eng.metrics()["cross_entropy"])
+    assert int(eng.gstep.item()) == 12
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert min(losses[-3:]) < losses[0]     # memorises the fixed batch
