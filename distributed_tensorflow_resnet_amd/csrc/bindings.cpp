@@ -154,11 +154,15 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   if ((pre_scale != 0) && mode != MODE_FWD)
     throw std::invalid_argument("fused BN+ReLU prologue is forward-only");
   if (g.abwd.x != nullptr) {
-    if (!conv_direct_covers(g, mode))
-      throw std::invalid_argument("abwd: this dgrad is not covered by the direct 3x3 kernel");
-    const int C = c.K;   // A channels of the dgrad
-    if (g.abwd.acc == nullptr && (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C)))   // 0: coef precomputed
-      throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
+    if (conv_direct_covers(g, mode)) {
+      const int C = c.K;   // A channels of the dgrad
+      if (g.abwd.acc == nullptr && (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C)))   // 0: coef precomputed
+        throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
+    } else if (!conv_gemm_abwd_covers(g)) {
+      throw std::invalid_argument("abwd: this dgrad is covered neither by the direct 3x3 kernel "
+                                  "nor by the implicit-GEMM ABWD loop (needs K % 64 == 0, "
+                                  "K <= 512, no add, precomputed coefficients)");
+    }
   }
   if (g.pfin.cnt > 0 && g.pfin.acc == nullptr) {
     const int C = c.C;   // PRE is forward-only: the A channels
@@ -704,7 +708,13 @@ struct Plan {
                                     S(comm_stream ? comm_stream : main_stream)};
     int bad_op = -1;
     hipError_t bad = hipSuccess;
-    if (use_threads(begin, end) && st[1] != st[0] && st[2] != st[0] && st[1] != st[2]) {
+    // Never while capturing a hipGraph: capture from several host threads is not
+    // reliable on this runtime (capture_end failed with hipErrorInvalidValue in one
+    // of three runs); the graph replays without host issue cost anyway.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st[0], &cap);
+    if (cap == hipStreamCaptureStatusNone && use_threads(begin, end) && st[1] != st[0] &&
+        st[2] != st[0] && st[1] != st[2]) {
       py::gil_scoped_release nogil;
       prepare_threads();
       const unsigned g = ++gen == 0 ? ++gen : gen;   // 0 = never issued
@@ -913,6 +923,20 @@ PYBIND11_MODULE(_C, m) {
     g.Ncol = mode == MODE_FWD ? c.K : c.C;
     return conv_direct_covers(g, mode);
   }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
+  m.def("conv_gemm_abwd_covers", [](std::vector<int> geom, bool has_add) {
+    GemmArgs g{};
+    g.g = geom_from(geom);
+    g.M = g.g.N * g.g.H * g.g.W;
+    g.Ncol = g.g.C;
+    g.Kdim = g.g.kh * g.g.kw * g.g.K;
+    // opt-in (DTR_GEMM_ABWD=1): measured 3x slower per dgrad on ImageNet RN50 (the
+    // per-element BN-backward VALU work is repeated per column tile and per tap and
+    // outweighs the MFMAs it feeds: 13.3 -> 17.8 ms/step), so the step keeps the
+    // separate bandwidth-bound bn_bwd_apply (profiles/bn_bwd_apply_bandwidth.md)
+    const char* e = std::getenv("DTR_GEMM_ABWD");
+    if (e == nullptr || e[0] != '1') return false;
+    return !has_add && conv_gemm_abwd_covers(g);
+  }, "whether the implicit-GEMM dgrad of geom can apply a pending BN backward itself");
   m.def("set_wgrad_direct", &set_wgrad_direct,
         "enable/disable the direct 3x3 small-C wgrad kernel (default: on unless "
         "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");

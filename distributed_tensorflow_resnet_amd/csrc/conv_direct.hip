@@ -351,6 +351,9 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
   // two column tiles (half the weights and MFMAs per workgroup, twice the workgroups)
   // for the layers whose grids are small: 8x8x64 (16 workgroups per image batch of 16)
   // and, at small batch, 16x16x32
+  if (split & 4) {   // four column tiles of the 8x8x64 layers (sweep: DTR_DIRECT_SPLITN=5|7)
+    DTR_DIRECT_BN(64, 8, 64, 16, 4, 1)
+  }
   if (split & 2) {
     DTR_DIRECT_BN(64, 8, 64, 32, 2, 2)
   }

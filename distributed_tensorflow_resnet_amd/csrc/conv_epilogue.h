@@ -180,8 +180,13 @@ struct EpiPre {
   static constexpr int RIT = ON ? (EL::PR + EL::RPP - 1) / EL::RPP : 1;   // per phase
   static constexpr int NX = ON ? RIT * EL::PHASES : 1;
   static constexpr int RR = (XO || EL::PHASES > 1) ? 1 : RIT;
+  // per-column BN coefficients held from kernel start.  In the multi-phase (128x128)
+  // dgrad this pushes the kernel to 256 VGPRs + 24 spilled, yet reading them at the
+  // epilogue instead (0 spills) measured 1 % SLOWER on ImageNet RN50 (13.29 -> 13.43
+  // ms/step): the spill traffic hides in the K loop, the epilogue round trip does not.
+  static constexpr bool COEF = XO;
   bf16x8 res[RR], acc[RR], x[NX];
-  f32x4 bsc[XO ? 2 : 1], bsh[XO ? 2 : 1], bmu[XO ? 2 : 1], brs[XO ? 2 : 1];
+  f32x4 bsc[COEF ? 2 : 1], bsh[COEF ? 2 : 1], bmu[COEF ? 2 : 1], brs[COEF ? 2 : 1];
 };
 
 template <int BM, int BN, int WM, int FLAGS, bool XO = false>
@@ -210,7 +215,7 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
         if constexpr ((FLAGS & F_BNB) != 0)
           P.x[ph * PP::RIT + it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
       }
-    if constexpr (XO && (FLAGS & F_BNB) != 0) {
+    if constexpr (PP::COEF && (FLAGS & F_BNB) != 0) {
       const bool colok = col0 < args.Ncol;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -270,13 +275,14 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   float bnb_t1 = 0.f, bnb_t2 = 0.f;   // BNB column totals (thread tid < BN)
   float bsc[8], bsh[8], bmu[8], brs[8];
   if constexpr (BNB) {
-    if (XO && EpiPre<BM, BN, WM, XO>::ON && pre) {
+    constexpr bool COEF = EpiPre<BM, BN, WM, XO>::COEF;
+    if (COEF && EpiPre<BM, BN, WM, XO>::ON && pre) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        bsc[j] = pre->bsc[XO ? j / 4 : 0][j % 4];
-        bsh[j] = pre->bsh[XO ? j / 4 : 0][j % 4];
-        bmu[j] = pre->bmu[XO ? j / 4 : 0][j % 4];
-        brs[j] = pre->brs[XO ? j / 4 : 0][j % 4];
+        bsc[j] = pre->bsc[COEF ? j / 4 : 0][j % 4];
+        bsh[j] = pre->bsh[COEF ? j / 4 : 0][j % 4];
+        bmu[j] = pre->bmu[COEF ? j / 4 : 0][j % 4];
+        brs[j] = pre->brs[COEF ? j / 4 : 0][j % 4];
       }
     } else {
 #pragma unroll

@@ -27,6 +27,7 @@
 //           gradient g = d_a * [x*scale+shift > 0]:  per-tile sum(g) and
 //           sum(g * xhat), so no separate pass re-reads d_a and x.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
@@ -60,6 +61,12 @@ conv_gemm_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
+  // ABWD (dgrad, FAST loop only): the A operand is the pending BatchNorm+ReLU backward
+  // of the produced gradient, dh = a*g - b - c*xhat with g = da*[x*scale+shift > 0],
+  // applied while staging A (coefficients precomputed by bn_bwd_finalize); the
+  // workgroups of column tile 0 also write dh once (center tap) for the weight
+  // gradient -- no separate bn_bwd_apply pass over da / x / dh.
+  constexpr bool ABWD = (FLAGS & F_ABWD) != 0;
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MR = WTM / 16, NR = WTN / 16;
@@ -297,6 +304,12 @@ conv_gemm_kernel(GemmArgs args) {
   bf16x8 pa[2][A_PER_T], pb[2][B_PER_T];
   unsigned pmask[2] = {0u, 0u};
   int pci[2] = {0, 0};
+  bf16x8 px[ABWD ? 2 : 1][ABWD ? A_PER_T : 1];   // ABWD: BN input rows of the A chunks
+  int poff[ABWD ? 2 : 1][ABWD ? A_PER_T : 1];    // ABWD: their byte offsets (dh write)
+  bool pctr[2] = {false, false};                 // ABWD: the tile is the center tap
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(ABWD ? args.abwd.x : args.a), 0, (int)(fast && ABWD ? a_elems * 2 : 0),
+      0x00020000);
   auto issue = [&](int t, auto P) {   // loads of K tile t into set P (t >= KT: zeros)
     constexpr int p = decltype(P)::value;
     const int kb = t * BK;                       // uniform
@@ -306,6 +319,10 @@ conv_gemm_kernel(GemmArgs args) {
     if constexpr (PRE) pci[p] = kv ? ci : 0;
     const int rr = tap / g.kw, cc = tap - rr * g.kw;
     unsigned msk = 0u;
+    if constexpr (ABWD) {
+      pci[p] = kv ? ci : 0;
+      pctr[p] = kv && rr == g.kh / 2 && cc == g.kw / 2;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       int off = kOOB;
@@ -324,10 +341,15 @@ conv_gemm_kernel(GemmArgs args) {
         }
         ok = ok && hp < g.Ho && wp < g.Wo;
         off = ok ? ((a_base[i] + hp * g.Wo + wp) * g.K + ci) * 2 : kOOB;
+        msk |= ok ? (1u << i) : 0u;
       }
       pa[p][i] = bload(rs_a, off);
+      if constexpr (ABWD) {
+        px[p][i] = bload(rs_x, off);
+        poff[p][i] = off;
+      }
     }
-    if constexpr (PRE) pmask[p] = msk;
+    if constexpr (PRE || ABWD) pmask[p] = msk;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int q = tid + i * 256;
@@ -343,6 +365,26 @@ conv_gemm_kernel(GemmArgs args) {
     constexpr int p = decltype(P)::value;
     bf16* A = As + buf * BM * BK;
     bf16* B = Bs + buf * BN * BK;
+    float ca[8], ccr[8], cd[8], csc[8], csh[8];   // ABWD: this thread's 8 channels
+    if constexpr (ABWD) {
+      const float* T = pre_s + pci[p];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 va = *reinterpret_cast<const f32x4*>(T + 4 * h);
+        const f32x4 vc = *reinterpret_cast<const f32x4*>(T + Acin + 4 * h);
+        const f32x4 vd = *reinterpret_cast<const f32x4*>(T + 2 * Acin + 4 * h);
+        const f32x4 vs = *reinterpret_cast<const f32x4*>(T + 3 * Acin + 4 * h);
+        const f32x4 vh = *reinterpret_cast<const f32x4*>(T + 4 * Acin + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ca[4 * h + j] = va[j];
+          ccr[4 * h + j] = vc[j];
+          cd[4 * h + j] = vd[j];
+          csc[4 * h + j] = vs[j];
+          csh[4 * h + j] = vh[j];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int q = tid + i * 256;
@@ -352,6 +394,19 @@ conv_gemm_kernel(GemmArgs args) {
         if constexpr (PRE) {
           const unsigned sel = 0u - ((pmask[p] >> i) & 1u);   // all-ones: real pixel
           v = affine_relu8_sel(v, s0, s1, b0, b1, sel);
+        }
+        if constexpr (ABWD) {
+          const bool real = (pmask[p] >> i) & 1u;   // padding / out-of-range stays zero
+          bf16x8 dh;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xv = (float)px[p][i][j];
+            const float gg = (xv * csc[j] + csh[j] > 0.f) ? (float)v[j] : 0.f;
+            dh[j] = (bf16)(real ? ca[j] * gg - ccr[j] * xv - cd[j] : 0.f);
+          }
+          v = dh;
+          if (real && pctr[p] && tn == 0)   // each dh element once: center tap, column tile 0
+            *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(args.abwd.a_out) + poff[p][i]) = dh;
         }
         *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
       }
@@ -408,7 +463,21 @@ conv_gemm_kernel(GemmArgs args) {
     using I1 = std::integral_constant<int, 1>;
     issue(0, I0{});
     issue(1, I1{});
-    if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+    if constexpr (BNB && !ABWD) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+    if constexpr (ABWD) {   // [5][Acin]: a, c*rstd, b - c*rstd*mean, scale, shift
+      // dh = a*g - b - c*(x - mean)*rstd = a*g - (c*rstd)*x - (b - c*rstd*mean)
+      const BnBwdPre& Q = args.abwd;
+      for (int c = tid; c < Acin; c += 256) {
+        const float a = Q.coef[c], bb = Q.coef[Acin + c], cc = Q.coef[2 * Acin + c];
+        const float cr = cc * Q.rstd[c];
+        pre_s[c] = a;
+        pre_s[Acin + c] = cr;
+        pre_s[2 * Acin + c] = bb - cr * Q.mean[c];
+        pre_s[3 * Acin + c] = Q.scale[c];
+        pre_s[4 * Acin + c] = Q.shift[c];
+      }
+      __syncthreads();
+    }
     if constexpr (PRE) {
       if (args.pfin.cnt > 0) {
         bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
@@ -473,10 +542,10 @@ conv_gemm_kernel(GemmArgs args) {
   }
   }
 
-  if constexpr (BNB && EP::ON)
+  if constexpr (BNB && EP::ON && !ABWD)
     conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre, tm, tn);
   else
-    conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0, nullptr, tm, tn);
+    conv_epilogue<BM, BN, WM, WN, FLAGS, false>(args, acc, smem, m0, n0, nullptr, tm, tn);
 }
 
 // ---------------------------------------------------------------------------
@@ -525,10 +594,22 @@ static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)NBUF * (BM + BN) * 64 * sizeof(bf16);
   if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);
+  if (FLAGS & F_ABWD) lds += (size_t)5 * Acin * sizeof(float);
   lds = std::max(lds, EpiLayout<BM, BN, WM>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
-  // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles
+  // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles; the
+  // fused BN backward (ABWD) exists only there
+  if constexpr ((FLAGS & F_ABWD) != 0) {
+    if constexpr (BN >= 64) {
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
+                         dim3(256), lds, s, a);
+      DTR_CHECK_LAUNCH();
+    } else {
+      throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
+    }
+    return;
+  }
   if constexpr (BN >= 64) {
     if (conv_gemm_fast(a, MODE)) {
       hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
@@ -552,6 +633,15 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
     else if (st) launch_cfg<BM, BN, WM, WN, MODE, F_STATS>(a, s);
     else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   } else {
+    const bool ab = a.abwd.x != nullptr;
+    if constexpr (BN >= 64) {
+      if (ab) {
+        if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB | F_ABWD>(a, s);
+        else launch_cfg<BM, BN, WM, WN, MODE, F_ABWD>(a, s);
+        return;
+      }
+    }
+    if (ab) throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
     if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB>(a, s);
     else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   }
@@ -562,8 +652,17 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
 // partial buffer has one row per M tile).
 int conv_gemm_bm(int M, int nc) {
   const long m = M;
-  if (nc <= 16) return m >= 256L * 512 ? 256 : 64;
-  if (nc <= 32) return m >= 128L * 512 ? 128 : 64;
+  // DTR_SMALLC_BM="b16,b32": the large-M tile heights of the 16- / 32-column convs
+  // (the CIFAR stages 1 / 2; sweeps of rows per workgroup vs workgroups per CU)
+  static int b16 = -1, b32 = -1;
+  if (b16 < 0) {
+    b16 = 256, b32 = 128;
+    if (const char* e = std::getenv("DTR_SMALLC_BM")) std::sscanf(e, "%d,%d", &b16, &b32);
+    if (b16 != 256 && b16 != 64) b16 = 256;
+    if (b32 != 128 && b32 != 64) b32 = 128;
+  }
+  if (nc <= 16) return m >= 256L * 512 ? b16 : 64;
+  if (nc <= 32) return m >= 128L * 512 ? b32 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
   return (m >= 128L * 128 && nc % 128 == 0) ? 128 : 64;
 }
@@ -610,10 +709,26 @@ static void launch_mode(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+// Whether the implicit-GEMM dgrad can apply a pending BN backward (ABWD) itself: the
+// FAST loop's structure (A channels a multiple of 64, tensors < 2^30 elements), a
+// >= 64-column tile, the [5][C] coefficient table within 10 KB of LDS (C <= 512, the
+// bottleneck's inner BNs), no residual add (the block-input BNs), coefficients
+// precomputed by bn_bwd_finalize (cnt 0).
+bool conv_gemm_abwd_covers(const GemmArgs& a) {
+  const ConvGeom& g = a.g;
+  const long a_elems = (long)g.N * g.Ho * g.Wo * g.K;
+  const long b_elems = (long)g.kh * g.kw * g.C * g.K;
+  if (g.K % 64 != 0 || g.K > 512 || a_elems >= (1L << 30) || b_elems >= (1L << 30)) return false;
+  if (a.Ncol < 64 || a.Ncol % 16 != 0) return false;
+  if (a.abwd.x != nullptr && (a.abwd.add != nullptr || a.abwd.cnt != 0 || a.abwd.acc != nullptr))
+    return false;
+  return true;
+}
+
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
   if (conv_direct(a, mode, s)) return;
-  if (a.abwd.x != nullptr)   // the generic kernel has no BN-backward prologue: never silently
-    throw std::runtime_error("conv_gemm: fused BN backward (abwd) needs the direct 3x3 kernel");
+  if (a.abwd.x != nullptr && (mode != MODE_DGRAD || !conv_gemm_abwd_covers(a)))
+    throw std::runtime_error("conv_gemm: fused BN backward (abwd) not covered for this dgrad");
   if (mode == MODE_FWD) launch_mode<MODE_FWD>(a, s);
   else launch_mode<MODE_DGRAD>(a, s);
 }

@@ -133,6 +133,7 @@ void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
+bool conv_gemm_abwd_covers(const GemmArgs& a);   // generic dgrad with the fused BN backward
 void set_conv_direct(int enabled);
 void set_conv_wide_tile(int mask);     // 128x64 tiles for > 64 output columns (experiment)
 void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loops (DTR_CONV_PIPE)

@@ -623,12 +623,18 @@ class Engine:
         a_src = dy
         pb = self._pending_bwd
         if pb is not None:
-            if (pb["out"] is dy and dx is not None and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
-                    and self.nat.conv_direct_covers(1, geom)):
+            fuse = pb["out"] is dy and dx is not None and \
+                os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
+            direct = fuse and self.nat.conv_direct_covers(1, geom)
+            # the implicit-GEMM dgrad applies it too (1x1 / strided / ImageNet shapes),
+            # from coefficients finalized by a separate tiny launch
+            gemm = fuse and not direct and self.nat.conv_gemm_abwd_covers(geom,
+                                                                          pb["add"] is not None)
+            if direct or gemm:
                 bn = pb["bn"]
                 add = pb["add"]
                 part, cnt = pb["part"], pb["cnt"]
-                if cnt != -1 and cnt > self._consumer_cap(s.cout):
+                if gemm or (cnt != -1 and cnt > self._consumer_cap(s.cout)):
                     # too many partials for the prologue: finalize separately, the
                     # dgrad then reads the coefficients (cnt = 0)
                     plan.bn_bwd_finalize(part, cnt, pb["M"], bn.spec.channels, bn.gamma,
