@@ -923,6 +923,8 @@ PYBIND11_MODULE(_C, m) {
     g.Ncol = mode == MODE_FWD ? c.K : c.C;
     return conv_direct_covers(g, mode);
   }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
+  m.def("set_direct_probe", [](ptr_t p) { set_direct_probe(P<long long>(p)); },
+        "diagnostics: direct-conv workgroups write 4 wall-clock stamps each to p (0 = off)");
   m.def("conv_gemm_abwd_covers", [](std::vector<int> geom, bool has_add) {
     GemmArgs g{};
     g.g = geom_from(geom);

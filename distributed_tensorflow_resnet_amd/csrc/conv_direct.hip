@@ -64,6 +64,10 @@ conv3x3_direct_kernel(GemmArgs args) {
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
   const bf16x8 zero8 = {};
+  // diagnostics (scripts/probe_direct.py): wall-clock stamps (100 MHz) of this
+  // workgroup's phases -- start, operands staged, MFMAs done, epilogue issued
+  long long* const probe = args.probe ? args.probe + 4 * (blockIdx.x + gridDim.x * blockIdx.y) : nullptr;
+  if (probe && tid == 0) probe[0] = wall_clock64();
 
   // ---- 1. all global loads in flight at once: weights (VGPR) + halo (VGPR) ----
   bf16x8 breg[KSTEPS][NR];
@@ -222,6 +226,7 @@ conv3x3_direct_kernel(GemmArgs args) {
     }
   }
   __syncthreads();
+  if (probe && tid == 0) probe[1] = wall_clock64();
 
   // ---- 3. MFMA over (tap, channel) k-steps ----
   f32x4 acc[MR][NR];
@@ -256,13 +261,20 @@ conv3x3_direct_kernel(GemmArgs args) {
     }
   }
   __syncthreads();   // halo dead: the epilogue reuses the LDS
+  if (probe && tid == 0) probe[2] = wall_clock64();
 
   // ---- 4. shared epilogue ----
   conv_epilogue<BM, BN, WM, WN, FLAGS>(args, acc, smem, m0, n0, &epre);
+  if (probe && tid == 0) probe[3] = wall_clock64();
 }
 
+static long long* g_probe = nullptr;   // set_direct_probe (diagnostics only): each launch
+void set_direct_probe(long long* p) { g_probe = p; }   // advances it past its own stamps
+
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
-static void launch_direct_cfg(const GemmArgs& a, hipStream_t s) {
+static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.probe = g_probe;
   constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
   constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(7 * CA + 768) * sizeof(float);
   const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
@@ -270,6 +282,7 @@ static void launch_direct_cfg(const GemmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
                      dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
+  if (g_probe) g_probe += 4L * grid.x * grid.y;
 }
 
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE>
