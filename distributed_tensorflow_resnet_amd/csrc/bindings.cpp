@@ -578,6 +578,8 @@ struct Plan {
   size_t rec_of_n = 0;
   unsigned gen = 0;
   std::atomic<bool> abort_run{false};
+  std::mutex err_mu;
+  std::string err_msg;           // first exception message of a threaded run
 
   ~Plan() {
     for (auto& w : workers) w.reset();
@@ -691,7 +693,14 @@ struct Plan {
           }
         }
       }
-      hipError_t e = issue(i, s);
+      hipError_t e = hipSuccess;
+      try {   // a launch closure may throw (shape / coverage checks): never out of a thread
+        e = issue(i, s);
+      } catch (const std::exception& ex) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (err_msg.empty()) err_msg = ex.what();
+        e = hipErrorInvalidValue;
+      }
       if (e == hipSuccess && ops[i].kind == OP_LAUNCH) e = hipGetLastError();  // per thread
       if (e != hipSuccess) {
         abort_run.store(true);
@@ -719,6 +728,7 @@ struct Plan {
       prepare_threads();
       const unsigned g = ++gen == 0 ? ++gen : gen;   // 0 = never issued
       abort_run.store(false);
+      err_msg.clear();
       std::pair<int, hipError_t> res[PLAN_STREAMS];
       bool used[PLAN_STREAMS] = {false, false, false};
       for (int i = begin; i < end; ++i) used[ops[i].stream] = true;
@@ -765,7 +775,8 @@ struct Plan {
     }
     if (bad != hipSuccess)
       throw std::runtime_error("plan op " + std::to_string(bad_op) + " (" + names[bad_op] +
-                               ") failed: " + hipGetErrorString(bad));
+                               ") failed: " + (err_msg.empty() ? hipGetErrorString(bad)
+                                                               : err_msg.c_str()));
   }
   int size() const { return (int)ops.size(); }
 };
