@@ -4,6 +4,7 @@
 // footprint of `v_mfma_f32_16x16x32_bf16` operands (8 x bf16 = 4 VGPRs) and
 // accumulators (4 x f32).  No CUDA-compat shims: HIP on gfx950 only.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -125,6 +126,16 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
     r[p] = __builtin_bit_cast(unsigned, m) & sel;
   }
   return __builtin_bit_cast(bf16x8, r);
+}
+
+// Host: whether conv epilogues store write-through (DTR_WT_STORE=1; read once).
+inline bool wt_store_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DTR_WT_STORE");
+    v = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
 }
 
 }  // namespace dtr

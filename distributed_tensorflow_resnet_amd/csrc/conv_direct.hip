@@ -66,7 +66,7 @@ conv3x3_direct_kernel(GemmArgs args) {
   const bf16x8 zero8 = {};
   // diagnostics (scripts/probe_direct.py): wall-clock stamps (100 MHz) of this
   // workgroup's phases -- start, operands staged, MFMAs done, epilogue issued
-  long long* const probe = args.probe ? args.probe + 4 * (blockIdx.x + gridDim.x * blockIdx.y) : nullptr;
+  long long* const probe = args.probe ? args.probe + 8 * (blockIdx.x + gridDim.x * blockIdx.y) : nullptr;
   if (probe && tid == 0) probe[0] = wall_clock64();
 
   // ---- 1. all global loads in flight at once: weights (VGPR) + halo (VGPR) ----
@@ -275,6 +275,7 @@ template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   a.probe = g_probe;
+  a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
   constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
   constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(7 * CA + 768) * sizeof(float);
   const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
@@ -282,7 +283,7 @@ static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
   hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
                      dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
-  if (g_probe) g_probe += 4L * grid.x * grid.y;
+  if (g_probe) g_probe += 8L * grid.x * grid.y;
 }
 
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE>

@@ -120,18 +120,42 @@ __device__ __forceinline__ void sum_combine(const float* src, int NC, int n0, in
 }
 
 // Column sums of the epilogue's 8-column row vectors: thread (r0 = tid / CPR,
-// cc = tid % CPR) holds v[j] for column cc*8+j.  Lanes with equal cc sit CPR apart
-// in a wave: xor-shuffles fold the wave, then lanes < CPR write the 4 wave totals
+// cc = tid % CPR) holds v[j] for column cc*8+j.  The lanes with equal cc are
+// summed by DPP row_ror steps of CPR, 2*CPR, .. within each 16-lane row (VALU, fused
+// into v_add_f32_dpp), then two xor shuffles across the four rows, leaving every lane
+// with its column's wave total (was: a __shfl_xor tree of log2(64 / CPR) ds_bpermute
+// steps per value -> 80-116 per conv, ~1 us of the epilogue,
+// profiles/cifar_direct_conv_phases.md).  Lanes < CPR then write the 4 wave totals
 // to wred[4][BN] (fixed order, deterministic).  Ends with a barrier; the caller
-// adds wred[0..3][col].  (A serial loop over the RPP rows by BN threads cost
-// 2.5-4 us per conv at 256-row tiles.)
+// adds wred[0..3][col].
+template <int OFF>
+__device__ __forceinline__ float row_ror_add(float v) {   // v + v of lane (l - OFF) mod 16
+  if constexpr (OFF < 16)
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                             0, __builtin_bit_cast(int, v), 0x120 + OFF, 0xf, 0xf,
+                                             false));
+  return v;
+}
+
+template <int CPR>
+__device__ __forceinline__ float lanes_colsum(float v) {
+  v = row_ror_add<CPR>(v);
+  if constexpr (2 * CPR < 16) v = row_ror_add<2 * CPR>(v);
+  if constexpr (4 * CPR < 16) v = row_ror_add<4 * CPR>(v);
+  if constexpr (8 * CPR < 16) v = row_ror_add<8 * CPR>(v);
+  // the four 16-lane rows: two shuffles.  (v_permlane16/32_swap with the value on both
+  // sides would do it on the VALU, but hipcc folds permlane*_swap(x, x) to one result
+  // and silently drops a row: caught by test_conv_fused_prologue_epilogue.)
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
 template <int CPR, int BN>
 __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
+  static_assert(CPR >= 1 && CPR <= 16 && (CPR & (CPR - 1)) == 0, "CPR");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int off = CPR; off < 64; off <<= 1) v[j] += __shfl_xor(v[j], off, 64);
+  for (int j = 0; j < 8; ++j) v[j] = lanes_colsum<CPR>(v[j]);
   if (lane < CPR) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) wred[wave * BN + lane * 8 + j] = v[j];
@@ -143,14 +167,13 @@ __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
 template <int CPR, int BN>
 __device__ __forceinline__ void colsum8x2(float (&v)[8], float (&w)[8], float* wred,
                                           float* wred2) {
+  static_assert(CPR >= 1 && CPR <= 16 && (CPR & (CPR - 1)) == 0, "CPR");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int off = CPR; off < 64; off <<= 1) {
-      v[j] += __shfl_xor(v[j], off, 64);
-      w[j] += __shfl_xor(w[j], off, 64);
-    }
+  for (int j = 0; j < 8; ++j) {
+    v[j] = lanes_colsum<CPR>(v[j]);
+    w[j] = lanes_colsum<CPR>(w[j]);
+  }
   if (lane < CPR) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -184,7 +207,9 @@ struct EpiPre {
   // dgrad this pushes the kernel to 256 VGPRs + 24 spilled, yet reading them at the
   // epilogue instead (0 spills) measured 1 % SLOWER on ImageNet RN50 (13.29 -> 13.43
   // ms/step): the spill traffic hides in the K loop, the epilogue round trip does not.
-  static constexpr bool COEF = XO;
+  // The single-phase direct-conv dgrad prefetches them too (reading them at its epilogue
+  // cost ~1 us of LDS-staging time per launch, profiles/cifar_direct_conv_phases.md).
+  static constexpr bool COEF = XO || EL::PHASES == 1;
   bf16x8 res[RR], acc[RR], x[NX];
   f32x4 bsc[COEF ? 2 : 1], bsh[COEF ? 2 : 1], bmu[COEF ? 2 : 1], brs[COEF ? 2 : 1];
 };
@@ -355,6 +380,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     lds_barrier();
+    if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 4] = wall_clock64();
     // Pass 1: values of this thread's rows (residual / accumulate, ONE bf16
     // rounding) kept in registers; BN sums accumulated.  Global stores are issued
     // only AFTER the statistics' barriers: a __syncthreads() waits for every
@@ -445,6 +471,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         }
       }
     }
+    if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 5] = wall_clock64();
     if constexpr (STATS) {
       colsum8x2<EL::CPR, BN>(p1, p2, red, red2);
       if (tid < BN) {
@@ -469,13 +496,28 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         }
       }
     }
-    // Pass 2: the stores
+    if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 6] = wall_clock64();
+    // Pass 2: the stores (args.wt: write-through sc1 buffer stores, so the tile does not
+    // sit dirty in this XCD's L2 for the end-of-kernel release to write back)
     if (!args.out_f32) {
+      if (args.wt) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.out, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int it = 0; it < RIT; ++it) {
-        const int r = r0 + it * EL::RPP;
-        if (!colok || r >= nph) continue;
-        *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
+        for (int it = 0; it < RIT; ++it) {
+          const int r = r0 + it * EL::RPP;
+          if (!colok || r >= nph) continue;
+          typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ob[it]), rs,
+                                                 (int)(((long)(prow0 + r) * NC + col0) * 2), 0,
+                                                 16);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) {
+          const int r = r0 + it * EL::RPP;
+          if (!colok || r >= nph) continue;
+          *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
+        }
       }
     }
     // the next phase overwrites the tile (LDS-only: this phase's stores stay in flight)

@@ -591,6 +591,7 @@ static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   }
   GemmArgs a = a0;
   a.swz = (g_xcd_swz && (a.Ncol + BN - 1) / BN > 1) ? 1 : 0;
+  a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)NBUF * (BM + BN) * 64 * sizeof(bf16);
   if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);

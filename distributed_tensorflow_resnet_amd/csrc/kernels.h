@@ -128,6 +128,7 @@ struct GemmArgs {
   int M, Ncol, Kdim;
   int swz = 0;              // conv_gemm: XCD-grouped tile order (set by the launcher)
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
+  int wt = 0;                   // epilogue output stores write-through (sc1): DTR_WT_STORE
 };
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Inside-the-kernel timeline of the direct 3x3 conv (conv_direct.hip) on the CIFAR
 shapes: every workgroup stamps wall_clock64 (100 MHz) at start, operands staged in
-LDS, MFMAs done and epilogue issued.  For a back-to-back chain of identical
+LDS, MFMAs done, and inside the epilogue (conv_epilogue.h) after the fp32 tile is
+staged in LDS, after the row pass (residual / rounding / BN sums), after the
+column-sum reductions and when the stores and atomics are issued.  For a back-to-back chain of identical
 launches (the step's pattern) this prints, per launch, the dispatch gap (previous
 launch's last stamp -> this launch's first start), the start skew across
 workgroups, and the median per-workgroup phase durations.
@@ -63,7 +65,7 @@ def main():
                                    0, 0, 0, gl, bnb, [], [acc.data_ptr()], [], abwd_acc, 0.997,
                                    1e-5, 1)
             # grid size: from a probe-less dry run count is not exposed; allocate generously
-            probe = torch.zeros(NL * 4 * 8192, dtype=torch.int64, device=dev)
+            probe = torch.zeros(NL * 8 * 8192, dtype=torch.int64, device=dev)
             st = torch.cuda.current_stream().cuda_stream
             for rnd in range(3):
                 probe.zero_()
@@ -71,10 +73,10 @@ def main():
                 plan.run(0, plan.size(), st, st, st)
                 nat.set_direct_probe(0)
                 torch.cuda.synchronize()
-            pr = probe.view(-1, 4).cpu()
+            pr = probe.view(-1, 8).cpu()
             rows = pr[pr[:, 0] != 0]
             nwg = rows.shape[0] // NL
-            L = rows.view(NL, nwg, 4).double() * 10.0   # 100 MHz ticks -> ns
+            L = rows.view(NL, nwg, 8).double() * 10.0   # 100 MHz ticks -> ns
             t0 = L[:, :, 0].min()
             lines = []
             for i in range(1, NL):
@@ -82,14 +84,15 @@ def main():
                 start = L[i, :, 0]
                 gap = (start.min() - prev_end) / 1e3
                 skew = (start.max() - start.min()) / 1e3
-                ph = [statistics.median((L[i, :, k + 1] - L[i, :, k]).tolist()) / 1e3 for k in range(3)]
+                d = lambda a, b: statistics.median((L[i, :, b] - L[i, :, a]).tolist()) / 1e3  # noqa
+                ph = [d(0, 1), d(1, 2), d(2, 4), d(4, 5), d(5, 6), d(6, 3)]
                 span = (L[i, :, 3].max() - start.min()) / 1e3
                 lines.append((gap, skew, *ph, span))
             med = [statistics.median(c) for c in zip(*lines)]
-            print(f"N{N} H{H:2d} C{C:2d} {var:5s} wg {nwg:4d}: gap {med[0]:5.2f} | start skew "
-                  f"{med[1]:5.2f} | load+prologue {med[2]:5.2f} | mfma {med[3]:5.2f} | "
-                  f"epilogue issue {med[4]:5.2f} | first start -> last epilogue {med[5]:5.2f} us",
-                  flush=True)
+            print(f"N{N} H{H:2d} C{C:2d} {var:5s} wg {nwg:4d}: gap {med[0]:4.2f} | skew "
+                  f"{med[1]:4.2f} | stage {med[2]:4.2f} | mfma {med[3]:4.2f} | epi: lds "
+                  f"{med[4]:4.2f} rows {med[5]:4.2f} colsum {med[6]:4.2f} store+atomic "
+                  f"{med[7]:4.2f} | span {med[8]:5.2f} us", flush=True)
 
 
 if __name__ == "__main__":
