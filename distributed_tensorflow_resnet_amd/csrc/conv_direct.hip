@@ -32,7 +32,7 @@
 
 namespace dtr {
 
-template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
+template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS, bool LW>
 __global__ void __launch_bounds__(256)
 conv3x3_direct_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
@@ -47,10 +47,18 @@ conv3x3_direct_kernel(GemmArgs args) {
   constexpr int MR = WTM / 16, NR = WTN / 16;
   static_assert(BM % WI == 0 && WM * WN == 4 && MR >= 1 && NR >= 1, "tile");
   static_assert((U & (U - 1)) == 0, "C/8 must be a power of two");
+  // LW: the workgroup's weight slice is staged once through LDS ([BN][KP] rows,
+  // padded 16 B so the 16 lanes of a fragment read hit distinct banks) instead of
+  // every wave gathering its B fragments into VGPRs
+  constexpr int KP = KSTEPS * 32 + 8;
+  constexpr int WU = BN * KSTEPS * 4;                         // weight 16-B units
+  constexpr int WPT = LW ? (WU + 255) / 256 : 1;
+  constexpr int WBYTES = LW ? BN * KP * 2 : 0;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = reinterpret_cast<bf16*>(smem);
-  float* pre_s = reinterpret_cast<float*>(smem + HU * 16);   // PRE: [2][CA] scale, shift
+  bf16* wl = reinterpret_cast<bf16*>(smem + HU * 16);
+  float* pre_s = reinterpret_cast<float*>(smem + HU * 16 + WBYTES);   // PRE: [2][CA] scale, shift
   float* fin_scratch = pre_s + 7 * CA;                        // 768 floats (prologue sums)
 
   const ConvGeom& g = args.g;
@@ -70,9 +78,25 @@ conv3x3_direct_kernel(GemmArgs args) {
   if (probe && tid == 0) probe[0] = wall_clock64();
 
   // ---- 1. all global loads in flight at once: weights (VGPR) + halo (VGPR) ----
-  bf16x8 breg[KSTEPS][NR];
+  bf16x8 breg[LW ? 1 : KSTEPS][NR];
+  bf16x8 wv[WPT];
+  if constexpr (LW) {
 #pragma unroll
-  for (int s = 0; s < KSTEPS; ++s) {
+    for (int i = 0; i < WPT; ++i) {
+      const int q = tid + i * 256;
+      const int nl = q / (KSTEPS * 4), kk = (q - nl * (KSTEPS * 4)) * 8;
+      const int tap = kk / CA, c = kk - tap * CA, n = n0 + nl;
+      bf16x8 v = zero8;
+      if (q < WU && tap < 9 && n < NC) {
+        const long off = (MODE == MODE_FWD) ? (long)n * (9 * CA) + kk
+                                            : ((long)tap * NC + n) * CA + c;
+        v = *reinterpret_cast<const bf16x8*>(args.b + off);
+      }
+      wv[i] = v;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < (LW ? 0 : KSTEPS); ++s) {
     const int kk = s * 32 + fq * 8;
     const int tap = kk / CA, c = kk - tap * CA;
 #pragma unroll
@@ -225,6 +249,14 @@ conv3x3_direct_kernel(GemmArgs args) {
       *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = v;
     }
   }
+  if constexpr (LW) {
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int q = tid + i * 256;
+      const int nl = q / (KSTEPS * 4), kk = (q - nl * (KSTEPS * 4)) * 8;
+      if (q < WU) *reinterpret_cast<bf16x8*>(wl + nl * KP + kk) = wv[i];
+    }
+  }
   __syncthreads();
   if (probe && tid == 0) probe[1] = wall_clock64();
 
@@ -257,7 +289,14 @@ conv3x3_direct_kernel(GemmArgs args) {
       const bf16x8 af =
           *reinterpret_cast<const bf16x8*>(halo + (pix * U + (unit ^ (hc & (U - 1)))) * 8);
 #pragma unroll
-      for (int b = 0; b < NR; ++b) acc[a][b] = mfma16(af, breg[s][b], acc[a][b]);
+      for (int b = 0; b < NR; ++b) {
+        if constexpr (LW) {
+          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(wl + (wn * WTN + b * 16 + fr) * KP + kk);
+          acc[a][b] = mfma16(af, bf, acc[a][b]);
+        } else {
+          acc[a][b] = mfma16(af, breg[s][b], acc[a][b]);
+        }
+      }
     }
   }
   __syncthreads();   // halo dead: the epilogue reuses the LDS
@@ -271,19 +310,37 @@ conv3x3_direct_kernel(GemmArgs args) {
 static long long* g_probe = nullptr;   // set_direct_probe (diagnostics only): each launch
 void set_direct_probe(long long* p) { g_probe = p; }   // advances it past its own stamps
 
+// DTR_DIRECT_LDSW bitmask (1: C16, 2: C32, 4: C64) of the layers whose weights are
+// staged through LDS.  Default 4, measured (CIFAR RN50, probe + bench): C64 stage
+// phase 4.8 -> 4.0 us (dgrad) and 3.5 -> 3.1 (fwd); step bs16 0.978 -> 0.955 ms,
+// bs128 unchanged (1.293 / 1.300); C16/C32 add LDS reads without a gain.
+static int g_direct_ldsw = -1;   // -1: read DTR_DIRECT_LDSW once
+
+template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS, bool LW>
+static void launch_direct_lw(const GemmArgs& a, hipStream_t s) {
+  constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
+  constexpr int KSTEPS = (9 * CA + 31) / 32;
+  constexpr size_t WB = LW ? (size_t)BN * (KSTEPS * 32 + 8) * 2 : 0;
+  constexpr size_t MAIN = (size_t)HU * 16 + WB + (size_t)(7 * CA + 768) * sizeof(float);
+  const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
+  dim3 grid(a.M / BM, (a.Ncol + BN - 1) / BN);
+  hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS, LW>), grid,
+                     dim3(256), lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   a.probe = g_probe;
   a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
-  constexpr int HU = (BM / WI + 2) * (WI + 2) * (CA / 8);
-  constexpr size_t MAIN = (size_t)HU * 16 + (size_t)(7 * CA + 768) * sizeof(float);
-  const size_t lds = (std::max(MAIN, EpiLayout<BM, BN, WM>::BYTES) + 15) & ~(size_t)15;
-  dim3 grid(a.M / BM, (a.Ncol + BN - 1) / BN);
-  hipLaunchKernelGGL((conv3x3_direct_kernel<CA, WI, BM, BN, WM, WN, MODE, FLAGS>), grid,
-                     dim3(256), lds, s, a);
-  DTR_CHECK_LAUNCH();
-  if (g_probe) g_probe += 8L * grid.x * grid.y;
+  if (g_direct_ldsw < 0) {
+    const char* e = std::getenv("DTR_DIRECT_LDSW");
+    g_direct_ldsw = e ? std::atoi(e) : 4;
+  }
+  if (g_direct_ldsw & (CA / 16)) launch_direct_lw<CA, WI, BM, BN, WM, WN, MODE, FLAGS, true>(a, s);
+  else launch_direct_lw<CA, WI, BM, BN, WM, WN, MODE, FLAGS, false>(a, s);
+  if (g_probe) g_probe += 8L * (a.M / BM) * ((a.Ncol + BN - 1) / BN);
 }
 
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE>
