@@ -441,6 +441,11 @@ static Launch mk_fill(ptr_t p, long n, float a) {
   return [=](hipStream_t s) { fill_f32(P<float>(p), n, a, s); };
 }
 
+static Launch mk_delay(double us) {   // diagnostics: one spinning wave (diag.hip)
+  const long long ticks = (long long)(us * 100.0);
+  return [=](hipStream_t s) { plan_delay(ticks, s); };
+}
+
 static Launch mk_memset(ptr_t p, long bytes) {
   return [=](hipStream_t s) {
     if (hipMemsetAsync(P<void>(p), 0, (size_t)bytes, s) != hipSuccess)
@@ -580,6 +585,29 @@ struct Plan {
   std::atomic<bool> abort_run{false};
   std::mutex err_mu;
   std::string err_msg;           // first exception message of a threaded run
+  // schedule perturbation (race check, utils/racecheck.py): 0 off; 1 serialize every
+  // stream onto the main stream (plan order = a valid sequential schedule); 2 jitter:
+  // a plan_delay of U[0, pmax_ticks) in front of a launch with probability pprob,
+  // drawn from (pseed, run, op) so each run perturbs a different schedule
+  int perturb = 0;
+  unsigned long long pseed = 0, prun = 0;
+  double pprob = 0.0;
+  long long pmax_ticks = 0;
+
+  static unsigned long long mix64(unsigned long long x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+  }
+  void set_perturb(int mode, unsigned long long seed, double prob, double max_us) {
+    if (mode < 0 || mode > 2) throw std::invalid_argument("perturb mode: 0 off, 1 serialize, 2 jitter");
+    perturb = mode;
+    pseed = seed;
+    prun = 0;
+    pprob = prob;
+    pmax_ticks = (long long)(max_us * 100.0);   // wall clock: 100 MHz
+  }
 
   ~Plan() {
     for (auto& w : workers) w.reset();
@@ -634,6 +662,11 @@ struct Plan {
   hipError_t issue(int i, hipStream_t s) {
     const PlanOp& o = ops[i];
     if (o.kind == OP_LAUNCH) {
+      if (perturb == 2 && pmax_ticks > 0) {
+        const unsigned long long h = mix64(mix64(pseed ^ (prun << 32)) ^ (unsigned long long)i);
+        if ((double)(h >> 11) * (1.0 / 9007199254740992.0) < pprob)
+          plan_delay((long long)(mix64(h) % (unsigned long long)pmax_ticks), s);
+      }
       o.fn(s);
       return hipSuccess;
     }
@@ -715,6 +748,8 @@ struct Plan {
     if (begin < 0 || end > (int)ops.size() || begin > end) throw std::out_of_range("plan range");
     hipStream_t st[PLAN_STREAMS] = {S(main_stream), S(side_stream ? side_stream : main_stream),
                                     S(comm_stream ? comm_stream : main_stream)};
+    if (perturb == 1) st[1] = st[2] = st[0];   // sequential: plan order on one stream
+    ++prun;
     int bad_op = -1;
     hipError_t bad = hipSuccess;
     // Never while capturing a hipGraph: capture from several host threads is not
@@ -812,6 +847,8 @@ PYBIND11_MODULE(_C, m) {
       .def("run", &Plan::run, py::arg("begin"), py::arg("end"), py::arg("stream"),
            py::arg("side_stream") = 0, py::arg("comm_stream") = 0)
       .def("size", &Plan::size)
+      .def("set_perturb", &Plan::set_perturb, py::arg("mode"), py::arg("seed") = 0,
+           py::arg("prob") = 0.0, py::arg("max_us") = 0.0)
       .def("new_event", &Plan::new_event)
       .def("record", &Plan::record)
       .def("wait", &Plan::wait)
@@ -916,6 +953,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "l2_half_sum", mk_l2_half_sum);
   def_op(m, plan, "fill", mk_fill);
   def_op(m, plan, "memset", mk_memset);
+  def_op(m, plan, "delay", mk_delay);
   def_op(m, plan, "cifar_augment", mk_cifar_augment);
   def_op(m, plan, "imagenet_u8_pack", mk_imagenet_u8_pack);
   def_op(m, plan, "pad_channels", mk_pad_channels);

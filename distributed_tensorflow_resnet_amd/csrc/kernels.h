@@ -137,6 +137,7 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
 bool conv_gemm_abwd_covers(const GemmArgs& a);   // generic dgrad with the fused BN backward
 void set_direct_probe(long long* p);   // per-workgroup phase stamps of the direct conv (diag)
+void plan_delay(long long ticks, hipStream_t s);   // spin one wave for ticks x 10 ns (diag.hip)
 void set_conv_direct(int enabled);
 void set_conv_wide_tile(int mask);     // 128x64 tiles for > 64 output columns (experiment)
 void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loops (DTR_CONV_PIPE)

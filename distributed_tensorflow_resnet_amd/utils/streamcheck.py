@@ -11,9 +11,13 @@ detection": stream-ordering asserts around comm/compute events; the reference
 has none -- its only checks are graph asserts,
 `/root/reference/vgg_preprocessing.py:67-84`, `cifar_input.py:110-115`).
 
-It is a check of the fork/join STRUCTURE, with happens-before computed by
-vector clocks over the three streams; it does not know which buffers an op
-reads or writes, so its rules are stated conservatively in terms of "all work
+It is a check of the fork/join STRUCTURE only, with happens-before computed by
+vector clocks over the three streams.  It does not know which buffers an op
+reads or writes.  For example, a side-stream op that reads a buffer the main
+stream rewrites after the side stream's last fork passes R2.  Buffer-level races
+are the job of the dynamic check in utils/racecheck.py: it runs the plan under
+randomly perturbed schedules and compares the state bitwise against plan order
+on one stream.  The rules below are stated conservatively in terms of "all work
 queued earlier".  Rules, per segment (a range of ops the host runs with one
 `Plan.run` call):
 

@@ -46,7 +46,9 @@ def _eval(device, data, td, ed):
     evs = records.read_events(glob.glob(os.path.join(ed, "events.out.tfevents.*"))[0])
     best = [e for e in evs if "Best_Precision" in e["scalars"]]
     assert best and best[-1]["step"] == STEPS
-    return float(m.group(1)), best[-1]["scalars"]["Best_Precision"]
+    prec = best[-1]["scalars"]["Precision"]   # the event's fp32 value (stdout rounds to 3 digits)
+    assert abs(prec - float(m.group(1))) < 1e-3
+    return prec, best[-1]["scalars"]["Best_Precision"]
 
 
 def test_resnet20_gpu_bf16_matches_cpu_fp32_on_learnable_task(gpu, tmp_path):
