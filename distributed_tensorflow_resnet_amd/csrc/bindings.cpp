@@ -201,6 +201,46 @@ static Launch mk_conv_wgrad(ptr_t dy, ptr_t x, ptr_t pre_scale, ptr_t pre_shift,
   return [w](hipStream_t s) { conv_wgrad(w, s); };
 }
 
+// Same-shape weight gradients of several layers: one grouped direct launch when the
+// direct kernel covers the shape, else one conv_wgrad per member.
+static Launch mk_conv_wgrad_group(std::vector<ptr_t> dy, std::vector<ptr_t> x,
+                                  std::vector<ptr_t> pre_scale, std::vector<ptr_t> pre_shift,
+                                  std::vector<ptr_t> part, std::vector<int> geom, int splits,
+                                  int px_per_split) {
+  const size_t n = dy.size();
+  if (n < 1 || n > (size_t)WGRAD_GROUP_MAX || x.size() != n || pre_scale.size() != n ||
+      pre_shift.size() != n || part.size() != n)
+    throw std::invalid_argument("conv_wgrad_group: 1..8 members, equal-length operand lists");
+  std::vector<WgradArgs> ws;
+  WgradGroup grp{};
+  grp.n = (int)n;
+  for (size_t i = 0; i < n; ++i) {
+    WgradArgs w{};
+    w.dy = P<const bf16>(dy[i]);
+    w.x = P<const bf16>(x[i]);
+    w.pre_scale = P<const float>(pre_scale[i]);
+    w.pre_shift = P<const float>(pre_shift[i]);
+    w.part = P<float>(part[i]);
+    w.g = geom_from(geom);
+    w.splits = splits;
+    w.px_per_split = px_per_split;
+    if (w.g.C % 8 || w.g.K % 16) throw std::invalid_argument("wgrad: C%8 and K%16 required");
+    if (px_per_split % 64) throw std::invalid_argument("wgrad: px_per_split % 64");
+    if ((pre_scale[i] != 0) != (pre_scale[0] != 0))
+      throw std::invalid_argument("conv_wgrad_group: members must all (or none) fuse BN+ReLU");
+    grp.dy[i] = w.dy;
+    grp.x[i] = w.x;
+    grp.scale[i] = w.pre_scale;
+    grp.shift[i] = w.pre_shift;
+    grp.part[i] = w.part;
+    ws.push_back(w);
+  }
+  return [ws, grp](hipStream_t s) {
+    if (ws.size() > 1 && conv_wgrad_direct_group(ws[0], grp, s)) return;
+    for (const auto& w : ws) conv_wgrad(w, s);
+  };
+}
+
 static Launch mk_wgrad_reduce(ptr_t part, ptr_t grad, int splits, int K, int K_valid, int taps,
                               int C, int C_valid, float scale, int accumulate) {
   return [=](hipStream_t s) {
@@ -926,6 +966,7 @@ PYBIND11_MODULE(_C, m) {
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);
   def_op(m, plan, "conv_wgrad", mk_conv_wgrad);
+  def_op(m, plan, "conv_wgrad_group", mk_conv_wgrad_group);
   def_op(m, plan, "wgrad_reduce", mk_wgrad_reduce);
   def_op(m, plan, "wgrad_reduce_grouped", mk_wgrad_reduce_grouped);
   def_op(m, plan, "bn_finalize", mk_bn_finalize);

@@ -31,7 +31,7 @@ namespace dtr {
 
 template <int C, int KO, int WI, int HI, int BMP, int TJ, bool PRE>
 __global__ void __launch_bounds__(256)
-conv_wgrad_direct_kernel(WgradArgs args) {
+conv_wgrad_direct_kernel(WgradArgs args, WgradGroup grp) {
   constexpr int HW = HI * WI;
   constexpr int NIMG = BMP >= HW ? BMP / HW : 1;
   constexpr int RH = BMP >= HW ? HI : BMP / WI;       // rows per image in the tile
@@ -54,6 +54,14 @@ conv_wgrad_direct_kernel(WgradArgs args) {
   bf16* halo = dys + BMP * KO;                                // [NIMG][RH+2][W2][C]
   float* pre_s = reinterpret_cast<float*>(halo + HU * 8);     // [2][C]
 
+  if (grp.n > 0) {   // grouped launch: this workgroup's member (uniform)
+    const int z = blockIdx.z;
+    args.dy = grp.dy[z];
+    args.x = grp.x[z];
+    args.pre_scale = grp.scale[z];
+    args.pre_shift = grp.shift[z];
+    args.part = grp.part[z];
+  }
   const int split = blockIdx.x, tj = blockIdx.y;
   const int p0 = split * BMP;                                 // first pixel of the tile
   const int img0 = p0 / HW, h0 = (p0 - img0 * HW) / WI;       // h0 = 0 for whole images
@@ -173,7 +181,7 @@ conv_wgrad_direct_kernel(WgradArgs args) {
 
 // (C, W, H, BMP, TJ) variants; BMP pixels per split, TJ taps per workgroup.
 template <int C, int WI, int HI, int BMP, int TJ>
-static void wgd_launch(const WgradArgs& a, hipStream_t s) {
+static void wgd_launch(const WgradArgs& a, hipStream_t s, const WgradGroup& grp = WgradGroup{}) {
   constexpr int NIMG = BMP >= HI * WI ? BMP / (HI * WI) : 1;
   constexpr int RH = BMP >= HI * WI ? HI : BMP / WI;
   constexpr size_t MAIN = (size_t)BMP * C * 2 + (size_t)NIMG * (RH + 2) * (WI + 2) * C * 2 +
@@ -181,13 +189,13 @@ static void wgd_launch(const WgradArgs& a, hipStream_t s) {
   constexpr int WK = 4 / (C / 16);
   constexpr size_t RED = (size_t)WK * C * TJ * C * sizeof(float);
   const size_t lds = ((MAIN > RED ? MAIN : RED) + 15) & ~(size_t)15;
-  dim3 grid(a.splits, 9 / TJ);
+  dim3 grid(a.splits, 9 / TJ, grp.n > 0 ? grp.n : 1);
   if (a.pre_scale)
     hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, true>), grid, dim3(256),
-                       lds, s, a);
+                       lds, s, a, grp);
   else
     hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, false>), grid,
-                       dim3(256), lds, s, a);
+                       dim3(256), lds, s, a, grp);
   DTR_CHECK_LAUNCH();
 }
 
@@ -255,29 +263,40 @@ int wgrad_direct_bmp(const ConvGeom& g) {
   return bmp;
 }
 
-bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) {
+static bool wgd_dispatch(const WgradArgs& a, hipStream_t s, const WgradGroup& grp) {
   const int bmp = wgrad_direct_bmp(a.g);
   if (bmp == 0 || a.px_per_split != bmp) return false;
   const ConvGeom& g = a.g;
   const int tj = wgd_taps(g, bmp);
   if (g.C == 16) {
-    if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s);
-    else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s);
-    else if (bmp == 256) wgd_launch<16, 32, 32, 256, 9>(a, s);
-    else wgd_launch<16, 32, 32, 128, 9>(a, s);
+    if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s, grp);
+    else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s, grp);
+    else if (bmp == 256) wgd_launch<16, 32, 32, 256, 9>(a, s, grp);
+    else wgd_launch<16, 32, 32, 128, 9>(a, s, grp);
   } else if (g.C == 32) {
-    if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s);
-    else if (bmp == 256) wgd_launch<32, 16, 16, 256, 3>(a, s);
-    else if (bmp == 128) wgd_launch<32, 16, 16, 128, 3>(a, s);
-    else if (tj == 3) wgd_launch<32, 16, 16, 64, 3>(a, s);
-    else wgd_launch<32, 16, 16, 64, 1>(a, s);
+    if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s, grp);
+    else if (bmp == 256) wgd_launch<32, 16, 16, 256, 3>(a, s, grp);
+    else if (bmp == 128) wgd_launch<32, 16, 16, 128, 3>(a, s, grp);
+    else if (tj == 3) wgd_launch<32, 16, 16, 64, 3>(a, s, grp);
+    else wgd_launch<32, 16, 16, 64, 1>(a, s, grp);
   } else {
-    if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s);
-    else if (bmp == 128) wgd_launch<64, 8, 8, 128, 3>(a, s);
-    else if (tj == 3) wgd_launch<64, 8, 8, 64, 3>(a, s);
-    else wgd_launch<64, 8, 8, 64, 1>(a, s);
+    if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s, grp);
+    else if (bmp == 128) wgd_launch<64, 8, 8, 128, 3>(a, s, grp);
+    else if (tj == 3) wgd_launch<64, 8, 8, 64, 3>(a, s, grp);
+    else wgd_launch<64, 8, 8, 64, 1>(a, s, grp);
   }
   return true;
+}
+
+bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) { return wgd_dispatch(a, s, WgradGroup{}); }
+
+// All members share a's geometry and split layout and either all or none carry the
+// fused BN+ReLU of x (the PRE template flag comes from a.pre_scale).
+bool conv_wgrad_direct_group(const WgradArgs& a, const WgradGroup& grp, hipStream_t s) {
+  if (grp.n < 1 || grp.n > WGRAD_GROUP_MAX) return false;
+  for (int i = 0; i < grp.n; ++i)
+    if ((grp.scale[i] != nullptr) != (a.pre_scale != nullptr)) return false;
+  return wgd_dispatch(a, s, grp);
 }
 
 }  // namespace dtr

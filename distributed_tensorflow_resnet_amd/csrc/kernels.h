@@ -159,6 +159,18 @@ struct WgradArgs {
 void conv_wgrad(const WgradArgs& a, hipStream_t s);
 // Direct halo-tiled wgrad for 3x3/s1 small C (conv_wgrad_direct.hip).
 bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s);
+// Several same-shape direct wgrads in ONE launch (blockIdx.z = member): the
+// operands of member z replace a's dy / x / pre_scale / pre_shift / part.
+constexpr int WGRAD_GROUP_MAX = 8;
+struct WgradGroup {
+  int n = 0;
+  const bf16* dy[WGRAD_GROUP_MAX];
+  const bf16* x[WGRAD_GROUP_MAX];
+  const float* scale[WGRAD_GROUP_MAX];
+  const float* shift[WGRAD_GROUP_MAX];
+  float* part[WGRAD_GROUP_MAX];
+};
+bool conv_wgrad_direct_group(const WgradArgs& a, const WgradGroup& grp, hipStream_t s);
 int wgrad_direct_bmp(const ConvGeom& g);   // pixels per split, 0 = not covered
 void set_wgrad_direct(int enabled);
 // grad[tap][ci][co] (+)= scale * sum_s part[s][co][tap*C+ci] for co < K_valid, ci < C_valid

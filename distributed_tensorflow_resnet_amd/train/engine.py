@@ -183,6 +183,14 @@ class Engine:
             # handles the cross-stream event edges poorly); graphs stay single-stream
             fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
         self.fork_every = max(1, int(os.environ.get("DTR_FORK_EVERY", "2")))
+        # same-shape weight gradients per grouped launch (_emit_wgrads; 1 = ungrouped).
+        # Default 1, measured (CIFAR RN50 step, ms): bs16 0.958 ungrouped vs 0.987 / 0.978
+        # / 0.983 grouping 2 / 8 stage-1 only / 8 all; bs128 1.298 vs 1.296-1.306.  The
+        # grouped launch does shorten the side stream's tail (4 layers in one 5-7 us
+        # kernel), but its 4x wider grids delay the main stream's critical dgrads.
+        self.wgrad_group = min(8, max(1, int(os.environ.get("DTR_WGRAD_GROUP", "1"))))
+        # which input-channel counts group (bit 0: 16, 1: 32, 2: 64, 3: others; -1 all)
+        self.wgrad_group_cmask = int(os.environ.get("DTR_WGRAD_GROUP_C", "-1"))
         self.markers = os.environ.get("DTR_ROCTX", "0") != "0"
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
@@ -687,15 +695,12 @@ class Engine:
         off, sp, pps = self.wg_off[s.name]
         part = self.wg_part.data_ptr() + 4 * off
 
-        def emit(plan=plan, dy=dy, x=x, pre=pre, part=part, geom=geom, sp=sp, pps=pps):
-            if "wgrad" not in _DIAG_SKIP:   # diagnostics only (scripts/diag_step.py)
-                plan.conv_wgrad(dy.data_ptr(), x.data_ptr(),
-                                0 if pre is None else pre.scale.data_ptr(),
-                                0 if pre is None else pre.shift.data_ptr(), part, geom, sp, pps)
+        desc = (dy.data_ptr(), x.data_ptr(), 0 if pre is None else pre.scale.data_ptr(),
+                0 if pre is None else pre.shift.data_ptr(), part, tuple(geom), sp, pps)
         if self.fork_wgrad and side:
-            self._side_q.append(emit)
+            self._side_q.append(desc)
         else:
-            emit()
+            self._emit_wgrads(plan, [desc])
             # a side-stream reduce of this slab must fork after it (_flush_side)
             self._main_wgrad = self.fork_wgrad
         self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
@@ -757,10 +762,43 @@ class Engine:
         plan.record(ev)
         plan.use_stream(1)
         plan.wait(ev)
-        for emit in self._side_q:
-            emit()
+        self._emit_wgrads(plan, self._side_q)
         plan.use_stream(0)
         self._side_q, self._side_blocks = [], 0
+
+    def _emit_wgrads(self, plan, descs):
+        """Weight-gradient launches on the current stream.  Runs of same-shape layers
+        (the residual blocks of a stage, queued together by _flush_side) go out as
+        ONE grouped launch (`conv_wgrad_group`, up to `wgrad_group` members): at 16-32
+        images per rank a CIFAR wgrad is a 4-6 us kernel, and its launch boundary cost
+        as much again on the side stream, which then trailed the backward pass."""
+        i = 0
+        while i < len(descs):
+            if callable(descs[i]):   # a queued non-wgrad side op (head reduce, dense wgrad)
+                descs[i]()
+                i += 1
+                continue
+            if "wgrad" in _DIAG_SKIP:   # diagnostics only (scripts/diag_step.py)
+                i += 1
+                continue
+            key = descs[i][5:] + (descs[i][2] != 0,)
+            j = i + 1
+            while (j < len(descs) and j - i < self.wgrad_group and not callable(descs[j])
+                   and descs[j][5:] + (descs[j][2] != 0,) == key):
+                j += 1
+            if self.wgrad_group_cmask >= 0 and not (
+                    self.wgrad_group_cmask >> {16: 0, 32: 1, 64: 2}.get(descs[i][5][3], 3) & 1):
+                j = i + 1   # this channel count stays ungrouped (DTR_WGRAD_GROUP_C)
+            run = descs[i:j]
+            geom, sp, pps = list(run[0][5]), run[0][6], run[0][7]
+            if len(run) == 1:
+                d = run[0]
+                plan.conv_wgrad(d[0], d[1], d[2], d[3], d[4], geom, sp, pps)
+            else:
+                plan.conv_wgrad_group([d[0] for d in run], [d[1] for d in run],
+                                      [d[2] for d in run], [d[3] for d in run],
+                                      [d[4] for d in run], geom, sp, pps)
+            i = j
 
     def _flush_buckets(self, plan, force: bool = False):
         """Emit the grouped split-K reduce of every reduce group whose gradients are

@@ -595,3 +595,33 @@ def test_gemm_dgrad_fused_bn_backward(gpu, N, H, Cin, K, k, s, bnb, monkeypatch)
     assert _rel(dx, dx2) < 5e-3
     if bnb:
         assert _rel(bpart_a, bpart_b) < 5e-3
+
+
+@pytest.mark.parametrize("N,H,C,pre", [(16, 32, 16, True), (16, 16, 32, False), (128, 8, 64, True),
+                                       (32, 16, 32, True)])
+def test_grouped_direct_wgrad_equals_per_layer(gpu, N, H, C, pre):
+    """conv_wgrad_group: several same-shape layers' direct wgrads in ONE launch
+    (blockIdx.z = layer) write exactly the slabs the per-layer launches write."""
+    torch.manual_seed(16)
+    nat = fn.native()
+    geom = [N, H, H, C, H, H, C, 3, 3, 1, 1]
+    sp, pps = nat.wgrad_pick_splits(geom)
+    G = 3
+    xs = [torch.randn(N, H, H, C, device=gpu).to(BF) for _ in range(G)]
+    dys = [torch.randn(N, H, H, C, device=gpu).to(BF) for _ in range(G)]
+    scs = [torch.rand(C, device=gpu) + 0.5 for _ in range(G)]
+    shs = [torch.randn(C, device=gpu) * 0.3 for _ in range(G)]
+    n = sp * C * 9 * C
+    one = torch.full((G, n), 7.0, device=gpu)
+    grp = torch.full((G, n), -7.0, device=gpu)
+    st = fn._stream()
+    for i in range(G):
+        nat.conv_wgrad(dys[i].data_ptr(), xs[i].data_ptr(), scs[i].data_ptr() if pre else 0,
+                       shs[i].data_ptr() if pre else 0, one[i].data_ptr(), geom, sp, pps, st)
+    nat.conv_wgrad_group([d.data_ptr() for d in dys], [x.data_ptr() for x in xs],
+                         [s.data_ptr() if pre else 0 for s in scs],
+                         [s.data_ptr() if pre else 0 for s in shs],
+                         [grp[i].data_ptr() for i in range(G)], geom, sp, pps, st)
+    torch.cuda.synchronize()
+    assert torch.equal(one, grp)
+    assert torch.isfinite(grp).all()
