@@ -1047,6 +1047,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);
   m.def("softmax_xent_ws_floats", &softmax_xent_ws_floats);
+  m.def("wgrad_reduce_chunks", &wgrad_reduce_chunks, py::arg("splits"), py::arg("K"),
+        py::arg("taps"), py::arg("C"),
+        "work chunks of one conv's slabs in wgrad_reduce_grouped (its desc's chunk0 stride)");
   m.def("wgrad_pick_splits", [](std::vector<int> geom) {
     int pps = 0;
     const int sp = wgrad_pick_splits(geom_from(geom), &pps);

@@ -582,9 +582,32 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
 
 static int g_xcd_swz = -1;   // DTR_XCD_SWZ: 0 off, 1 on (default: see launch_cfg)
 
+static int g_nbuf1 = -1;   // DTR_NBUF1_KT: single-buffered LDS when the K loop has <= this many tiles
+
+template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
+static void launch_nbuf(const GemmArgs& a0, hipStream_t s);
+
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS>
-static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
-  constexpr int NBUF = 2;   // 1 measured neutral on the ImageNet 128x128 tiles
+static void launch_cfg(const GemmArgs& a, hipStream_t s) {
+  // A one-tile K loop (the 64-channel 1x1 convs: 4 forward + 4 dgrad launches of the
+  // ImageNet 56x56 stage) double-buffers nothing: one LDS buffer halves the main-loop
+  // LDS, so the 128x128 tiles fit 4 workgroups per CU instead of 2 and the
+  // load -> MFMA -> epilogue phases of co-resident workgroups overlap.
+  if (g_nbuf1 < 0) {
+    const char* e = std::getenv("DTR_NBUF1_KT");
+    g_nbuf1 = e ? std::atoi(e) : 1;
+  }
+  if constexpr (BM * BN >= 128 * 64 && (FLAGS & F_ABWD) == 0) {
+    if ((a.Kdim + 63) / 64 <= g_nbuf1 && !conv_gemm_fast(a, MODE)) {
+      launch_nbuf<BM, BN, WM, WN, MODE, FLAGS, 1>(a, s);
+      return;
+    }
+  }
+  launch_nbuf<BM, BN, WM, WN, MODE, FLAGS, 2>(a, s);
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
+static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
   if (g_xcd_swz < 0) {
     const char* e = std::getenv("DTR_XCD_SWZ");
     g_xcd_swz = e ? std::atoi(e) : 0;
@@ -601,27 +624,33 @@ static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
   // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles; the
   // fused BN backward (ABWD) exists only there
-  if constexpr ((FLAGS & F_ABWD) != 0) {
-    if constexpr (BN >= 64) {
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
-                         dim3(256), lds, s, a);
-      DTR_CHECK_LAUNCH();
-    } else {
-      throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
-    }
-    return;
-  }
-  if constexpr (BN >= 64) {
-    if (conv_gemm_fast(a, MODE)) {
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
-                         dim3(256), lds, s, a);
-      DTR_CHECK_LAUNCH();
+  if constexpr (NBUF == 1) {   // general loop only (launch_cfg: one-tile K loops)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, 1>), grid,
+                       dim3(256), lds, s, a);
+    DTR_CHECK_LAUNCH();
+  } else {
+    if constexpr ((FLAGS & F_ABWD) != 0) {
+      if constexpr (BN >= 64) {
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
+                           dim3(256), lds, s, a);
+        DTR_CHECK_LAUNCH();
+      } else {
+        throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
+      }
       return;
     }
+    if constexpr (BN >= 64) {
+      if (conv_gemm_fast(a, MODE)) {
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
+                           dim3(256), lds, s, a);
+        DTR_CHECK_LAUNCH();
+        return;
+      }
+    }
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, NBUF>), grid,
+                       dim3(256), lds, s, a);
+    DTR_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, NBUF>), grid,
-                     dim3(256), lds, s, a);
-  DTR_CHECK_LAUNCH();
 }
 
 template <int BM, int BN, int WM, int WN, int MODE>
@@ -665,7 +694,16 @@ int conv_gemm_bm(int M, int nc) {
   if (nc <= 16) return m >= 256L * 512 ? b16 : 64;
   if (nc <= 32) return m >= 128L * 512 ? b32 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
-  return (m >= 128L * 128 && nc % 128 == 0) ? 128 : 64;
+  // DTR_BM128_MIN: rows from which the 128x128 tile is used.  Default 4096: the
+  // 7x7 stage (6272 rows) too -- its 64x64 grids re-read A and B 2x more from L2 /
+  // HBM (measured, bench_kernels.py: 7x7 fwd 118 -> 87 / 59 -> 46 us, dgrad 93 -> 84
+  // / 40 -> 33 us despite 196 tiles for 256 CUs; ImageNet RN50 step -0.6 %)
+  static long min128 = -1;
+  if (min128 < 0) {
+    const char* e = std::getenv("DTR_BM128_MIN");
+    min128 = e ? std::atol(e) : 4096;
+  }
+  return (m >= min128 && nc % 128 == 0) ? 128 : 64;
 }
 
 int conv_gemm_bn(int M, int nc) {

@@ -532,16 +532,34 @@ void wgrad_reduce(const float* part, float* grad_hwio, int splits, int K, int K_
 }
 
 // Grouped split-K reduction: ONE launch reduces the partial slabs of many
-// convolutions (all convs of a gradient bucket).  Work unit = WGR_COLS (256)
-// consecutive slab columns of one conv; a block finds its conv by binary search
-// over the descriptors' first-chunk offsets.  256 threads = 64 column groups of 4
-// (16-byte slab loads) x 4 split rows; the 4 row sums are combined in LDS in fixed
-// order (deterministic).  The ImageNet step reduces ~1.6 GB of slabs here: the
-// previous 4-byte-per-thread form ran at ~1 TB/s.
+// convolutions (all convs of a gradient bucket); a block finds its conv by binary
+// search over the descriptors' first-chunk offsets.  Two work-unit shapes, chosen
+// per conv by its split count (wgrad_reduce_chunks must match):
+//   deep (> WGR_WIDE_MAX splits: the many-pixel, small-weight layers): 256
+//     consecutive slab columns; 64 column groups of 4 (16-byte loads) x 4 split
+//     rows, the 4 row sums combined in LDS in fixed order;
+//   wide (few splits, large weights: the 14x14 / 7x7 stages): a 16 (co) x 64 (tap,
+//     ci) tile, every thread summing all splits of its 4 columns with the loads in
+//     flight together, then transposed through LDS so the HWIO gradient is written
+//     as 64-byte co runs instead of one float per co row (measured: the deep form ran
+//     the 3-split 28 MB slab of the 7x7 3x3 layer at 1.6 TB/s, half of a plain
+//     torch.sum over the same bytes).
+// Both sum the splits in a fixed order: deterministic.
 constexpr int WGR_COLS = 256;
+constexpr int WGR_WIDE_MAX = 8;
+__host__ __device__ inline long long wgrad_reduce_chunks_of(int splits, int K, int taps, int C) {
+  const long long NT = (long long)taps * C;
+  if (splits <= WGR_WIDE_MAX) return ((K + 15) / 16) * ((NT + 63) / 64);
+  return ((long long)K * NT + WGR_COLS - 1) / WGR_COLS;
+}
+
+long long wgrad_reduce_chunks(int splits, int K, int taps, int C) {
+  return wgrad_reduce_chunks_of(splits, K, taps, C);
+}
+
 __global__ void __launch_bounds__(256)
 wgrad_reduce_grouped_kernel(const WgReduceDesc* __restrict__ d, int nd, float scale) {
-  __shared__ f32x4 red[4][64];
+  __shared__ __attribute__((aligned(16))) float lds[64 * 17];
   const long chunk = blockIdx.x;
   int lo = 0, hi = nd - 1;
   while (lo < hi) {
@@ -552,7 +570,50 @@ wgrad_reduce_grouped_kernel(const WgReduceDesc* __restrict__ d, int nd, float sc
   const WgReduceDesc& q = d[lo];
   const long NT = (long)q.taps * q.C;
   const long total = (long)q.K * NT;           // multiple of 8 (C % 8 == 0)
-  const int cg = threadIdx.x & 63, sr = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  if (q.splits <= WGR_WIDE_MAX) {
+    const long ntn = (NT + 63) / 64;
+    const long local = chunk - q.chunk0;
+    const int co0 = (int)(local / ntn) * 16;
+    const long n0 = (local % ntn) * 64;
+    const int r = tid >> 4, c4 = (tid & 15) * 4;
+    const int co = co0 + r;
+    const long n = n0 + c4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (co < q.K && n < NT) {   // NT % 8 == 0: the 4 columns are all in range
+      const float* src = q.part + (long)co * NT + n;
+      f32x4 v[WGR_WIDE_MAX];
+#pragma unroll
+      for (int sp = 0; sp < WGR_WIDE_MAX; ++sp)
+        if (sp < q.splits) v[sp] = *reinterpret_cast<const f32x4*>(src + (long)sp * total);
+#pragma unroll
+      for (int sp = 0; sp < WGR_WIDE_MAX; ++sp)
+        if (sp < q.splits) acc += v[sp];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lds[(c4 + j) * 17 + r] = acc[j];
+    __syncthreads();
+    const int nl = tid >> 2, cq = (tid & 3) * 4;
+    const long nn = n0 + nl;
+    if (nn < NT) {
+      const long tap = nn / q.C, ci = nn - tap * q.C;
+      if (ci < q.Cv) {
+        float* dst = q.grad + (tap * q.Cv + ci) * q.Kv + co0 + cq;
+        const float* t = lds + nl * 17 + cq;
+        if ((q.Kv & 3) == 0 && co0 + cq + 3 < q.Kv) {
+          *reinterpret_cast<f32x4*>(dst) = f32x4{t[0] * scale, t[1] * scale, t[2] * scale,
+                                                 t[3] * scale};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co0 + cq + j < q.Kv) dst[j] = t[j] * scale;
+        }
+      }
+    }
+    return;
+  }
+  f32x4* red = reinterpret_cast<f32x4*>(lds);  // [4][64]
+  const int cg = tid & 63, sr = tid >> 6;
   const long idx = (chunk - q.chunk0) * WGR_COLS + cg * 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (idx < total) {
@@ -561,10 +622,10 @@ wgrad_reduce_grouped_kernel(const WgReduceDesc* __restrict__ d, int nd, float sc
     for (int sp = sr; sp < q.splits; sp += 4)
       acc += *reinterpret_cast<const f32x4*>(src + (long)sp * total);
   }
-  red[sr][cg] = acc;
+  red[sr * 64 + cg] = acc;
   __syncthreads();
   if (sr == 0 && idx < total) {
-    const f32x4 a = red[0][cg] + red[1][cg] + red[2][cg] + red[3][cg];
+    const f32x4 a = red[cg] + red[64 + cg] + red[128 + cg] + red[192 + cg];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long e = idx + j;

@@ -187,6 +187,8 @@ struct WgReduceDesc {      // one convolution's split-K slabs -> its HWIO gradie
 };
 void wgrad_reduce_grouped(const WgReduceDesc* descs_dev, int nd, long long total_chunks,
                           float scale, hipStream_t s);
+// work chunks of one conv in a grouped reduce (its desc's chunk0 advances by this)
+long long wgrad_reduce_chunks(int splits, int K, int taps, int C);
 
 // ---- BatchNorm (training mode, TF fused semantics) ----
 void bn_finalize(const float* stat_part, int tiles, int tile_rows, int M, int C,

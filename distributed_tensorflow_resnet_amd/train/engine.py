@@ -870,7 +870,7 @@ class Engine:
         chunk = 0
         for i, (part, grad, sp, K, Kv, taps, C, Cv) in enumerate(descs):
             arr[i] = (part, grad, sp, K, Kv, taps, C, Cv, chunk)
-            chunk += _ceil(K * taps * C, 256)   # WGR_COLS (conv_wgrad.hip)
+            chunk += self.nat.wgrad_reduce_chunks(sp, K, taps, C)
         t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
         self._keep.append(t)
         plan.use_stream(1 if self.fork_wgrad else 0)

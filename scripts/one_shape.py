@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Run one conv shape's fwd / dgrad / wgrad kernels a few times (for rocprofv3 --pmc
+passes on a single kernel).  usage: one_shape.py N H C K k s [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from distributed_tensorflow_resnet_amd.ops import functional as fn  # noqa: E402
+
+
+def main():
+    N, H, C, K, k, s = (int(v) for v in sys.argv[1:7])
+    reps = int(sys.argv[7]) if len(sys.argv) > 7 else 5
+    dev = torch.device("cuda")
+    g = fn.ConvGeom(N, H, H, C, K, k, k, s)
+    x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, k, k, C, device=dev) * 0.05).to(torch.bfloat16)
+    whwio = w.permute(1, 2, 3, 0).contiguous()
+    sc = torch.rand(C, device=dev) + 0.5
+    sh = torch.randn(C, device=dev) * 0.1
+    dy = torch.randn(N, g.Ho, g.Wo, K, device=dev).to(torch.bfloat16)
+    tiles, _ = fn.stat_tiles(N * g.Ho * g.Wo, K)
+    part = torch.empty(tiles * 2 * K, device=dev)
+    out = torch.empty(N, g.Ho, g.Wo, K, device=dev, dtype=torch.bfloat16)
+    dx = torch.empty_like(x)
+    gw = torch.empty(k, k, C, K, device=dev)
+    for _ in range(reps):
+        fn.conv2d_fwd(x, w, s, stat_part=part, out=out, pre_scale=sc, pre_shift=sh)
+        fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx)
+        fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc, pre_shift=sh)
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

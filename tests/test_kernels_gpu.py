@@ -625,3 +625,35 @@ def test_grouped_direct_wgrad_equals_per_layer(gpu, N, H, C, pre):
     torch.cuda.synchronize()
     assert torch.equal(one, grp)
     assert torch.isfinite(grp).all()
+
+
+def test_grouped_wgrad_reduce_wide_and_deep(gpu):
+    """wgrad_reduce_grouped over convs of both work-unit shapes (few splits: the
+    transposed 16x64 tile; many: the 256-column split-row form), with padded output
+    (Kv < K) and input (Cv < C) channels dropped, == sum over splits in HWIO."""
+    import numpy as np
+
+    from distributed_tensorflow_resnet_amd.train.engine import WGD_DTYPE
+
+    torch.manual_seed(17)
+    nat = fn.native()
+    cases = [(3, 512, 9, 512, 512, 512), (1, 64, 1, 256, 64, 256), (8, 32, 9, 24, 20, 24),
+             (96, 64, 1, 256, 64, 256), (12, 16, 9, 8, 10, 3), (5, 1024, 1, 2048, 1001, 2048)]
+    parts, grads, refs = [], [], []
+    arr = np.zeros(len(cases), dtype=WGD_DTYPE)
+    chunk = 0
+    for i, (sp, K, taps, C, Kv, Cv) in enumerate(cases):
+        p = torch.randn(sp, K, taps * C, device=gpu)
+        g = torch.full((taps, Cv, Kv), 7.0, device=gpu)
+        ref = p.double().sum(0).view(K, taps, C)[:Kv, :, :Cv].permute(1, 2, 0) * 0.5
+        parts.append(p)
+        grads.append(g)
+        refs.append(ref)
+        arr[i] = (p.data_ptr(), g.data_ptr(), sp, K, Kv, taps, C, Cv, chunk)
+        chunk += nat.wgrad_reduce_chunks(sp, K, taps, C)
+    t = torch.from_numpy(arr.view(np.uint8).copy()).to(gpu)
+    nat.wgrad_reduce_grouped(t.data_ptr(), len(cases), chunk, 0.5, fn._stream())
+    torch.cuda.synchronize()
+    for (sp, K, taps, C, Kv, Cv), g, r in zip(cases, grads, refs):
+        torch.testing.assert_close(g.double(), r, rtol=1e-5, atol=1e-5 * sp ** 0.5,
+                                   msg=lambda m: f"{(sp, K, taps, C, Kv, Cv)}: {m}")
