@@ -399,7 +399,7 @@ bool conv_direct_covers(const GemmArgs& a, int mode) {
   const int bm = conv_gemm_bm(a.M, a.Ncol);
   const int hw = g.H * g.W;
   if (bm % g.W != 0 || hw % bm != 0 || a.M % bm != 0) return false;
-  return (ca == 16 && g.W == 32 && (bm == 256 || bm == 64)) ||
+  return (ca == 16 && g.W == 32 && (bm == 256 || bm == 128 || bm == 64)) ||
          (ca == 32 && g.W == 16 && (bm == 128 || bm == 64)) ||
          (ca == 64 && g.W == 8 && bm == 64);
 }
@@ -432,6 +432,7 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
     DTR_DIRECT_BN(32, 16, 64, 16, 4, 1)
   }
   DTR_DIRECT(16, 32, 256, 4, 1)
+  DTR_DIRECT(16, 32, 128, 4, 1)
   DTR_DIRECT(16, 32, 64, 4, 1)
   DTR_DIRECT(32, 16, 128, 2, 2)
   DTR_DIRECT(32, 16, 64, 2, 2)

@@ -688,10 +688,19 @@ int conv_gemm_bm(int M, int nc) {
   if (b16 < 0) {
     b16 = 256, b32 = 128;
     if (const char* e = std::getenv("DTR_SMALLC_BM")) std::sscanf(e, "%d,%d", &b16, &b32);
-    if (b16 != 256 && b16 != 64) b16 = 256;
+    if (b16 != 256 && b16 != 128 && b16 != 64) b16 = 256;
     if (b32 != 128 && b32 != 64) b32 = 128;
   }
-  if (nc <= 16) return m >= 256L * 512 ? b16 : 64;
+  // DTR_C16_MID: rows from which (below 256 x 512) the 16-column convs use 128-row
+  // tiles.  Default 32768: the CIFAR stage-1 grids then stay near 2 workgroups per CU
+  // at 32-64 images (measured, CIFAR RN50 step: bs64 1.233 -> 1.08 ms, bs32 1.013 ->
+  // 1.004; bs16 keeps 64-row tiles, 256 workgroups: 0.953 vs 0.965 with 128)
+  static long mid16 = -2;
+  if (mid16 == -2) {
+    const char* e = std::getenv("DTR_C16_MID");
+    mid16 = e ? std::atol(e) : 32768;
+  }
+  if (nc <= 16) return m >= 256L * 512 ? b16 : (mid16 >= 0 && m >= mid16) ? 128 : 64;
   if (nc <= 32) return m >= 128L * 512 ? b32 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
   // DTR_BM128_MIN: rows from which the 128x128 tile is used.  Default 4096: the
@@ -735,6 +744,7 @@ static void launch_mode(const GemmArgs& a, hipStream_t s) {
   }
   if (nc <= 16) {
     if (bm == 256) launch_flags<256, 16, 4, 1, MODE>(a, s);
+    else if (bm == 128) launch_flags<128, 16, 4, 1, MODE>(a, s);   // DTR_SMALLC_BM sweeps
     else launch_flags<64, 16, 4, 1, MODE>(a, s);
   } else if (nc <= 32) {
     if (bm == 128) launch_flags<128, 32, 4, 1, MODE>(a, s);

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Run one conv shape's fwd / dgrad / wgrad kernels a few times (for rocprofv3 --pmc
-passes on a single kernel).  usage: one_shape.py N H C K k s [reps]"""
+passes on a single kernel).  usage: one_shape.py N H C K k s [reps] [passes]
+passes: comma list of fwd (pre+stats), fwd_plain, fwd_stats, dgrad, wgrad (default all 3)"""
 import os
 import sys
 
@@ -13,6 +14,7 @@ from distributed_tensorflow_resnet_amd.ops import functional as fn  # noqa: E402
 def main():
     N, H, C, K, k, s = (int(v) for v in sys.argv[1:7])
     reps = int(sys.argv[7]) if len(sys.argv) > 7 else 5
+    passes = (sys.argv[8] if len(sys.argv) > 8 else "fwd,dgrad,wgrad").split(",")
     dev = torch.device("cuda")
     g = fn.ConvGeom(N, H, H, C, K, k, k, s)
     x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
@@ -27,9 +29,16 @@ def main():
     dx = torch.empty_like(x)
     gw = torch.empty(k, k, C, K, device=dev)
     for _ in range(reps):
-        fn.conv2d_fwd(x, w, s, stat_part=part, out=out, pre_scale=sc, pre_shift=sh)
-        fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx)
-        fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc, pre_shift=sh)
+        if "fwd" in passes:
+            fn.conv2d_fwd(x, w, s, stat_part=part, out=out, pre_scale=sc, pre_shift=sh)
+        if "fwd_plain" in passes:
+            fn.conv2d_fwd(x, w, s, out=out)
+        if "fwd_stats" in passes:
+            fn.conv2d_fwd(x, w, s, stat_part=part, out=out)
+        if "dgrad" in passes:
+            fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx)
+        if "wgrad" in passes:
+            fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc, pre_shift=sh)
     torch.cuda.synchronize()
     print("ok", flush=True)
 
