@@ -701,7 +701,15 @@ int conv_gemm_bm(int M, int nc) {
     mid16 = e ? std::atol(e) : 32768;
   }
   if (nc <= 16) return m >= 256L * 512 ? b16 : (mid16 >= 0 && m >= mid16) ? 128 : 64;
-  if (nc <= 32) return m >= 128L * 512 ? b32 : 64;
+  // DTR_C32_MID: likewise for the 32-column convs.  Default 32768 (the stage-2 convs
+  // at 128 images: 256 instead of 512 workgroups, step 1.303 -> 1.273 ms; at 64
+  // images 128-row tiles measured 1.126 vs 1.088 ms, so smaller grids keep 64 rows)
+  static long mid32 = -2;
+  if (mid32 == -2) {
+    const char* e = std::getenv("DTR_C32_MID");
+    mid32 = e ? std::atol(e) : 32768;
+  }
+  if (nc <= 32) return m >= 128L * 512 ? b32 : (mid32 >= 0 && m >= mid32) ? 128 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
   // DTR_BM128_MIN: rows from which the 128x128 tile is used.  Default 4096: the
   // 7x7 stage (6272 rows) too -- its 64x64 grids re-read A and B 2x more from L2 /
