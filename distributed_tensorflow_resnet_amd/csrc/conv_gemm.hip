@@ -110,6 +110,10 @@ conv_gemm_kernel(GemmArgs args) {
 
   // ---- per-thread loader state (row decomposition is K-invariant) ----
   const int kg = tid & 7;  // fixed 16-B k-group of every chunk this thread stages
+  // 1x1 / stride 1 / no padding: output row m reads A row m (fwd and dgrad alike), so
+  // (a_base, h, w) = (m, 0, 0) -- no per-chunk integer divisions by H*W and W, which
+  // on the one-K-tile layers (64-channel 1x1) were a quarter of the kernel's VALU work
+  const bool pointwise = g.kh == 1 && g.kw == 1 && g.stride == 1 && g.pad == 0;
   int a_base[A_PER_T], a_h[A_PER_T], a_w[A_PER_T];
 #pragma unroll
   for (int i = 0; i < A_PER_T; ++i) {
@@ -119,7 +123,10 @@ conv_gemm_kernel(GemmArgs args) {
     a_h[i] = -(1 << 28);  // invalid row marker
     a_w[i] = 0;
     a_base[i] = 0;
-    if (q < A_CHUNKS && m < M) {
+    if (q < A_CHUNKS && m < M && pointwise) {
+      a_base[i] = m;
+      a_h[i] = 0;
+    } else if (q < A_CHUNKS && m < M) {
       if constexpr (MODE == MODE_FWD) {
         const int hw = g.Ho * g.Wo;
         const int n = m / hw, rem = m - n * hw;
