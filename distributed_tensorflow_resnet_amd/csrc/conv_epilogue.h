@@ -471,6 +471,31 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         }
       }
     }
+    // Pass 2: the stores, issued BEFORE the statistics' reductions: those end in
+    // lds_barrier()s, which wait for LDS only, so the stores drain while the column
+    // sums run (args.wt: write-through sc1 buffer stores, so the tile does not
+    // sit dirty in this XCD's L2 for the end-of-kernel release to write back)
+    if (!args.out_f32) {
+      if (args.wt) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.out, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) {
+          const int r = r0 + it * EL::RPP;
+          if (!colok || r >= nph) continue;
+          typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ob[it]), rs,
+                                                 (int)(((long)(prow0 + r) * NC + col0) * 2), 0,
+                                                 16);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) {
+          const int r = r0 + it * EL::RPP;
+          if (!colok || r >= nph) continue;
+          *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
+        }
+      }
+    }
     if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 5] = wall_clock64();
     if constexpr (STATS) {
       colsum8x2<EL::CPR, BN>(p1, p2, red, red2);
@@ -497,29 +522,6 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 6] = wall_clock64();
-    // Pass 2: the stores (args.wt: write-through sc1 buffer stores, so the tile does not
-    // sit dirty in this XCD's L2 for the end-of-kernel release to write back)
-    if (!args.out_f32) {
-      if (args.wt) {
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.out, 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int it = 0; it < RIT; ++it) {
-          const int r = r0 + it * EL::RPP;
-          if (!colok || r >= nph) continue;
-          typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ob[it]), rs,
-                                                 (int)(((long)(prow0 + r) * NC + col0) * 2), 0,
-                                                 16);
-        }
-      } else {
-#pragma unroll
-        for (int it = 0; it < RIT; ++it) {
-          const int r = r0 + it * EL::RPP;
-          if (!colok || r >= nph) continue;
-          *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
-        }
-      }
-    }
     // the next phase overwrites the tile (LDS-only: this phase's stores stay in flight)
     if constexpr (EL::PHASES > 1) lds_barrier();
   }

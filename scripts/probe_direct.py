@@ -3,7 +3,7 @@
 shapes: every workgroup stamps wall_clock64 (100 MHz) at start, operands staged in
 LDS, MFMAs done, and inside the epilogue (conv_epilogue.h) after the fp32 tile is
 staged in LDS, after the row pass (residual / rounding / BN sums), after the
-column-sum reductions and when the stores and atomics are issued.  For a back-to-back chain of identical
+column-sum reductions (after the row stores are issued) and when the atomics are issued.  For a back-to-back chain of identical
 launches (the step's pattern) this prints, per launch, the dispatch gap (previous
 launch's last stamp -> this launch's first start), the start skew across
 workgroups, and the median per-workgroup phase durations.
@@ -91,7 +91,7 @@ def main():
             med = [statistics.median(c) for c in zip(*lines)]
             print(f"N{N} H{H:2d} C{C:2d} {var:5s} wg {nwg:4d}: gap {med[0]:4.2f} | skew "
                   f"{med[1]:4.2f} | stage {med[2]:4.2f} | mfma {med[3]:4.2f} | epi: lds "
-                  f"{med[4]:4.2f} rows {med[5]:4.2f} colsum {med[6]:4.2f} store+atomic "
+                  f"{med[4]:4.2f} rows+stores {med[5]:4.2f} colsum {med[6]:4.2f} atomics "
                   f"{med[7]:4.2f} | span {med[8]:5.2f} us", flush=True)
 
 
