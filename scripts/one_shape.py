@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run one conv shape's fwd / dgrad / wgrad kernels a few times (for rocprofv3 --pmc
 passes on a single kernel).  usage: one_shape.py N H C K k s [reps] [passes]
-passes: comma list of fwd (pre+stats), fwd_plain, fwd_stats, dgrad, wgrad (default all 3)"""
+passes: comma list of fwd (pre+stats), fwd_plain, fwd_stats, dgrad, dgrad_bnb, wgrad
+(default fwd,dgrad,wgrad)"""
 import os
 import sys
 
@@ -28,6 +29,10 @@ def main():
     out = torch.empty(N, g.Ho, g.Wo, K, device=dev, dtype=torch.bfloat16)
     dx = torch.empty_like(x)
     gw = torch.empty(k, k, C, K, device=dev)
+    M = N * H * H
+    bnb = (x, torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, sc, sh,
+           torch.zeros((M // 64 + 1) * 2 * C, device=dev))
+    bacc = torch.zeros(8 * 2 * C, device=dev, dtype=torch.float64)
     for _ in range(reps):
         if "fwd" in passes:
             fn.conv2d_fwd(x, w, s, stat_part=part, out=out, pre_scale=sc, pre_shift=sh)
@@ -37,6 +42,8 @@ def main():
             fn.conv2d_fwd(x, w, s, stat_part=part, out=out)
         if "dgrad" in passes:
             fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx)
+        if "dgrad_bnb" in passes:
+            fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx, bnb=bnb, bfin=[bacc])
         if "wgrad" in passes:
             fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc, pre_shift=sh)
     torch.cuda.synchronize()
