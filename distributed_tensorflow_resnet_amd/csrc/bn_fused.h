@@ -121,7 +121,7 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
       const float sh = bet - fmu * sc;
       sc_s[c] = sc;
       sh_s[c] = sh;
-      if (blockIdx.x == 0 && blockIdx.y == 0) {
+      if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
         P.mean[c] = fmu;
         P.rstd[c] = rs;
         P.scale[c] = sc;
@@ -142,7 +142,7 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
   if (tid < C) {
     gam = P.gamma[tid];
     bet = P.beta[tid];
-    if (P.update_moving && blockIdx.x == 0 && blockIdx.y == 0) {
+    if (P.update_moving && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
       mmv = P.mmean[tid];
       mvv = P.mvar[tid];
     }
@@ -213,7 +213,7 @@ __device__ __forceinline__ void bn_prefin_table(const BnPreFin& P, int C, float*
     const float sh = bet - fmu * sc;
     sc_s[c] = sc;
     sh_s[c] = sh;
-    if (blockIdx.x == 0 && blockIdx.y == 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
       P.mean[c] = fmu;
       P.rstd[c] = rs;
       P.scale[c] = sc;

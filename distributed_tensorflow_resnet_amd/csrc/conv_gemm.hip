@@ -317,10 +317,14 @@ conv_gemm_kernel(GemmArgs args) {
   const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16*>(ABWD ? args.abwd.x : args.a), 0, (int)(fast && ABWD ? a_elems * 2 : 0),
       0x00020000);
-  auto issue = [&](int t, auto P) {   // loads of K tile t into set P (t >= KT: zeros)
+  // split-K slice of this workgroup: K tiles [t_beg, t_end)
+  const int KT_all = (KD + BK - 1) / BK;
+  const int t_beg = (int)(((long)blockIdx.z * KT_all) / gridDim.z);
+  const int t_end = (int)(((long)(blockIdx.z + 1) * KT_all) / gridDim.z);
+  auto issue = [&](int t, auto P) {   // loads of K tile t into set P (t >= t_end: zeros)
     constexpr int p = decltype(P)::value;
     const int kb = t * BK;                       // uniform
-    const bool kv = kb < KD;
+    const bool kv = kb < KD && t < t_end;
     const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
     const int ci = kb - tap * Acin + kg * 8;
     if constexpr (PRE) pci[p] = kv ? ci : 0;
@@ -468,8 +472,8 @@ conv_gemm_kernel(GemmArgs args) {
   if constexpr (FAST) {
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    issue(0, I0{});
-    issue(1, I1{});
+    issue(t_beg, I0{});
+    issue(t_beg + 1, I1{});
     if constexpr (BNB && !ABWD) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
     if constexpr (ABWD) {   // [5][Acin]: a, c*rstd, b - c*rstd*mean, scale, shift
       // dh = a*g - b - c*(x - mean)*rstd = a*g - (c*rstd)*x - (b - c*rstd*mean)
@@ -513,12 +517,65 @@ conv_gemm_kernel(GemmArgs args) {
       stage(p ^ 1, std::integral_constant<int, p ^ 1>{});
       __syncthreads();
     };
-    int t = 0;
-    for (; t + 1 < KT; t += 2) {
+    int t = t_beg;
+    for (; t + 1 < t_end; t += 2) {
       body(t, I0{});
       body(t + 1, I1{});
     }
-    if (t < KT) body(t, I0{});
+    if (t < t_end) body(t, I0{});
+    if (gridDim.z > 1) {
+      // split-K: publish this slice's fp32 tile (write-through, thread-native order),
+      // take a ticket; the last slice of the tile sums all slices in slice order
+      // (bitwise independent of arrival order) and alone runs the epilogue
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      constexpr int NV = MR * NR;                           // f32x4 per thread
+      const int tile = tm * gridDim.y + tn;
+      const int S = gridDim.z, z = blockIdx.z;
+      const long slab = (long)BM * BN;                     // floats per slice tile
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long)tile * S * slab, 0,
+                                                        0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4_t, acc[a][b]), rs,
+              (int)((((long)z * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16);
+      int* flag = reinterpret_cast<int*>(smem);
+      if (!last_arriver(args.sk_cnt + tile, (unsigned)S, flag)) return;
+      f32x4 tot[MR][NR];
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) tot[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int zz = 0; zz < S; ++zz) {
+        if (zz == z) {
+#pragma unroll
+          for (int a = 0; a < MR; ++a)
+#pragma unroll
+            for (int b = 0; b < NR; ++b) tot[a][b] += acc[a][b];
+        } else {
+          f32x4 v[MR][NR];
+#pragma unroll
+          for (int a = 0; a < MR; ++a)
+#pragma unroll
+            for (int b = 0; b < NR; ++b)
+              v[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, (int)((((long)zz * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16));
+#pragma unroll
+          for (int a = 0; a < MR; ++a)
+#pragma unroll
+            for (int b = 0; b < NR; ++b) tot[a][b] += v[a][b];
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) acc[a][b] = tot[a][b];
+      reset_counter(args.sk_cnt + tile);
+      __syncthreads();   // the flag word's LDS is the epilogue's
+      (void)NV;
+    }
   } else {   // general gather (runtime `fast` only for the narrow-column tiles)
   load_tile(0);
   if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
@@ -564,6 +621,29 @@ void set_conv_pipeline(int enabled) {
   set_wgrad_pipeline(enabled);
 }
 
+// Split-K of the FAST loop for under-filled grids (the 7x7 stage: 196 tiles of 128x128
+// for 256 CUs, each a 32-72 K-tile loop at one workgroup per CU).  DTR_SPLITK = max
+// slices (default 2; 0 or 1 = off).  Workspace: one fp32 tile per slice and tile plus a
+// ticket per tile, allocated on first need (never while a graph is being captured --
+// the launch then runs unsplit) and grown, never freed.
+static int g_splitk = -1;
+static float* g_sk_part = nullptr;
+static size_t g_sk_part_bytes = 0;
+static unsigned* g_sk_cnt = nullptr;
+static size_t g_sk_cnt_n = 0;
+
+void set_conv_splitk(int max_slices) { g_splitk = max_slices < 1 ? 1 : max_slices; }
+
+static int pick_ksplit(long tiles, int KT) {
+  if (g_splitk < 0) {
+    const char* e = std::getenv("DTR_SPLITK");
+    g_splitk = e ? std::atoi(e) : 2;
+  }
+  int S = 1;
+  while (S * 2 <= g_splitk && tiles * S <= 128 * 2 && KT / (S * 2) >= 8) S *= 2;
+  return S;
+}
+
 // FAST-path eligibility (see the kernel): must match the kernel's own `fast` test.
 static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   if (g_pipe_enabled < 0) {
@@ -584,10 +664,43 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   //   dgrad:   >= 16k rows (1.06-1.16x at 14x14..56x56; the 7x7 grids of <= 200
   //            tiles run 0.88-0.95x).
   if (a.Kdim < 256) return false;
-  return mode == MODE_FWD ? a.Ncol >= 128 : a.M >= 16384;
+  if (mode == MODE_FWD) return a.Ncol >= 128;
+  if (a.M >= 16384) return true;
+  // the 7x7 dgrads: pipelined once split-K doubles their grid (DTR_DGRAD_SPLITK=0: off)
+  static int dsk = -1;
+  if (dsk < 0) {
+    const char* e = std::getenv("DTR_DGRAD_SPLITK");
+    dsk = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!dsk || a.Ncol < 128) return false;
+  const int bm = conv_gemm_bm(a.M, a.Ncol), bn = conv_gemm_bn(a.M, a.Ncol);
+  const long tiles = (long)((a.M + bm - 1) / bm) * ((a.Ncol + bn - 1) / bn);
+  return pick_ksplit(tiles, (a.Kdim + 63) / 64) > 1;
 }
 
 static int g_xcd_swz = -1;   // DTR_XCD_SWZ: 0 off, 1 on (default: see launch_cfg)
+
+static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s) {
+  if (part_bytes <= g_sk_part_bytes && tiles <= g_sk_cnt_n) return true;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cap);
+  if (cap != hipStreamCaptureStatusNone) return false;
+  if (part_bytes > g_sk_part_bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, part_bytes) != hipSuccess) return false;
+    g_sk_part = static_cast<float*>(p);   // the old buffer may still be read in flight: kept
+    g_sk_part_bytes = part_bytes;
+  }
+  if (tiles > g_sk_cnt_n) {
+    void* p = nullptr;
+    const size_t n = tiles < 4096 ? 4096 : tiles;
+    if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return false;
+    if (hipMemsetAsync(p, 0, n * sizeof(unsigned), s) != hipSuccess) return false;
+    g_sk_cnt = static_cast<unsigned*>(p);
+    g_sk_cnt_n = n;
+  }
+  return true;
+}
 
 static int g_nbuf1 = -1;   // DTR_NBUF1_KT: single-buffered LDS when the K loop has <= this many tiles
 
@@ -648,6 +761,15 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
     }
     if constexpr (BN >= 64) {
       if (conv_gemm_fast(a, MODE)) {
+        const long tiles = (long)grid.x * grid.y;
+        const int S = pick_ksplit(tiles, (a.Kdim + 63) / 64);
+        if (S > 1 && splitk_workspace((size_t)S * tiles * BM * BN * sizeof(float),
+                                      (size_t)tiles, s)) {
+          a.ksplit = S;
+          a.sk_part = g_sk_part;
+          a.sk_cnt = g_sk_cnt;
+          grid.z = S;
+        }
         hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
                            dim3(256), lds, s, a);
         DTR_CHECK_LAUNCH();

@@ -129,9 +129,16 @@ struct GemmArgs {
   int swz = 0;              // conv_gemm: XCD-grouped tile order (set by the launcher)
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
   int wt = 0;                   // epilogue output stores write-through (sc1): DTR_WT_STORE
+  // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
+  // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
+  // (sk_cnt) sums the slices in slice order and runs the epilogue
+  int ksplit = 1;
+  float* sk_part = nullptr;
+  unsigned* sk_cnt = nullptr;
 };
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
+void set_conv_splitk(int max_slices);   // split-K of under-filled FAST grids (1 = off)
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);

@@ -657,3 +657,72 @@ def test_grouped_wgrad_reduce_wide_and_deep(gpu):
     for (sp, K, taps, C, Kv, Cv), g, r in zip(cases, grads, refs):
         torch.testing.assert_close(g.double(), r, rtol=1e-5, atol=1e-5 * sp ** 0.5,
                                    msg=lambda m: f"{(sp, K, taps, C, Kv, Cv)}: {m}")
+
+
+@pytest.mark.parametrize("N,H,C,K,k,pre", [(128, 7, 512, 512, 3, True), (128, 7, 2048, 512, 1, True),
+                                           (64, 7, 512, 512, 3, False), (16, 14, 256, 256, 3, True)])
+def test_splitk_conv_matches_unsplit(gpu, N, H, C, K, k, pre):
+    """Split-K of the pipelined implicit GEMM (under-filled grids, the 7x7 stage): the
+    slices' fp32 tiles summed by the last arriver == the one-slice result (to fp32
+    summation order) and the fp32 reference; BN statistics likewise; repeated launches
+    reuse the tickets (each last arriver resets its tile's)."""
+    torch.manual_seed(18)
+    nat = fn.native()
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(K, k, k, C, device=gpu) / math.sqrt(k * k * C)).to(BF)
+    sc = torch.rand(C, device=gpu) + 0.5
+    sh = torch.randn(C, device=gpu) * 0.1
+    kw = dict(pre_scale=sc, pre_shift=sh) if pre else {}
+    M = N * H * H
+    tiles, _ = fn.stat_tiles(M, K)
+    outs, parts = [], []
+    for slices in (1, 4, 2):
+        nat.set_conv_splitk(slices)
+        try:
+            part = torch.zeros(tiles * 2 * K, device=gpu)
+            for _ in range(3):
+                out = fn.conv2d_fwd(x, w, 1, stat_part=part, **kw)
+            torch.cuda.synchronize()
+        finally:
+            nat.set_conv_splitk(2)
+        outs.append(out.float())
+        parts.append(part.clone())
+    a = torch.relu(x.float() * sc + sh) if pre else x.float()
+    ref_out = ref.conv2d(a.to(BF).float(), w.float().permute(1, 2, 3, 0), 1)
+    for o, p in zip(outs[1:], parts[1:]):
+        assert _rel(o, outs[0]) < 2e-3
+        torch.testing.assert_close(p, parts[0], rtol=1e-3, atol=1e-3)
+    assert _rel(outs[2], ref_out) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K,k", [(128, 7, 512, 512, 3), (128, 7, 512, 2048, 1)])
+def test_splitk_dgrad_matches_unsplit(gpu, N, H, C, K, k):
+    """The 7x7 dgrads run the pipelined loop split in two: == one slice and the
+    fp32 reference, BN-backward sums (BNB epilogue) included."""
+    torch.manual_seed(19)
+    nat = fn.native()
+    dy = torch.randn(N, H, H, K, device=gpu).to(BF)
+    w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * K)).to(BF)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    mean, rstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
+    M = N * H * H
+    outs, accs = [], []
+    for slices in (1, 2):
+        nat.set_conv_splitk(slices)
+        try:
+            acc = torch.zeros(8 * 2 * C, device=gpu, dtype=torch.float64)
+            part = torch.zeros((M // 64 + 1) * 2 * C, device=gpu)
+            out = fn.conv2d_dgrad(dy, w, tuple(x.shape), 1, bnb=(x, mean, rstd, sc, sh, part),
+                                  bfin=[acc])
+            torch.cuda.synchronize()
+        finally:
+            nat.set_conv_splitk(2)
+        outs.append(out.float())
+        accs.append(acc.view(8, 2, C).sum(0))
+    wt = w.float().permute(0, 1, 2, 3)  # HWIO [kh][kw][C][K]
+    xt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
+    ref.conv2d(xt, wt, 1).backward(dy.float())
+    assert _rel(outs[1], outs[0]) < 2e-3
+    assert _rel(outs[1], xt.grad) < 1e-2
+    torch.testing.assert_close(accs[1], accs[0], rtol=2e-3, atol=1e-2)
