@@ -128,14 +128,26 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// Host: whether conv epilogues store write-through (DTR_WT_STORE=1; read once).
-inline bool wt_store_enabled() {
-  static int v = -1;
-  if (v < 0) {
+// Host: conv epilogue / dh stores write-through (sc1).  DTR_WT_STORE=1 forces it on for
+// every conv, =0 off; unset: the direct 3x3 convs decide by output size
+// (wt_store_direct), the implicit-GEMM convs store normally.
+inline int wt_store_mode() {
+  static int v = -2;
+  if (v == -2) {
     const char* e = std::getenv("DTR_WT_STORE");
-    v = (e != nullptr && e[0] == '1') ? 1 : 0;
+    v = e == nullptr ? -1 : (e[0] == '1' ? 1 : 0);
   }
-  return v == 1;
+  return v;
+}
+inline bool wt_store_enabled() { return wt_store_mode() == 1; }
+// Direct convs: write-through once a launch writes >= 2 MB.  A kernel boundary pays
+// ~bytes / 6 TB/s to write back the dirty lines its predecessor left in L2
+// (MI355X_MICROARCH.md "boundary"); write-through stores leave none.  Measured, CIFAR
+// RN50 bs128: boundaries 2.4-2.6 -> 1.6-2.1 us, step 1.304 -> 1.282 ms; bs16 / bs64
+// (outputs < 2 MB per launch) unchanged.
+inline bool wt_store_direct(long out_bytes) {
+  const int m = wt_store_mode();
+  return m == 1 || (m == -1 && out_bytes >= (2L << 20));
 }
 
 }  // namespace dtr

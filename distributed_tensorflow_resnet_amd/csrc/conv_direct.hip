@@ -241,9 +241,18 @@ conv3x3_direct_kernel(GemmArgs args) {
           }
           v = r;
           const int hr = pix / HW2;
-          if (hr >= 1 && hr <= R && hc >= 1 && hc <= WI && blockIdx.y == 0)   // interior: this tile's dh rows
-            *reinterpret_cast<bf16x8*>(args.abwd.a_out + ibase +
-                                       ((long)(h0 + hr - 1) * WI + hc - 1) * CA + u * 8) = v;
+          if (hr >= 1 && hr <= R && hc >= 1 && hc <= WI && blockIdx.y == 0) {   // interior: this tile's dh rows
+            const long e = ibase + ((long)(h0 + hr - 1) * WI + hc - 1) * CA + u * 8;
+            if (args.wt) {   // write-through (sc1), like the epilogue's stores under wt
+              typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+              const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.abwd.a_out, 0, 0x7fffffff,
+                                                                0x00020000);   // uniform base
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs,
+                                                     (int)(e * 2), 0, 16);
+            } else {
+              *reinterpret_cast<bf16x8*>(args.abwd.a_out + e) = v;
+            }
+          }
         }
       }
       *reinterpret_cast<bf16x8*>(halo + (pix * U + (u ^ (hc & (U - 1)))) * 8) = v;
@@ -333,7 +342,8 @@ template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS>
 static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   a.probe = g_probe;
-  a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
+  const long out_bytes = (long)a.M * a.Ncol * 2;
+  a.wt = wt_store_direct(out_bytes) && out_bytes < (1L << 31) ? 1 : 0;
   if (g_direct_ldsw < 0) {
     const char* e = std::getenv("DTR_DIRECT_LDSW");
     g_direct_ldsw = e ? std::atoi(e) : 4;
