@@ -162,6 +162,7 @@ struct WgradArgs {
   ConvGeom g;
   int splits;
   int px_per_split;         // multiple of 64
+  int wt = 0;               // direct kernel: partials stored write-through (set by the launcher)
 };
 void conv_wgrad(const WgradArgs& a, hipStream_t s);
 // Direct halo-tiled wgrad for 3x3/s1 small C (conv_wgrad_direct.hip).
