@@ -387,7 +387,11 @@ conv_wgrad_kernel(WgradArgs args) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * WTM + a * 16 + gq * 4 + i;
-        if (m < Cout && n < NT) out[(long)m * NT + n] = acc[a][b][i];
+        if (m < Cout && n < NT) {
+          if (args.wt) __hip_atomic_store(out + (long)m * NT + n, acc[a][b][i], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
+          else out[(long)m * NT + n] = acc[a][b][i];
+        }
       }
   }
 }
@@ -412,7 +416,14 @@ static bool wgrad_fast(const WgradArgs& a) {
 }
 
 template <int BM, int BN, int WM, int WN>
-static void wg_launch(const WgradArgs& a, hipStream_t s) {
+static void wg_launch(const WgradArgs& a0, hipStream_t s) {
+  static int wt = -1;   // DTR_WG_WT=1: split-K partials stored write-through (A/B knob)
+  if (wt < 0) {
+    const char* e = std::getenv("DTR_WG_WT");
+    wt = (e && e[0] == '1') ? 1 : 0;
+  }
+  WgradArgs a = a0;
+  a.wt = wt;
   const int NT = a.g.kh * a.g.kw * a.g.C;
   size_t lds = (size_t)2 * 64 * (BM + BN) * sizeof(bf16);
   dim3 grid((NT + BN - 1) / BN, (a.g.K + BM - 1) / BM, a.splits);
