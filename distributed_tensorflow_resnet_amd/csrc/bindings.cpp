@@ -1052,6 +1052,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("wgrad_reduce_chunks", &wgrad_reduce_chunks, py::arg("splits"), py::arg("K"),
         py::arg("taps"), py::arg("C"),
         "work chunks of one conv's slabs in wgrad_reduce_grouped (its desc's chunk0 stride)");
+  m.def("wgrad_direct_bmp", [](std::vector<int> geom) { return wgrad_direct_bmp(geom_from(geom)); },
+        "pixels per split of the direct 3x3 wgrad for this conv (0: the generic kernel runs)");
   m.def("wgrad_pick_splits", [](std::vector<int> geom) {
     int pps = 0;
     const int sp = wgrad_pick_splits(geom_from(geom), &pps);

@@ -766,6 +766,26 @@ class Engine:
         plan.use_stream(0)
         self._side_q, self._side_blocks = [], 0
 
+    def _wgrad_matpre(self, geom) -> bool:
+        """Materialize the BN+ReLU of a wgrad's input first (DTR_WGRAD_MATPRE=1): 3x3
+        convs on the generic split-K kernel only (the direct CIFAR kernel stages a halo
+        and applies it once per element already).  Off by default: it removes the 9x
+        VALU of the im2col staging (those wgrads issue ~19 VALU per MFMA), but the
+        extra read + write pass cost more on the shared HBM (ImageNet RN50 13.05 ->
+        13.10 ms)."""
+        if os.environ.get("DTR_WGRAD_MATPRE", "0") != "1":
+            return False
+        return geom[7] * geom[8] > 1 and self.nat.wgrad_direct_bmp(list(geom)) == 0
+
+    def _matpre_buf(self, geom):
+        """Scratch relu(bn(x)) tensor for a materialized wgrad input: one per shape,
+        reused by every such wgrad on the stream that issues them in order."""
+        n = geom[0] * geom[1] * geom[2] * geom[3]
+        bufs = self.__dict__.setdefault("_matpre_bufs", {})
+        if n not in bufs:
+            bufs[n] = torch.empty(n, dtype=BF16, device=self.device)
+        return bufs[n].data_ptr()
+
     def _emit_wgrads(self, plan, descs):
         """Weight-gradient launches on the current stream.  Runs of same-shape layers
         (the residual blocks of a stage, queued together by _flush_side) go out as
@@ -793,7 +813,15 @@ class Engine:
             geom, sp, pps = list(run[0][5]), run[0][6], run[0][7]
             if len(run) == 1:
                 d = run[0]
-                plan.conv_wgrad(d[0], d[1], d[2], d[3], d[4], geom, sp, pps)
+                x, sc, sh = d[1], d[2], d[3]
+                if sc and self._wgrad_matpre(geom):
+                    # relu(bn(x)) once into a scratch tensor, then a plain wgrad: the
+                    # generic kernel's im2col staging otherwise applies the BN+ReLU to
+                    # every element once per filter tap (9x VALU on the 3x3 convs)
+                    x = self._matpre_buf(geom)
+                    plan.bn_relu_apply(d[1], sc, sh, x, geom[0] * geom[1] * geom[2], geom[3])
+                    sc = sh = 0
+                plan.conv_wgrad(d[0], x, sc, sh, d[4], geom, sp, pps)
             else:
                 plan.conv_wgrad_group([d[0] for d in run], [d[1] for d in run],
                                       [d[2] for d in run], [d[3] for d in run],
