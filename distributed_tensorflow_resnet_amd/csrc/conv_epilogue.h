@@ -143,9 +143,12 @@ __device__ __forceinline__ float lanes_colsum(float v) {
   if constexpr (2 * CPR < 16) v = row_ror_add<2 * CPR>(v);
   if constexpr (4 * CPR < 16) v = row_ror_add<4 * CPR>(v);
   if constexpr (8 * CPR < 16) v = row_ror_add<8 * CPR>(v);
-  // the four 16-lane rows: two shuffles.  (v_permlane16/32_swap with the value on both
-  // sides would do it on the VALU, but hipcc folds permlane*_swap(x, x) to one result
-  // and silently drops a row: caught by test_conv_fused_prologue_epilogue.)
+  // the four 16-lane rows: two shuffles.  (v_permlane16/32_swap on two copies of the
+  // value does it on the VALU, but a VALU write feeding the swap is a hazard: without
+  // wait states a row is silently dropped -- caught by test_conv_fused_prologue_epilogue
+  // and test_direct_conv3x3_matches_reference_and_generic.  Inline asm with s_nop 1
+  // before each swap passes every test but measured no faster than the shuffles:
+  // colsum phase 0.68-0.72 us vs 0.64-0.76, CIFAR bs16 0.946 vs 0.938-0.950 ms.)
   v += __shfl_xor(v, 16, 64);
   return v + __shfl_xor(v, 32, 64);
 }
