@@ -1047,6 +1047,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_stats_tile_rows", &bn_stats_tile_rows);
   m.def("l2_workspace_floats", &l2_workspace_floats);
   m.def("softmax_xent_ws_floats", &softmax_xent_ws_floats);
+  m.def("set_conv_parity", &set_conv_parity, py::arg("enabled"),
+        "stride-2 dgrads as 4 output-parity classes (DTR_PARITY_DGRAD)");
   m.def("set_conv_splitk", &set_conv_splitk, py::arg("max_slices"),
         "max split-K slices of under-filled implicit-GEMM grids (1 = off; DTR_SPLITK)");
   m.def("wgrad_reduce_chunks", &wgrad_reduce_chunks, py::arg("splits"), py::arg("K"),

@@ -137,6 +137,16 @@ __device__ __forceinline__ float row_ror_add(float v) {   // v + v of lane (l - 
   return v;
 }
 
+// Output row (pixel) of epilogue row `row`: the identity, or for a stride-2 dgrad parity
+// class (GemmArgs::par) the class's row-major pixel (n, h0 + 2 hh, w0 + 2 ww).
+__device__ __forceinline__ long epi_row(const GemmArgs& a, int row) {
+  if (!a.par) return row;
+  const int per = a.par_hc * a.par_wc;
+  const int n = row / per, rem = row - n * per;
+  const int hh = rem / a.par_wc, ww = rem - hh * a.par_wc;
+  return ((long)n * a.g.H + a.par_h0 + 2 * hh) * a.g.W + a.par_w0 + 2 * ww;
+}
+
 template <int CPR>
 __device__ __forceinline__ float lanes_colsum(float v) {
   v = row_ror_add<CPR>(v);
@@ -233,7 +243,7 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
       for (int it = 0; it < PP::RIT; ++it) {
         const int row = m0 + ph * EL::PR + r0 + it * EL::RPP;
         const bool ok = col0 < args.Ncol && r0 + it * EL::RPP < EL::PR && row < args.M;
-        const long o = (long)row * args.Ncol + col0;
+        const long o = epi_row(args, row) * args.Ncol + col0;
         if constexpr (!XO && EL::PHASES == 1) {
           P.res[it] = (ok && args.residual) ? *reinterpret_cast<const bf16x8*>(args.residual + o)
                                             : zero8;
@@ -355,7 +365,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       for (int it = 0; it < RIT; ++it) {
         const int r = r0 + it * EL::RPP;
         if (!colok || r >= nph) continue;
-        const long o = (long)(prow0 + r) * NC + col0;
+        const long o = epi_row(args, prow0 + r) * NC + col0;
         if constexpr (BNB) lx[BATCH ? it : 0] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
       }
     }
@@ -364,7 +374,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       for (int it = 0; it < RIT; ++it) {
         const int r = r0 + it * EL::RPP;
         const bool ok = colok && r < nph;
-        const long o = (long)(prow0 + (ok ? r : 0)) * NC + (ok ? col0 : 0);
+        const long o = epi_row(args, prow0 + (ok ? r : 0)) * NC + (ok ? col0 : 0);
         lr[BATCHR ? it : 0] = *reinterpret_cast<const bf16x8*>(args.residual + o);
       }
     }
@@ -420,7 +430,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       const f32x4 lo = *reinterpret_cast<const f32x4*>(cp);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cp + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const long o = (long)row * NC + col0;
+      const long o = epi_row(args, row) * NC + col0;
       if (args.residual) {
         const bf16x8 rv = (PRER && pre) ? pre->res[PRER ? it : 0]
                           : BATCHR      ? lr[BATCHR ? it : 0]
@@ -487,7 +497,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
           if (!colok || r >= nph) continue;
           typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ob[it]), rs,
-                                                 (int)(((long)(prow0 + r) * NC + col0) * 2), 0,
+                                                 (int)((epi_row(args, prow0 + r) * NC + col0) * 2), 0,
                                                  16);
         }
       } else {
@@ -495,7 +505,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         for (int it = 0; it < RIT; ++it) {
           const int r = r0 + it * EL::RPP;
           if (!colok || r >= nph) continue;
-          *reinterpret_cast<bf16x8*>(args.out + (long)(prow0 + r) * NC + col0) = ob[it];
+          *reinterpret_cast<bf16x8*>(args.out + epi_row(args, prow0 + r) * NC + col0) = ob[it];
         }
       }
     }

@@ -83,7 +83,27 @@ conv_gemm_kernel(GemmArgs args) {
   float* pre_s = reinterpret_cast<float*>(Bs + NBUF * BN * BK); // [2][Cin] (PRE)
 
   const ConvGeom& g = args.g;
+  // stride-2 dgrad parity class (blockIdx.z): its rows, reduction depth and taps
+  int par_ph = 0, par_pw = 0, par_ns = 1;
+  if (MODE == MODE_DGRAD && args.par) {
+    par_ph = blockIdx.z >> 1;
+    par_pw = blockIdx.z & 1;
+    args.par_h0 = (par_ph + g.pad) & 1;
+    args.par_w0 = (par_pw + g.pad) & 1;
+    args.par_hc = (g.H - args.par_h0 + 1) >> 1;
+    args.par_wc = (g.W - args.par_w0 + 1) >> 1;
+    par_ns = (g.kw - par_pw + 1) >> 1;
+    args.M = g.N * args.par_hc * args.par_wc;
+    args.Kdim = ((g.kh - par_ph + 1) >> 1) * par_ns * g.K;
+  }
   const int M = args.M, NC = args.Ncol, KD = args.Kdim;
+  if (MODE == MODE_DGRAD && args.par && (int)(blockIdx.x * BM) >= M) return;   // class rows done
+  // (kernel tap of a class-local K tap: rows ph, ph + 2, ..; columns pw, pw + 2, ..)
+  auto class_tap = [&](int tl, int& rr, int& cc) {
+    const int q = par_ns > 0 ? tl / par_ns : 0;
+    rr = par_ph + 2 * q;
+    cc = par_pw + 2 * (tl - q * par_ns);
+  };
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -135,9 +155,20 @@ conv_gemm_kernel(GemmArgs args) {
         a_h[i] = ho * g.stride - g.pad;
         a_w[i] = wo * g.stride - g.pad;
       } else {
-        const int hw = g.H * g.W;
-        const int n = m / hw, rem = m - n * hw;
-        const int h = rem / g.W, w = rem - h * g.W;
+        int n, h, w;
+        if (args.par) {   // class-local row -> (n, h0 + 2 hh, w0 + 2 ww)
+          const int per = args.par_hc * args.par_wc;
+          n = m / per;
+          const int rem = m - n * per, hh = rem / args.par_wc;
+          h = args.par_h0 + 2 * hh;
+          w = args.par_w0 + 2 * (rem - hh * args.par_wc);
+        } else {
+          const int hw = g.H * g.W;
+          n = m / hw;
+          const int rem = m - n * hw;
+          h = rem / g.W;
+          w = rem - h * g.W;
+        }
         a_base[i] = n * g.Ho * g.Wo;
         a_h[i] = h + g.pad;
         a_w[i] = w + g.pad;
@@ -191,7 +222,9 @@ conv_gemm_kernel(GemmArgs args) {
     const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
     const int ci = kb - tap * Acin + kg * 8;
     if constexpr (PRE) pre_ci = kv ? ci : 0;
-    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+    int rr = tap / g.kw, cc = tap - rr * g.kw;
+    if (MODE == MODE_DGRAD && args.par) class_tap(tap, rr, cc);
+    const int gtap = rr * g.kw + cc;   // kernel tap (weight layout)
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       int off = kOOB;
@@ -220,7 +253,7 @@ conv_gemm_kernel(GemmArgs args) {
       int off = kOOB;
       if (q < B_CHUNKS && n0 + nrow < NC && kv) {
         if constexpr (MODE == MODE_FWD) off = ((n0 + nrow) * KD + kb + kg * 8) * 2;
-        else off = ((tap * g.C + (n0 + nrow)) * g.K + ci) * 2;
+        else off = ((gtap * g.C + (n0 + nrow)) * g.K + ci) * 2;
       }
       rb[i] = bload(rs_b, off);
     }
@@ -236,7 +269,9 @@ conv_gemm_kernel(GemmArgs args) {
     const int tap = kvalid ? k / Acin : 0;
     const int ci = k - tap * Acin;
     if constexpr (PRE) pre_ci = kvalid ? ci : 0;
-    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+    int rr = tap / g.kw, cc = tap - rr * g.kw;
+    if (MODE == MODE_DGRAD && args.par) class_tap(tap, rr, cc);
+    const int gtap = rr * g.kw + cc;   // kernel tap (weight layout)
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       bf16x8 v = zero8;
@@ -272,7 +307,7 @@ conv_gemm_kernel(GemmArgs args) {
         if constexpr (MODE == MODE_FWD) {
           off = (long)(n0 + nrow) * KD + k;                    // W[co][r][c][ci]
         } else {
-          off = ((long)tap * g.C + (n0 + nrow)) * g.K + ci;    // W[r][c][ci][co]
+          off = ((long)gtap * g.C + (n0 + nrow)) * g.K + ci;   // W[r][c][ci][co]
         }
         v = *reinterpret_cast<const bf16x8*>(args.b + off);
       }
@@ -319,8 +354,9 @@ conv_gemm_kernel(GemmArgs args) {
       0x00020000);
   // split-K slice of this workgroup: K tiles [t_beg, t_end)
   const int KT_all = (KD + BK - 1) / BK;
-  const int t_beg = (int)(((long)blockIdx.z * KT_all) / gridDim.z);
-  const int t_end = (int)(((long)(blockIdx.z + 1) * KT_all) / gridDim.z);
+  const int sk_n = args.ksplit > 1 ? args.ksplit : 1, sk_z = sk_n > 1 ? (int)blockIdx.z : 0;
+  const int t_beg = (int)(((long)sk_z * KT_all) / sk_n);
+  const int t_end = (int)(((long)(sk_z + 1) * KT_all) / sk_n);
   auto issue = [&](int t, auto P) {   // loads of K tile t into set P (t >= t_end: zeros)
     constexpr int p = decltype(P)::value;
     const int kb = t * BK;                       // uniform
@@ -328,7 +364,9 @@ conv_gemm_kernel(GemmArgs args) {
     const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
     const int ci = kb - tap * Acin + kg * 8;
     if constexpr (PRE) pci[p] = kv ? ci : 0;
-    const int rr = tap / g.kw, cc = tap - rr * g.kw;
+    int rr = tap / g.kw, cc = tap - rr * g.kw;
+    if (MODE == MODE_DGRAD && args.par) class_tap(tap, rr, cc);
+    const int gtap = rr * g.kw + cc;   // kernel tap (weight layout)
     unsigned msk = 0u;
     if constexpr (ABWD) {
       pci[p] = kv ? ci : 0;
@@ -368,7 +406,7 @@ conv_gemm_kernel(GemmArgs args) {
       const bool ok = (B_CHUNKS % 256 == 0 || q < B_CHUNKS) && n0 + nrow < NC && kv;
       int off;
       if constexpr (MODE == MODE_FWD) off = ((n0 + nrow) * KD + kb + kg * 8) * 2;
-      else off = ((tap * g.C + (n0 + nrow)) * g.K + ci) * 2;
+      else off = ((gtap * g.C + (n0 + nrow)) * g.K + ci) * 2;
       pb[p][i] = bload(rs_b, ok ? off : kOOB);
     }
   };
@@ -523,14 +561,14 @@ conv_gemm_kernel(GemmArgs args) {
       body(t + 1, I1{});
     }
     if (t < t_end) body(t, I0{});
-    if (gridDim.z > 1) {
+    if (sk_n > 1) {
       // split-K: publish this slice's fp32 tile (write-through, thread-native order),
       // take a ticket; the last slice of the tile sums all slices in slice order
       // (bitwise independent of arrival order) and alone runs the epilogue
       typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
       constexpr int NV = MR * NR;                           // f32x4 per thread
       const int tile = tm * gridDim.y + tn;
-      const int S = gridDim.z, z = blockIdx.z;
+      const int S = sk_n, z = sk_z;
       const long slab = (long)BM * BN;                     // floats per slice tile
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long)tile * S * slab, 0,
                                                         0x7fffffff, 0x00020000);
@@ -749,7 +787,7 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
   if (FLAGS & F_ABWD) lds += (size_t)5 * Acin * sizeof(float);
   lds = std::max(lds, EpiLayout<BM, BN, WM>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
-  dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN);
+  dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN, a.par ? 4 : 1);
   // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles; the
   // fused BN backward (ABWD) exists only there
   if constexpr (NBUF == 1) {   // general loop only (launch_cfg: one-tile K loops)
@@ -770,7 +808,7 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
     if constexpr (BN >= 64) {
       if (conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
-        const int S = pick_ksplit(tiles, (a.Kdim + 63) / 64);
+        const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
         if (S > 1 && splitk_workspace((size_t)S * tiles * BM * BN * sizeof(float),
                                       (size_t)tiles, s)) {
           a.ksplit = S;
@@ -919,12 +957,42 @@ bool conv_gemm_abwd_covers(const GemmArgs& a) {
   return true;
 }
 
+static int g_parity = -1;   // DTR_PARITY_DGRAD: stride-2 dgrads by output parity class
+void set_conv_parity(int enabled) { g_parity = enabled ? 1 : 0; }
+
+// Stride-2 dgrad as 4 parity classes of output pixels (one launch, blockIdx.z = class):
+// a pixel with (h + pad, w + pad) = (ph, pw) mod 2 only receives the filter taps r = ph,
+// ph + 2, .. and s = pw, pw + 2, .., so each class is a dense implicit GEMM over a
+// quarter of the rows and its own taps -- instead of every pixel running all kh x kw
+// taps with 3/4 of the (pixel, tap) pairs masked to zero (ImageNet's stride-2 dgrads
+// ran 3-3.5x slower than their forward convs).  Not with the fused BN backward (ABWD)
+// or tile-partial BN sums (their layouts are per row tile of the whole output).
+static bool parity_dgrad(const GemmArgs& a) {
+  if (g_parity < 0) {
+    const char* e = std::getenv("DTR_PARITY_DGRAD");
+    g_parity = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_parity && a.g.stride == 2 && a.abwd.x == nullptr &&
+         (a.bnb_part == nullptr || a.bnb_acc != nullptr) && a.out_f32 == nullptr &&
+         a.bias == nullptr && a.residual == nullptr;
+}
+
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
   if (conv_direct(a, mode, s)) return;
   if (a.abwd.x != nullptr && (mode != MODE_DGRAD || !conv_gemm_abwd_covers(a)))
     throw std::runtime_error("conv_gemm: fused BN backward (abwd) not covered for this dgrad");
-  if (mode == MODE_FWD) launch_mode<MODE_FWD>(a, s);
-  else launch_mode<MODE_DGRAD>(a, s);
+  if (mode == MODE_FWD) {
+    launch_mode<MODE_FWD>(a, s);
+  } else if (parity_dgrad(a)) {
+    GemmArgs b = a;   // tiles / FAST chosen for the largest class (the kernel derives its own)
+    const ConvGeom& g = a.g;
+    b.par = 1;
+    b.M = g.N * ((g.H + 1) >> 1) * ((g.W + 1) >> 1);
+    b.Kdim = ((g.kh + 1) >> 1) * ((g.kw + 1) >> 1) * g.K;
+    launch_mode<MODE_DGRAD>(b, s);
+  } else {
+    launch_mode<MODE_DGRAD>(a, s);
+  }
 }
 
 }  // namespace dtr

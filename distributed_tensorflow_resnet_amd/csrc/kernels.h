@@ -135,10 +135,17 @@ struct GemmArgs {
   int ksplit = 1;
   float* sk_part = nullptr;
   unsigned* sk_cnt = nullptr;
+  // stride-2 dgrad by output parity class (conv_gemm; set by the launcher): gridDim.z = 4
+  // classes (h+pad, w+pad) mod 2, each a dense GEMM over its own rows and only the filter
+  // taps that reach them.  par != 0 enables it; the kernel fills in its class's row
+  // geometry (first row / column, rows / columns per image) for the epilogue.
+  int par = 0;
+  int par_h0 = 0, par_w0 = 0, par_hc = 0, par_wc = 0;
 };
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 void set_conv_splitk(int max_slices);   // split-K of under-filled FAST grids (1 = off)
+void set_conv_parity(int enabled);      // stride-2 dgrads by output parity class
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);

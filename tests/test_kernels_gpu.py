@@ -726,3 +726,43 @@ def test_splitk_dgrad_matches_unsplit(gpu, N, H, C, K, k):
     assert _rel(outs[1], outs[0]) < 2e-3
     assert _rel(outs[1], xt.grad) < 1e-2
     torch.testing.assert_close(accs[1], accs[0], rtol=2e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("N,H,C,K,k,acc", [(64, 32, 16, 32, 3, False), (64, 32, 16, 32, 1, True),
+                                           (32, 16, 32, 64, 3, False), (8, 56, 128, 128, 3, False),
+                                           (8, 56, 256, 512, 1, True), (4, 14, 1024, 2048, 1, False),
+                                           (8, 28, 256, 256, 3, True)])
+def test_parity_class_stride2_dgrad(gpu, N, H, C, K, k, acc):
+    """Stride-2 dgrad by output parity class (4 dense GEMMs over their own rows and
+    taps, one launch) == the masked all-taps kernel and the fp32 reference, with the
+    BN-backward sums (fp64 accumulators) and accumulate-into-output."""
+    torch.manual_seed(20)
+    nat = fn.native()
+    g = fn.ConvGeom(N, H, H, C, K, k, k, 2)
+    dy = torch.randn(N, g.Ho, g.Wo, K, device=gpu).to(BF)
+    w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * K)).to(BF)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    base = torch.randn(N, H, H, C, device=gpu).to(BF)
+    mean, rstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
+    M = N * H * H
+    outs, accs = [], []
+    for parity in (0, 1):
+        nat.set_conv_parity(parity)
+        try:
+            bacc = torch.zeros(8 * 2 * C, device=gpu, dtype=torch.float64)
+            part = torch.zeros((M // 64 + 1) * 2 * C, device=gpu)
+            out = base.clone()
+            fn.conv2d_dgrad(dy, w, tuple(x.shape), 2, out=out, accumulate=acc,
+                            bnb=(x, mean, rstd, sc, sh, part), bfin=[bacc])
+            torch.cuda.synchronize()
+        finally:
+            nat.set_conv_parity(1)
+        outs.append(out.float())
+        accs.append(bacc.view(8, 2, C).sum(0))
+    xt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
+    ref.conv2d(xt, w.float(), 2).backward(dy.float())
+    want = xt.grad + (base.float() if acc else 0)
+    assert _rel(outs[1], outs[0]) < 1e-2
+    assert _rel(outs[1], want) < 1e-2
+    torch.testing.assert_close(accs[1], accs[0], rtol=1e-2, atol=1e-1)
