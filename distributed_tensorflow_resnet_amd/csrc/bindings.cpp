@@ -506,12 +506,21 @@ static Launch mk_cifar_augment(ptr_t img, ptr_t out, int N, int H, int W, int Cp
 
 static Launch mk_imagenet_u8_pack(ptr_t img, ptr_t out, int N, int H, int W,
                                   unsigned long long seed, ptr_t gstep, int train, ptr_t zero,
-                                  long zero_bytes) {
+                                  long zero_bytes, int s2d) {
   if (zero_bytes % 16) throw std::invalid_argument("imagenet_u8_pack: zero_bytes % 16 != 0");
+  if (s2d && ((H | W) & 1)) throw std::invalid_argument("imagenet_u8_pack: s2d needs even H, W");
   return [=](hipStream_t s) {
     imagenet_u8_pack(P<const uint8_t>(img), P<bf16>(out), N, H, W, seed,
-                     P<const long long>(gstep), train, P<void>(zero), zero_bytes, s);
+                     P<const long long>(gstep), train, P<void>(zero), zero_bytes, s2d, s);
   };
+}
+
+static Launch mk_stem_s2d_pack(ptr_t w7, ptr_t w4, int K) {
+  return [=](hipStream_t s) { stem_s2d_pack(P<const float>(w7), P<bf16>(w4), K, s); };
+}
+
+static Launch mk_stem_s2d_grad(ptr_t g4, ptr_t g7, int K) {
+  return [=](hipStream_t s) { stem_s2d_grad(P<const float>(g4), P<float>(g7), K, s); };
 }
 
 static Launch mk_pad_channels(ptr_t x, ptr_t out, long npix, int C, int Cpad) {
@@ -997,6 +1006,8 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "delay", mk_delay);
   def_op(m, plan, "cifar_augment", mk_cifar_augment);
   def_op(m, plan, "imagenet_u8_pack", mk_imagenet_u8_pack);
+  def_op(m, plan, "stem_s2d_pack", mk_stem_s2d_pack);
+  def_op(m, plan, "stem_s2d_grad", mk_stem_s2d_grad);
   def_op(m, plan, "pad_channels", mk_pad_channels);
   def_op(m, plan, "synthetic_images", mk_synthetic);
   def_op(m, plan, "cast_f32_bf16", mk_cast_f2b);

@@ -204,7 +204,12 @@ conv_gemm_kernel(GemmArgs args) {
   const long a_elems = (MODE == MODE_FWD) ? (long)g.N * g.H * g.W * g.C
                                           : (long)g.N * g.Ho * g.Wo * g.K;
   const long b_elems = (long)g.kh * g.kw * g.C * g.K;
-  const bool fast = (Acin % BK) == 0 && a_elems < (1L << 30) && b_elems < (1L << 30);
+  // Narrow forward operands (the ImageNet stem: 8 channels, or 16 in space-to-depth
+  // form) take the same branch-free buffer-load gather with a per-thread tap: a K tile
+  // then spans BK / Acin taps, one 8-channel group each (load_tile_fast).
+  constexpr bool NARROW_OK = MODE == MODE_FWD && !PRE;
+  const bool narrow = NARROW_OK && Acin < BK && Acin % 8 == 0 && BK % Acin == 0;
+  const bool fast = ((Acin % BK) == 0 || narrow) && a_elems < (1L << 30) && b_elems < (1L << 30);
   const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.a), 0,
                                                       (int)(fast ? a_elems * 2 : 0), 0x00020000);
   const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.b), 0,
@@ -218,9 +223,17 @@ conv_gemm_kernel(GemmArgs args) {
   auto load_tile_fast = [&](int t) {
     if constexpr (PRE) amask = 0;
     const int kb = t * BK;                       // uniform
-    const bool kv = kb < KD;
-    const int tap = kv ? kb / Acin : 0;          // uniform (scalar unit)
-    const int ci = kb - tap * Acin + kg * 8;
+    bool kv = kb < KD;
+    int tap = kv ? kb / Acin : 0;                // uniform (scalar unit)
+    int ci = kb - tap * Acin + kg * 8;
+    if constexpr (NARROW_OK) {
+      if (narrow) {   // this thread's own tap (K tail checked per 8-channel group)
+        const int k = kb + kg * 8;
+        kv = k < KD;
+        tap = kv ? k / Acin : 0;
+        ci = k - tap * Acin;
+      }
+    }
     if constexpr (PRE) pre_ci = kv ? ci : 0;
     int rr = tap / g.kw, cc = tap - rr * g.kw;
     if (MODE == MODE_DGRAD && args.par) class_tap(tap, rr, cc);

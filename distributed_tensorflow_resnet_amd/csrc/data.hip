@@ -236,7 +236,7 @@ namespace dtr {
 __global__ void __launch_bounds__(256)
 imagenet_u8_pack_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int H, int W,
                         unsigned long long seed, const long long* gstep, int train,
-                        uint4* __restrict__ zero, long zero_vec, long npix) {
+                        uint4* __restrict__ zero, long zero_vec, long npix, int s2d) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < zero_vec; i += (long)gridDim.x * 256)
     zero[i] = make_uint4(0u, 0u, 0u, 0u);
   const long p = blockIdx.x * 256L + threadIdx.x;
@@ -252,22 +252,73 @@ imagenet_u8_pack_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out,
   }
   const int xs = flip ? W - 1 - x : x;
   const uint8_t* src = img + ((n * H + y) * (long)W + xs) * 3;
+  const bf16 c0 = (bf16)((float)src[0] - 123.68f);
+  const bf16 c1 = (bf16)((float)src[1] - 116.78f);
+  const bf16 c2 = (bf16)((float)src[2] - 103.94f);
+  if (s2d) {   // space-to-depth stem operand [N][H/2][W/2][16] (stem_s2d_pack below)
+    bf16x4 r = {c0, c1, c2, (bf16)0.f};
+    const long q = (n * (H >> 1) + (y >> 1)) * (long)(W >> 1) + (x >> 1);
+    *reinterpret_cast<bf16x4*>(out + q * 16 + ((y & 1) * 2 + (x & 1)) * 4) = r;
+    return;
+  }
   bf16x8 r = {};
-  r[0] = (bf16)((float)src[0] - 123.68f);
-  r[1] = (bf16)((float)src[1] - 116.78f);
-  r[2] = (bf16)((float)src[2] - 103.94f);
+  r[0] = c0;
+  r[1] = c1;
+  r[2] = c2;
   *reinterpret_cast<bf16x8*>(out + p * 8) = r;
 }
 
 void imagenet_u8_pack(const uint8_t* img, bf16* out, int N, int H, int W,
                       unsigned long long seed, const long long* gstep, int train, void* zero,
-                      long zero_bytes, hipStream_t s) {
+                      long zero_bytes, int s2d, hipStream_t s) {
   if (zero_bytes % 16 != 0) throw std::invalid_argument("imagenet_u8_pack: zero_bytes % 16");
+  if (s2d && ((H | W) & 1)) throw std::invalid_argument("imagenet_u8_pack: s2d needs even H, W");
   const long npix = (long)N * H * W;
   const int grid = (int)((npix + 255) / 256);
   hipLaunchKernelGGL(imagenet_u8_pack_kernel, dim3(grid), dim3(256), 0, s, img, out, H, W, seed,
                      gstep, train, reinterpret_cast<uint4*>(zero), zero ? zero_bytes / 16 : 0,
-                     npix);
+                     npix, s2d);
+  DTR_CHECK_LAUNCH();
+}
+
+// Space-to-depth ImageNet stem.  The 7x7 / stride-2 conv (TF fixed padding 3) over
+// a 224x224x3 image equals a 4x4 / stride-1 conv (padding 2 before, 1 after) over
+// the 112x112x16 space-to-depth image S[q][p][(rh*2 + rw)*4 + c] = X[2q+rh][2p+rw][c]
+// (c = 3 zero): out(o) = sum_th S(o - 2 + th) reads rows 2o - 4 + 2th + rh, i.e.
+// tap kh = 2th + rh - 1 of the 7x7 filter (kh = -1 is a zero row).  K = 4*4*16 = 256
+// instead of 7*7*8 = 392 (57 % of the MACs real instead of 37 %), stride-1 gathers of
+// 32-B pixel rows, and a weight gradient of 256 columns (two 128-wide tiles instead of
+// four, the last 94 % empty).  The fp32 master weight stays the 7x7x3 HWIO of the
+// checkpoint; these two kernels map it to the bf16 4x4x16 OHWI operand and the 4x4x16
+// HWIO weight gradient back.
+__global__ void stem_s2d_pack_kernel(const float* __restrict__ w7, bf16* __restrict__ w4, int K) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // [K][4][4][16]
+  if (i >= K * 256) return;
+  const int o = i >> 8, r = i & 255;
+  const int th = r >> 6, tw = (r >> 4) & 3, ch = r & 15;
+  const int kh = 2 * th + (ch >> 3) - 1, kw = 2 * tw + ((ch >> 2) & 1) - 1, c = ch & 3;
+  float v = 0.f;
+  if (c < 3 && kh >= 0 && kh < 7 && kw >= 0 && kw < 7) v = w7[((kh * 7 + kw) * 3 + c) * K + o];
+  w4[i] = (bf16)v;
+}
+
+__global__ void stem_s2d_grad_kernel(const float* __restrict__ g4, float* __restrict__ g7, int K) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // [7][7][3][K]
+  if (i >= 147 * K) return;
+  const int o = i % K, t = i / K;
+  const int c = t % 3, tap = t / 3;
+  const int kh = tap / 7 + 1, kw = tap % 7 + 1;   // +1: row / column of the 8x8 grid
+  const int ch = ((kh & 1) * 2 + (kw & 1)) * 4 + c;
+  g7[i] = g4[(((kh >> 1) * 4 + (kw >> 1)) * 16 + ch) * K + o];
+}
+
+void stem_s2d_pack(const float* w7, bf16* w4, int K, hipStream_t s) {
+  hipLaunchKernelGGL(stem_s2d_pack_kernel, dim3(K), dim3(256), 0, s, w7, w4, K);
+  DTR_CHECK_LAUNCH();
+}
+
+void stem_s2d_grad(const float* g4, float* g7, int K, hipStream_t s) {
+  hipLaunchKernelGGL(stem_s2d_grad_kernel, dim3((147 * K + 255) / 256), dim3(256), 0, s, g4, g7, K);
   DTR_CHECK_LAUNCH();
 }
 

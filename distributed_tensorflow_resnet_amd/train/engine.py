@@ -191,6 +191,14 @@ class Engine:
         self.wgrad_group = min(8, max(1, int(os.environ.get("DTR_WGRAD_GROUP", "1"))))
         # which input-channel counts group (bit 0: 16, 1: 32, 2: 64, 3: others; -1 all)
         self.wgrad_group_cmask = int(os.environ.get("DTR_WGRAD_GROUP_C", "-1"))
+        # Backward tail: the weight gradients still queued for the side stream when the
+        # main stream's dgrad chain ends (the first stage's) are shared out -- this
+        # fraction of them, the last-queued ones, runs on the otherwise idle main stream
+        # after the stem (_split_tail).  0 = all on the side stream.  Measured (CIFAR RN50,
+        # ms/step, 0 / 0.5 / 0.75 / 1): bs16 0.978 / 0.972 / 0.972 / 0.970, bs32 1.002 /
+        # 0.994 / 1.017 / 1.011, bs64 1.128 / 1.131 / 1.131 / 1.130, bs128 1.326 / 1.316 /
+        # 1.314 / 1.303 (scripts/ab_tail.sh)
+        self.tail_main = min(1.0, max(0.0, float(os.environ.get("DTR_TAIL_MAIN", "1"))))
         self.markers = os.environ.get("DTR_ROCTX", "0") != "0"
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
@@ -198,6 +206,13 @@ class Engine:
         self.input_mode = input_mode
         self.kpad = _ceil(spec.num_classes, 16) * 16
         self.cpad_in = 8
+        # ImageNet stem as a space-to-depth 4x4/1 conv over [N, H/2, W/2, 16] (data.hip
+        # stem_s2d_*: K 392 -> 256, stride-1 gathers, a 2-tile weight gradient instead of 4)
+        st = spec.stem
+        self.stem_s2d = (os.environ.get("DTR_STEM_S2D", "1") != "0" and st.kh == 7 and
+                         st.kw == 7 and st.stride == 2 and st.cin <= 3 and
+                         spec.image_h % 2 == 0 and spec.image_w % 2 == 0 and
+                         2 * st.ho == spec.image_h and 2 * st.wo == spec.image_w)
 
         dev = self.device
         self.params = ParamStore(spec, device=dev)
@@ -291,8 +306,11 @@ class Engine:
                 cpad = self.cpad_in if c.cin < 8 else c.cin
                 rec["kh"], rec["kw"], rec["C"], rec["K"] = c.kh, c.kw, c.cin, c.cout
                 rec["cpad"], rec["kpad"] = cpad, c.cout
-                rec["bf_ohwi"] = bf_total
-                bf_total += c.cout * taps * cpad
+                if self.stem_s2d and c.name == spec.stem.name:
+                    rec["bf_ohwi"] = -1   # its OHWI operand comes from stem_s2d_pack
+                else:
+                    rec["bf_ohwi"] = bf_total
+                    bf_total += c.cout * taps * cpad
                 if c.cin >= 8:   # the stem never needs dgrad
                     rec["bf_hwio"] = bf_total
                     bf_total += taps * c.cin * c.cout
@@ -325,8 +343,15 @@ class Engine:
             if s.kind == "conv":
                 c = conv_specs[s.name.split("/")[0]]
                 cin = self.cpad_in if c.cin < 8 else c.cin
+                ohwi = bptr + 2 * int(rec["bf_ohwi"])
+                if self.stem_s2d and c.name == spec.stem.name:
+                    cin = 16
+                    self.stem_w4 = torch.zeros(c.cout * 256, dtype=BF16, device=self.device)
+                    self.stem_g4 = torch.zeros(c.cout * 256, device=self.device)
+                    self.stem_master = mptr + 4 * s.offset
+                    ohwi = self.stem_w4.data_ptr()
                 self.convs[c.name] = _Conv(
-                    c, cin, bptr + 2 * int(rec["bf_ohwi"]),
+                    c, cin, ohwi,
                     bptr + 2 * int(rec["bf_hwio"]) if rec["bf_hwio"] >= 0 else 0,
                     gptr + 4 * s.offset, c.cin, s.name)
             elif s.kind == "dense_kernel":
@@ -374,7 +399,7 @@ class Engine:
             self.img_u8 = torch.zeros((N, 3, H, W), dtype=torch.uint8, device=dev)
         elif self.input_mode == "imagenet_u8":   # VGG crops, HWC (imagenet_u8_pack)
             self.img_u8 = torch.zeros((N, H, W, 3), dtype=torch.uint8, device=dev)
-        self.x_in = torch.zeros((N, H, W, self.cpad_in), dtype=BF16, device=dev)
+        self.x_in = torch.zeros(self._x_in_shape(N), dtype=BF16, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
         st = spec.stem
         self.stem_out = torch.empty((N, st.ho, st.wo, st.cout), dtype=BF16, device=dev)
@@ -453,7 +478,8 @@ class Engine:
         for name, c in self.convs.items():
             sp, pps = self.nat.wgrad_pick_splits(self._geom(c, N))
             self.wg_off[name] = (tot, sp, pps)
-            tot += sp * c.spec.cout * c.spec.kh * c.spec.kw * c.cin
+            g = self._geom(c, N)
+            tot += sp * c.spec.cout * g[7] * g[8] * g[3]
         sp, pps = self.nat.wgrad_pick_splits(self._dense_geom(N))
         self.wg_off["dense"] = (tot, sp, pps)
         tot += sp * self.kpad * F
@@ -462,8 +488,29 @@ class Engine:
         self.xent_ws = torch.empty(self.nat.softmax_xent_ws_floats(N, self.kpad), device=dev)
 
     # ------------------------------------------------------------------ helpers
+    def _x_in_shape(self, N):
+        H, W = self.spec.image_h, self.spec.image_w
+        return (N, H // 2, W // 2, 16) if self.stem_s2d else (N, H, W, self.cpad_in)
+
+    def _stem_input(self, x):
+        """[N, H, W, C <= cpad] image batch -> the stem's operand layout (x_in)."""
+        x = x.to(self.device)
+        N, H, W, C = x.shape
+        if self.stem_s2d:   # channel (rh * 2 + rw) * 4 + c of pixel (2q + rh, 2p + rw)
+            xp = torch.zeros((N, H, W, 4), dtype=BF16, device=self.device)
+            xp[..., :C] = x.to(BF16)
+            return xp.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(
+                N, H // 2, W // 2, 16)
+        if C != self.cpad_in:
+            xp = torch.zeros((N, H, W, self.cpad_in), dtype=BF16, device=self.device)
+            xp[..., :C] = x.to(BF16)
+            return xp
+        return x.to(BF16)
+
     def _geom(self, c: _Conv, N):
         s = c.spec
+        if self.stem_s2d and s.name == self.spec.stem.name:
+            return [N, s.h // 2, s.w // 2, 16, s.ho, s.wo, s.cout, 4, 4, 1, 2]
         return [N, s.h, s.w, c.cin, s.ho, s.wo, s.cout, s.kh, s.kw, s.stride, (s.kh - 1) // 2]
 
     def _dense_geom(self, N):
@@ -703,7 +750,11 @@ class Engine:
             self._emit_wgrads(plan, [desc])
             # a side-stream reduce of this slab must fork after it (_flush_side)
             self._main_wgrad = self.fork_wgrad
-        self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
+        if self.stem_s2d and s.name == self.spec.stem.name:   # 4x4x16 HWIO, mapped back by _emit_reduce
+            self._pending[c.name] = (part, self.stem_g4.data_ptr(), sp, s.cout, s.cout, 16, 16, 16)
+        else:
+            self._pending[c.name] = (part, c.grad, sp, s.cout, s.cout, s.kh * s.kw, c.cin,
+                                     c.cin_valid)
         self._produced.add(c.name)
 
     def _bn_bwd(self, plan, bn: _BN, dy, x, dx, add=None, reduced: bool = False):
@@ -765,6 +816,26 @@ class Engine:
         self._emit_wgrads(plan, self._side_q)
         plan.use_stream(0)
         self._side_q, self._side_blocks = [], 0
+
+    def _split_tail_on(self) -> bool:
+        return self.fork_wgrad and self.tail_main > 0
+
+    def _split_tail(self, plan) -> list:
+        """End of the dgrad chain (first block done): fork the first part of the queued
+        weight gradients to the side stream now and return the last `tail_main`
+        fraction, which the main stream runs after the stem instead of idling until the
+        side stream drains them.  The bucket reduces are emitted afterwards (forced
+        flush), so no reduce can read a slab before its main-stream wgrad."""
+        q = self._side_q
+        k = len(q) - int(round(self.tail_main * len(q)))
+        while k < len(q) and callable(q[k]):   # queued non-wgrad side ops stay on the side
+            k += 1
+        self._side_q = q[:k]
+        if self._side_q:
+            self._flush_side(plan, force=True)
+        else:
+            self._side_blocks = 0
+        return q[k:]
 
     def _wgrad_matpre(self, geom) -> bool:
         """Materialize the BN+ReLU of a wgrad's input first (DTR_WGRAD_MATPRE=1): 3x3
@@ -903,6 +974,10 @@ class Engine:
         self._keep.append(t)
         plan.use_stream(1 if self.fork_wgrad else 0)
         plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
+        st = self.spec.stem
+        sc = self.convs[st.name]
+        if self.stem_s2d and sc.name in names:   # names: slot names ("conv2d/kernel")
+            plan.stem_s2d_grad(self.stem_g4.data_ptr(), sc.grad, st.cout)
         plan.use_stream(0)
 
     def _g(self, i, shape):
@@ -937,7 +1012,8 @@ class Engine:
                                self.gstep.data_ptr(), 1, 0, *zero)
         elif self.input_mode == "imagenet_u8":
             plan.imagenet_u8_pack(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
-                                  spec.image_w, self.data_seed, self.gstep.data_ptr(), 1, *zero)
+                                  spec.image_w, self.data_seed, self.gstep.data_ptr(), 1, *zero,
+                                  int(self.stem_s2d))
         # ---- forward
         stem = self.convs[spec.stem.name]
         blocks = spec.blocks
@@ -1062,6 +1138,7 @@ class Engine:
                            0, 0, 0, 0, 0, 0, 0, dg, [], [], [], [], [], BN_DECAY, BN_EPS, 1)
             plan.avgpool_bwd(self.dpooled.data_ptr(), dact.data_ptr(), N, HL * WL, F)
             self._bn_bwd(plan, fbn, dact, XL, dout)
+        main_tail = []
         for i in range(len(blocks) - 1, -1, -1):
             b = blocks[i]
             X = self.X[i]
@@ -1099,6 +1176,9 @@ class Engine:
             dx = self._g(o2, tuple(X.shape))
             self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
+            if i == 0 and self._split_tail_on():
+                main_tail = self._split_tail(plan)
+                continue
             # the last block's weight gradients go out now so they overlap the stem's
             # backward (max-pool gather) instead of queueing behind it
             self._flush_side(plan, force=i == 0)
@@ -1118,6 +1198,9 @@ class Engine:
         # The stem's weight gradient is the main stream's last op (nothing else is
         # left for it), running alongside the side stream's last weight gradients.
         self._conv_bwd(plan, stem, dstem_src, self.x_in, N, None, side=False)
+        if main_tail:   # the main stream's share of the tail; the reduces fork after it
+            self._emit_wgrads(plan, main_tail)
+            self._main_wgrad = True
         self._flush_side(plan, force=True)
         self._flush_buckets(plan, force=True)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
@@ -1137,6 +1220,8 @@ class Engine:
         plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
                        self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr(),
                        self.gstep.data_ptr())   # + global_step += 1
+        if self.stem_s2d:
+            plan.stem_s2d_pack(self.stem_master, self.stem_w4.data_ptr(), spec.stem.cout)
         self._t_opt_end = plan.timing_point("opt_end")
         self.seg["opt"] = (b2, plan.size())
         # 1/2 sum v^2 of the weights, which only feeds the logged `cost`
@@ -1162,6 +1247,9 @@ class Engine:
         self.nat.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
                            self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
                            self.wbf.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+        if self.stem_s2d:
+            self.nat.stem_s2d_pack(self.stem_master, self.stem_w4.data_ptr(),
+                                   self.spec.stem.cout, torch.cuda.current_stream().cuda_stream)
 
     def _run(self, name, stream):
         a, b = self.seg[name]
@@ -1314,10 +1402,8 @@ class Engine:
             self.img_u8.copy_(images, non_blocking=True)
         else:
             x = images
-            if x.dim() == 4 and x.shape[-1] != self.cpad_in:
-                xp = torch.zeros(self.x_in.shape, dtype=BF16, device=self.device)
-                xp[..., :x.shape[-1]] = x.to(self.device, BF16)
-                x = xp
+            if x.dim() == 4 and tuple(x.shape) != tuple(self.x_in.shape):
+                x = self._stem_input(x)
             self.x_in.copy_(x, non_blocking=True)
         self.labels.copy_(labels.to(torch.int32), non_blocking=True)
 
@@ -1328,7 +1414,9 @@ class Engine:
                                             dtype=torch.uint8))
         else:
             npix = self.N * self.spec.image_h * self.spec.image_w
-            self.nat.synthetic_images(self.x_in.data_ptr(), npix, 3, self.cpad_in, seed,
+            # s2d: every 16-channel row holds 4 pixels of 3 (+1 zero) channels
+            self.nat.synthetic_images(self.x_in.data_ptr(), npix, 3,
+                                      4 if self.stem_s2d else self.cpad_in, seed,
                                       torch.cuda.current_stream().cuda_stream)
         self.labels.copy_(torch.randint(0, self.spec.num_classes, (self.N,), generator=g,
                                         dtype=torch.int32))
@@ -1393,7 +1481,7 @@ class _EvalPlan:
         nat, spec, dev = eng.nat, eng.spec, eng.device
         H, W = spec.image_h, spec.image_w
         self.img_u8 = torch.zeros((N, 3, H, W), dtype=torch.uint8, device=dev)
-        self.x_in = torch.zeros((N, H, W, eng.cpad_in), dtype=BF16, device=dev)
+        self.x_in = torch.zeros(eng._x_in_shape(N), dtype=BF16, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
         self.probs = torch.zeros((N, eng.kpad), device=dev)
         self.xent_ws = torch.empty(eng.nat.softmax_xent_ws_floats(N, eng.kpad), device=dev)
@@ -1402,8 +1490,9 @@ class _EvalPlan:
         p = nat.Plan()
         self.plan = p
         self.input_plan = nat.Plan()
-        self.input_plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, H, W,
-                                      eng.cpad_in, 4, 0, 0, 0, 0, 0, 0)
+        if not eng.stem_s2d:   # raw uint8 CIFAR records (run(raw_u8=True))
+            self.input_plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, H, W,
+                                          eng.cpad_in, 4, 0, 0, 0, 0, 0, 0)
         st = spec.stem
         stem = eng.convs[st.name]
         bufs = []
@@ -1473,10 +1562,8 @@ class _EvalPlan:
                 self.input_plan.run(0, self.input_plan.size(), st, 0)
             else:
                 x = images.to(self.eng.device)
-                if x.shape[-1] != self.eng.cpad_in:
-                    xp = torch.zeros(self.x_in.shape, device=self.eng.device)
-                    xp[..., :x.shape[-1]] = x.float()
-                    x = xp
+                if tuple(x.shape) != tuple(self.x_in.shape):
+                    x = self.eng._stem_input(x.float())
                 self.x_in.copy_(x.to(BF16))
         if labels is not None:
             self.labels.copy_(labels.to(torch.int32))

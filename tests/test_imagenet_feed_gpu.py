@@ -23,7 +23,7 @@ def test_u8_pack_flip_and_mean(gpu):
     zero = torch.ones(64, device=gpu)
     st = torch.cuda.current_stream().cuda_stream
     nat.imagenet_u8_pack(img.data_ptr(), out.data_ptr(), N, H, W, 99, gstep.data_ptr(), 1,
-                         zero.data_ptr(), zero.numel() * 4, st)
+                         zero.data_ptr(), zero.numel() * 4, 0, st)
     torch.cuda.synchronize()
     assert torch.count_nonzero(zero) == 0
     assert torch.count_nonzero(out[..., 3:]) == 0
@@ -37,9 +37,18 @@ def test_u8_pack_flip_and_mean(gpu):
         flips += 1
     assert 2 <= flips <= N - 2          # a fair coin per image
     # eval (train=0): no flip; a different step reshuffles the flips
-    nat.imagenet_u8_pack(img.data_ptr(), out.data_ptr(), N, H, W, 99, gstep.data_ptr(), 0, 0, 0, st)
+    nat.imagenet_u8_pack(img.data_ptr(), out.data_ptr(), N, H, W, 99, gstep.data_ptr(), 0, 0, 0, 0, st)
     torch.cuda.synchronize()
     assert torch.equal(out[..., :3].float().cpu(), ref)
+    # space-to-depth stem operand: [N][H/2][W/2][(rh*2 + rw)*4 + c], c = 3 zero
+    s2d = torch.full((N, H // 2, W // 2, 16), 7.0, dtype=torch.bfloat16, device=gpu)
+    nat.imagenet_u8_pack(img.data_ptr(), s2d.data_ptr(), N, H, W, 99, gstep.data_ptr(), 0, 0, 0, 1,
+                         st)
+    torch.cuda.synchronize()
+    r4 = torch.zeros(N, H, W, 4)
+    r4[..., :3] = ref
+    want = r4.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 16)
+    assert torch.equal(s2d.float().cpu(), want)
 
 
 def test_engine_trains_from_u8_crops(gpu):
