@@ -326,6 +326,18 @@ static Launch mk_bn_relu_apply(ptr_t x, ptr_t scale, ptr_t shift, ptr_t y, int M
   };
 }
 
+static Launch mk_bn_relu_apply_acc(ptr_t x, ptr_t y, int M, int C, ptr_t acc, ptr_t gamma,
+                                   ptr_t beta, ptr_t mmean, ptr_t mvar, float momentum, float eps,
+                                   int update_moving, ptr_t mean, ptr_t rstd, ptr_t scale,
+                                   ptr_t shift) {
+  return [=](hipStream_t s) {
+    bn_relu_apply_acc(P<const bf16>(x), P<bf16>(y), M, C, P<const double>(acc),
+                      P<const float>(gamma), P<const float>(beta), P<float>(mmean), P<float>(mvar),
+                      momentum, eps, update_moving, P<float>(mean), P<float>(rstd), P<float>(scale),
+                      P<float>(shift), s);
+  };
+}
+
 static Launch mk_bnrelu_avgpool(ptr_t x, ptr_t scale, ptr_t shift, ptr_t pooled, int N, int HW,
                                 int C) {
   if (C % 8 || C > 2048) throw std::invalid_argument("avgpool: C%8==0 and C<=2048");
@@ -985,6 +997,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "bn_bwd_finalize", mk_bn_bwd_finalize);
   def_op(m, plan, "bn_bwd_apply", mk_bn_bwd_apply);
   def_op(m, plan, "bn_relu_apply", mk_bn_relu_apply);
+  def_op(m, plan, "bn_relu_apply_acc", mk_bn_relu_apply_acc);
   def_op(m, plan, "bnrelu_avgpool", mk_bnrelu_avgpool);
   def_op(m, plan, "avgpool_bwd", mk_avgpool_bwd);
   def_op(m, plan, "softmax_xent", mk_softmax_xent);

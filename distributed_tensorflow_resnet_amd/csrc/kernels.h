@@ -233,6 +233,11 @@ void bn_bwd_finalize(const float* part, int tiles, int M, int C, const float* ga
 void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
                        const float* scale, const float* shift, const float* coef,
                        const bf16* add, bf16* dx, int M, int C, hipStream_t s);
+// acc-mode BN finalize + materializing BN+ReLU pass in one launch (bn.hip)
+void bn_relu_apply_acc(const bf16* x, bf16* y, int M, int C, const double* acc,
+                       const float* gamma, const float* beta, float* moving_mean,
+                       float* moving_var, float momentum, float eps, int update_moving,
+                       float* mean, float* rstd, float* scale, float* shift, hipStream_t s);
 void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M,
                    int C, hipStream_t s);
 // The same apply with the finalize fused in (accumulator mode, small C): every block

@@ -619,8 +619,17 @@ class Engine:
         if y is None:
             self._bn_finalize(plan, bn)
             return x, bn
-        self._bn_finalize(plan, bn, consumer_conv=False)
         C = bn.spec.channels
+        if (bn.pending is not None and bn.pending[0] == "acc"
+                and os.environ.get("DTR_FUSED_APPLY_FIN", "1") != "0"):
+            # the apply pass finalizes too (no bn_finalize launch in between)
+            _, part, M = bn.pending
+            bn.pending = None
+            plan.bn_relu_apply_acc(x.data_ptr(), y.data_ptr(), M, C, part, bn.gamma, bn.beta,
+                                   bn.mmean, bn.mvar, BN_DECAY, BN_EPS, 1, bn.mean.data_ptr(),
+                                   bn.rstd.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr())
+            return y, None
+        self._bn_finalize(plan, bn, consumer_conv=False)
         plan.bn_relu_apply(x.data_ptr(), bn.scale.data_ptr(), bn.shift.data_ptr(), y.data_ptr(),
                            x.numel() // C, C)
         return y, None
