@@ -587,31 +587,30 @@ bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
   const long T = (long)gridDim.x * 256;
   const int c0 = (int)(threadIdx.x % G) * 8;
   float sc[8], sh[8], mu[8], rs[8], ca[8], cb[8], cc[8];
-  __shared__ float cf[3][BWD_ACC_FIN_MAXC];
+  extern __shared__ float cf[];   // acc mode: [3][C] coefficients
   const float* cfp = coef;
-  int ld = C;
   if (fin.acc != nullptr) {   // accumulator mode: this launch is also the finalize
-    const int c = threadIdx.x;
-    if (c < C) {
+    for (int c = threadIdx.x; c < C; c += 256) {
       double s1, s2;
       bn_acc_sums(fin.acc, C, c, s1, s2);
       const float sg = (float)s1, sgx = (float)s2;
       const float a = fin.gamma[c] * rstd[c];
-      cf[0][c] = a;
-      cf[1][c] = a * sg / (float)fin.M;
-      cf[2][c] = a * sgx / (float)fin.M;
+      const float b = a * sg / (float)fin.M, d = a * sgx / (float)fin.M;
+      cf[c] = a;
+      cf[C + c] = b;
+      cf[2 * C + c] = d;
       if (blockIdx.x == 0) {
         fin.dbeta[c] = sg;
         fin.dgamma[c] = sgx;
-        fin.coef[c] = cf[0][c];
-        fin.coef[C + c] = cf[1][c];
-        fin.coef[2 * C + c] = cf[2][c];
+        fin.coef[c] = a;
+        fin.coef[C + c] = b;
+        fin.coef[2 * C + c] = d;
       }
     }
     __syncthreads();
-    cfp = &cf[0][0];
-    ld = BWD_ACC_FIN_MAXC;
+    cfp = cf;
   }
+  const int ld = C;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = c0 + j;
@@ -666,10 +665,34 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
   DTR_CHECK_LAUNCH();
 }
 
+// Grid of the finalize-fused apply: every workgroup re-reads 16 fp64 per channel, so
+// the grid is capped (BWD_FIN_BLOCKS, 4 vectors in flight per thread instead of 2).
+constexpr int BWD_FIN_U = 4;
+constexpr long BWD_FIN_BLOCKS = 256;
+static long bwd_fin_blocks(long nvec) {
+  const long b = (nvec + 256L * BWD_FIN_U - 1) / (256L * BWD_FIN_U);
+  return b < BWD_FIN_BLOCKS ? b : BWD_FIN_BLOCKS;
+}
+
+// round-1 rule (the CIFAR shapes): C <= 64 on the uncapped U = 2 grid of <= 1024 blocks
+static bool bwd_fin_small(int M, int C) {
+  return C <= BWD_ACC_FIN_MAXC && ((long)M * C / 8 + 511) / 512 <= 1024;
+}
+
+// DTR_BWD_APPLY_FIN: 0 = only C <= 64 (round-1 rule), 1 (default) = when the grid's
+// redundant finalize reads stay <= 1/4 of the apply's streamed bytes, 2 = always.
 bool bn_bwd_apply_acc_fits(int M, int C) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = std::getenv("DTR_BWD_APPLY_FIN");
+    mode = e ? std::atoi(e) : 1;
+  }
   const long nvec = (long)M * C / 8;
-  return C <= BWD_ACC_FIN_MAXC && C % 8 == 0 && 256 % (C / 8) == 0 &&
-         (nvec + 511) / 512 <= 1024;   // every block re-reads 16 fp64 per channel
+  if (C % 8 != 0 || 256 % (C / 8) != 0 || C > 2048) return false;
+  if (bwd_fin_small(M, C)) return true;
+  if (mode == 0) return false;
+  if (mode >= 2) return true;
+  return bwd_fin_blocks(nvec) * C * 16L * 8 <= nvec * 48 / 4;
 }
 
 void bn_relu_bwd_apply_acc(const bf16* dy, const bf16* x, const float* mean, const float* rstd,
@@ -678,10 +701,16 @@ void bn_relu_bwd_apply_acc(const bf16* dy, const bf16* x, const float* mean, con
   if (!bn_bwd_apply_acc_fits(M, C))
     throw std::runtime_error("bn_relu_bwd_apply_acc: shape exceeds the fused-finalize bound");
   const long nvec = (long)M * C / 8;
-  constexpr int U = 2;
-  const long blocks = (nvec + 256L * U - 1) / (256L * U);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3((unsigned)blocks), dim3(256), 0, s, dy, x,
-                     mean, rstd, scale, shift, fin.coef, add, dx, nvec, C, fin);
+  if (bwd_fin_small(M, C)) {   // measured: CIFAR keeps its wider U = 2 grid
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3((unsigned)((nvec + 511) / 512)), dim3(256),
+                       (size_t)3 * C * sizeof(float), s, dy, x, mean, rstd, scale, shift, fin.coef,
+                       add, dx, nvec, C, fin);
+    DTR_CHECK_LAUNCH();
+    return;
+  }
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<BWD_FIN_U>, dim3((unsigned)bwd_fin_blocks(nvec)),
+                     dim3(256), (size_t)3 * C * sizeof(float), s, dy, x, mean, rstd, scale, shift,
+                     fin.coef, add, dx, nvec, C, fin);
   DTR_CHECK_LAUNCH();
 }
 
@@ -694,6 +723,80 @@ __global__ void bn_relu_apply_kernel(const bf16* __restrict__ x, const float* __
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (size_t)i * 8);
     *reinterpret_cast<bf16x8*>(y + (size_t)i * 8) = affine_relu8(v, scale + c0, shift + c0);
   }
+}
+
+// Accumulator-mode finalize fused into the materializing BN+ReLU pass (the inner
+// bottleneck BatchNorms of the 14x14 / 7x7 stages, Engine._materialize_bn): every
+// workgroup finalizes the channels from the fp64 replicas into an LDS scale/shift table
+// (the bn_finalize_acc math; block 0 also writes mean/rstd/scale/shift and the moving
+// averages for the BN's later users), then streams U vectors per thread per round.
+// <= 256 workgroups keep the redundant finalize reads (16 fp64 per channel per
+// workgroup) at a few MB of L2 traffic; one launch instead of finalize + apply.
+template <int U>
+__global__ void __launch_bounds__(256)
+bn_relu_apply_acc_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, unsigned nvec, int M,
+                         int C, const double* __restrict__ acc, const float* __restrict__ gamma,
+                         const float* __restrict__ beta, float* moving_mean, float* moving_var,
+                         float momentum, float eps, int update_moving, float* mean_out,
+                         float* rstd_out, float* scale_out, float* shift_out) {
+  extern __shared__ __attribute__((aligned(16))) float tab[];   // [2][C]: scale, shift
+  for (int c = threadIdx.x; c < C; c += 256) {
+    double s1, s2;
+    bn_acc_sums(acc, C, c, s1, s2);
+    const double dm = s1 / (double)M;
+    const double var = fmax(s2 / (double)M - dm * dm, 0.0);
+    const float mean = (float)dm, fvar = (float)var;
+    const float rstd = rsqrtf(fvar + eps);
+    const float sc = gamma[c] * rstd, sh = beta[c] - mean * sc;
+    tab[c] = sc;
+    tab[C + c] = sh;
+    if (blockIdx.x == 0) {
+      mean_out[c] = mean;
+      rstd_out[c] = rstd;
+      scale_out[c] = sc;
+      shift_out[c] = sh;
+      if (update_moving) {
+        const float uvar = M > 1 ? (float)(var * M / (M - 1.0)) : fvar;
+        const float mm = moving_mean[c], mvv = moving_var[c];
+        moving_mean[c] = mm - (1.f - momentum) * (mm - mean);
+        moving_var[c] = mvv - (1.f - momentum) * (mvv - uvar);
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned G = (unsigned)C / 8, T = gridDim.x * 256u;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < nvec; i += U * T) {
+    bf16x8 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned iu = i + u * T;
+      if (iu < nvec) v[u] = *reinterpret_cast<const bf16x8*>(x + (size_t)iu * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned iu = i + u * T;
+      if (iu >= nvec) break;
+      const int c0 = (int)(iu % G) * 8;
+      *reinterpret_cast<bf16x8*>(y + (size_t)iu * 8) = affine_relu8(v[u], tab + c0, tab + C + c0);
+    }
+  }
+}
+
+void bn_relu_apply_acc(const bf16* x, bf16* y, int M, int C, const double* acc,
+                       const float* gamma, const float* beta, float* moving_mean,
+                       float* moving_var, float momentum, float eps, int update_moving,
+                       float* mean, float* rstd, float* scale, float* shift, hipStream_t s) {
+  const long nvec = (long)M * C / 8;
+  if (C % 8 != 0 || C > 4096 || nvec >= (1L << 31))
+    throw std::runtime_error("bn_relu_apply_acc: C % 8, C <= 4096, M*C/8 < 2^31");
+  constexpr int U = 4;
+  long blocks = (nvec + 256L * U - 1) / (256L * U);
+  if (blocks > 256) blocks = 256;
+  hipLaunchKernelGGL(bn_relu_apply_acc_kernel<U>, dim3((unsigned)blocks), dim3(256),
+                     (size_t)2 * C * sizeof(float), s, x, y, (unsigned)nvec, M, C, acc, gamma, beta,
+                     moving_mean, moving_var, momentum, eps, update_moving, mean, rstd, scale,
+                     shift);
+  DTR_CHECK_LAUNCH();
 }
 
 void bn_relu_apply(const bf16* x, const float* scale, const float* shift, bf16* y, int M, int C,

@@ -776,8 +776,17 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
     const char* e = std::getenv("DTR_NBUF1_KT");
     g_nbuf1 = e ? std::atoi(e) : 1;
   }
+  // The narrow stem operand (8 / 16 channels, K <= 4-7 tiles, 12.5k workgroups of pure
+  // load latency): single-buffered too, for more co-resident workgroups per CU
+  // (DTR_NARROW_NBUF1=1: on; A/B pending)
+  static int narrow_nbuf1 = -1;
+  if (narrow_nbuf1 < 0) {
+    const char* e = std::getenv("DTR_NARROW_NBUF1");
+    narrow_nbuf1 = (e && e[0] == '1') ? 1 : 0;
+  }
+  const bool narrow = MODE == MODE_FWD && (FLAGS & F_PRE) == 0 && a.g.C < 64 && narrow_nbuf1;
   if constexpr (BM * BN >= 128 * 64 && (FLAGS & F_ABWD) == 0) {
-    if ((a.Kdim + 63) / 64 <= g_nbuf1 && !conv_gemm_fast(a, MODE)) {
+    if (((a.Kdim + 63) / 64 <= g_nbuf1 || narrow) && !conv_gemm_fast(a, MODE)) {
       launch_nbuf<BM, BN, WM, WN, MODE, FLAGS, 1>(a, s);
       return;
     }
