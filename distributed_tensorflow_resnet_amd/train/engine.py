@@ -497,6 +497,8 @@ class Engine:
         x = x.to(self.device)
         N, H, W, C = x.shape
         if self.stem_s2d:   # channel (rh * 2 + rw) * 4 + c of pixel (2q + rh, 2p + rw)
+            if C > 4:       # an NHWC-8 (zero-padded) batch: its 3 image channels
+                x, C = x[..., :3], 3
             xp = torch.zeros((N, H, W, 4), dtype=BF16, device=self.device)
             xp[..., :C] = x.to(BF16)
             return xp.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(
