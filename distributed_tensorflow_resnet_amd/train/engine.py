@@ -182,7 +182,11 @@ class Engine:
             # measured: eager + forked wgrad stream beats hipGraph replay (which
             # handles the cross-stream event edges poorly); graphs stay single-stream
             fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
-        self.fork_every = max(1, int(os.environ.get("DTR_FORK_EVERY", "2")))
+        # residual blocks per side-stream fork.  Measured with the tail split and the
+        # tail reduces on main (ms/step, every 2 / 4 / 8): CIFAR bs16 0.959 / 0.948 /
+        # 1.012, bs128 1.301 / 1.299 / 1.350; ImageNet RN50 12.81 / 12.91 (2 / 4)
+        self.fork_every = max(1, int(os.environ.get(
+            "DTR_FORK_EVERY", "4" if spec.dataset.startswith("cifar") else "2")))
         # same-shape weight gradients per grouped launch (_emit_wgrads; 1 = ungrouped).
         # Default 1, measured (CIFAR RN50 step, ms): bs16 0.958 ungrouped vs 0.987 / 0.978
         # / 0.983 grouping 2 / 8 stage-1 only / 8 all; bs128 1.298 vs 1.296-1.306.  The
@@ -199,6 +203,9 @@ class Engine:
         # 0.994 / 1.017 / 1.011, bs64 1.128 / 1.131 / 1.131 / 1.130, bs128 1.326 / 1.316 /
         # 1.314 / 1.303 (scripts/ab_tail.sh)
         self.tail_main = min(1.0, max(0.0, float(os.environ.get("DTR_TAIL_MAIN", "1"))))
+        # ...and the last reduces then run on the main stream behind one join
+        # (DTR_REDUCE_MAIN_TAIL=0: forked to the side stream like the earlier buckets)
+        self.reduce_main_tail = os.environ.get("DTR_REDUCE_MAIN_TAIL", "1") != "0"
         self.markers = os.environ.get("DTR_ROCTX", "0") != "0"
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
@@ -929,7 +936,7 @@ class Engine:
             if not all((bi, gi) in self._reduced for gi in range(len(self.reduce_groups[bi]))):
                 continue
             if self.reduce_buckets or force:
-                if self.fork_wgrad:
+                if self.fork_wgrad and not self._reduce_main:
                     # join: the main stream (and the bucket's all-reduce) waits for the side stream
                     ev = plan.new_event()
                     plan.use_stream(1)
@@ -983,7 +990,7 @@ class Engine:
             chunk += self.nat.wgrad_reduce_chunks(sp, K, taps, C)
         t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
         self._keep.append(t)
-        plan.use_stream(1 if self.fork_wgrad else 0)
+        plan.use_stream(1 if self.fork_wgrad and not self._reduce_main else 0)
         plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
         st = self.spec.stem
         sc = self.convs[st.name]
@@ -1118,6 +1125,7 @@ class Engine:
         # the dense wgrad below runs on the main stream (unless the head is fused)
         self._main_wgrad = self.fork_wgrad and not self._head_fused
         self._pending_bwd, self._bnb_src = None, None
+        self._reduce_main = False
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
         dpart = self.wg_part.data_ptr() + 4 * off
@@ -1212,6 +1220,17 @@ class Engine:
         if main_tail:   # the main stream's share of the tail; the reduces fork after it
             self._emit_wgrads(plan, main_tail)
             self._main_wgrad = True
+        if self._split_tail_on() and self.reduce_main_tail:
+            # the remaining reduces run on the main stream after ONE join of the side
+            # stream, instead of a fork to the side and a join back per bucket
+            self._flush_side(plan, force=False)   # (the queue is empty after the split)
+            ev = plan.new_event()
+            plan.use_stream(1)
+            plan.record(ev)
+            plan.use_stream(0)
+            plan.wait(ev)
+            self._main_wgrad = False
+            self._reduce_main = True
         self._flush_side(plan, force=True)
         self._flush_buckets(plan, force=True)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
