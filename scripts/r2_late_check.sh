@@ -15,12 +15,7 @@ import json
 for l in open('$out'):
     d=json.loads(l); c=d['config']
     print(c['model'], c['per_gpu_batch'], d['ms_per_step'], d['value'], c.get('peak_mem_gb'))"
-for v in 0 1; do
-  r=$(DTR_NARROW_NBUF1=$v timeout -k 10 150 python bench.py --model imagenet_resnet50 --steps 30 --warmup 5 2>/dev/null | grep metric) || exit 1
-  echo "imagenet narrow_nbuf1=$v $(echo $r | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
-  r=$(DTR_NARROW_NBUF1=$v timeout -k 10 150 python bench.py --steps 300 --warmup 30 2>/dev/null | grep metric) || exit 1
-  echo "cifar bs128 narrow_nbuf1=$v $(echo $r | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
-done
+scripts/ab_fork4.sh || exit 1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/prof_c_late -o run -- python3 bench.py --steps 20 --warmup 5 > gpurun_out/prof_c_late.log 2>&1 || exit 1
 timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/prof_in_late -o run -- python3 bench.py --model imagenet_resnet50 --steps 10 --warmup 3 > gpurun_out/prof_in_late.log 2>&1
