@@ -43,6 +43,12 @@ MODELS = {
     "imagenet_resnet50": ("imagenet", 50, 128, False, 0.93, "README.md:39-44 (8 P100, 8ps-8wk)"),
     "imagenet_resnet101": ("imagenet", 101, 256, False, None, None),
 }
+DATA = {
+    True: "synthetic: random uint8 32x32 CIFAR records, on-device pad-4/crop/flip/standardize "
+          "every step; random-init weights",
+    False: "synthetic: random uint8 224x224 crops, on-device flip/mean-subtract/bf16 pack "
+           "every step (imagenet_u8_pack); random-init weights",
+}
 METRIC = "steps/sec (global_batch=128 CIFAR-10 / 1024 ImageNet) ResNet-50 at 1/2/4/8 MI355X"
 
 
@@ -67,6 +73,9 @@ def parse(argv=None):
     ap.add_argument("--phase-steps", type=int, default=5,
                     help="extra steps after the timed region with per-phase HIP-event timing "
                          "(forward / backward / exposed all-reduce / optimizer); 0 = skip")
+    ap.add_argument("--step-timeout", type=float, default=300.0,
+                    help="watchdog: abort the communicator and exit 3 when no step completes for "
+                         "this many seconds (first step: 3x), or on a communicator async error")
     ap.add_argument("--roctx", action="store_true",
                     help="wrap each step's phases in roctx ranges (rocprofv3 --marker-trace); "
                          "adds host overhead, recorded in the JSON")
@@ -81,14 +90,19 @@ def _free_port() -> int:
 
 def spawn_ranks(n: int, argv: list[str]) -> int:
     """Run this script as n rank processes (torchrun's env contract) and relay rank
-    0's stdout.  The parent never imports torch, so it never touches the GPU."""
+    0's stdout.  The parent never imports torch, so it never touches the GPU.
+    Rank 0 writes into a temp file, not a pipe, so a chatty rank (NCCL_DEBUG=INFO)
+    can never block on a full pipe while the others wait in a collective."""
+    import tempfile
+
     port = _free_port()
     procs = []
+    out0 = tempfile.TemporaryFile(mode="w+")
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-        out = subprocess.PIPE if r == 0 else subprocess.DEVNULL
+        out = out0 if r == 0 else subprocess.DEVNULL
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
                                       env=env, stdout=out, text=True))
     rc = 0
@@ -117,9 +131,10 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                 p.kill()
                 p.wait()
         rc = 1
-    out = procs[0].stdout.read() if procs[0].stdout else ""
-    for line in out.splitlines():
+    out0.seek(0)
+    for line in out0.read().splitlines():
         print(line, flush=True)
+    out0.close()
     return rc or max(p.returncode or 0 for p in procs)
 
 
@@ -166,6 +181,7 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
 
     from distributed_tensorflow_resnet_amd.models.spec import build_spec
     from distributed_tensorflow_resnet_amd.parallel.dist import DistContext, local_device_index
+    from distributed_tensorflow_resnet_amd.parallel.watchdog import CommWatchdog
     from distributed_tensorflow_resnet_amd.train.engine import (Engine, cifar_lr_schedule,
                                                                 imagenet_lr_schedule)
 
@@ -177,10 +193,15 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
     sched = cifar_lr_schedule() if dataset.startswith("cifar") else imagenet_lr_schedule()
     wd = 2e-4 if dataset.startswith("cifar") else 1e-4
     use_graph = bool(args.graph) and not args.no_graph
+    # per-step input work for both datasets: CIFAR augments random uint8 records
+    # (pad/crop/flip/standardize), ImageNet flips / mean-subtracts / packs random
+    # uint8 224x224 crops into the stem's bf16 layout (imagenet_u8_pack)
+    input_mode = "cifar_u8" if dataset.startswith("cifar") else "imagenet_u8"
     eng = Engine(spec, per_rank, weight_decay=wd, lr_schedule=sched, device=device,
                  dist_ctx=ctx, global_batch=global_batch, bucket_mb=args.bucket_mb,
                  seed=0, data_seed=1234 + ctx.rank, use_graph=use_graph,
-                 allreduce_dtype=args.allreduce_dtype)
+                 allreduce_dtype=args.allreduce_dtype, input_mode=input_mode)
+    dog = CommWatchdog(eng.comm, args.step_timeout, 3 * args.step_timeout).start()
     eng.broadcast_parameters(0)
     eng.fill_synthetic(seed=ctx.rank)
 
@@ -189,16 +210,19 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
         done = eng.capture(warmup=min(2, max(args.warmup, 1)))
     for _ in range(max(args.warmup - done, 0)):
         eng.step()
+        dog.beat()
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.step()
+        dog.beat()
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    dog.beat()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     ctx.all_reduce_max(t)
     elapsed = float(t.item())
@@ -211,6 +235,7 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
             for k, v in eng.step_timed().items():
                 acc[k] = acc.get(k, 0.0) + v
         phases = {k: round(v / args.phase_steps, 4) for k, v in acc.items()}
+    dog.stop()
     extra = {"dtype": "bf16", "device": torch.cuda.get_device_name(device),
              "graph": use_graph, "wgrad_stream": eng.fork_wgrad, "comm": eng.comm_info(),
              "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
@@ -268,7 +293,8 @@ def main(argv=None) -> int:
             "scaling": "strong" if is_global else "weak",
             "vs_baseline": round(sps / baseline, 3) if baseline else None,
             "dtype": extra["dtype"],
-            "data": "synthetic (random uint8 images, on-device augmentation each step), random-init weights",
+            "data": DATA[dataset.startswith("cifar")] if args.device == "cuda" else
+                    "synthetic uint8 batch (CPU fp32 trainer), random-init weights",
             "config": {
                 "model": f"resnet{size}_v2_{dataset}",
                 "global_batch": global_batch,

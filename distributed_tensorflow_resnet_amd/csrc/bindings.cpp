@@ -924,7 +924,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_threaded", [](Plan& p, bool on) { p.threaded = on ? 1 : 0; })
       .def("elapsed_ms", &Plan::elapsed_ms)
       // in-place SUM all-reduce of `count` elements at `ptr` on the plan's current
-      // stream through the native RCCL communicator (dtype: 7 fp32, 9 bf16)
+      // stream through the native communicator (dtype: 7 fp32, 9 bf16; any transport)
       .def("all_reduce", [](Plan& p, std::shared_ptr<Comm> c, ptr_t ptr, long long count,
                             int dtype) {
         if (!c) throw std::invalid_argument("all_reduce: no communicator");
@@ -959,8 +959,9 @@ PYBIND11_MODULE(_C, m) {
         return v;
       });
 
-  // Native RCCL communicator (comm.h).  Construction is collective and blocks
-  // until every rank has joined, so the GIL is released.
+  // Native communicator (comm.h).  Construction is collective and blocks until
+  // every rank has joined, and a host-staged (shm) collective blocks its caller,
+  // so the GIL is released around both.
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
       .def(py::init([](py::bytes id, int world, int rank, int device) {
              std::string uid = id;
@@ -968,18 +969,41 @@ PYBIND11_MODULE(_C, m) {
              return std::make_shared<Comm>(uid, world, rank, device);
            }),
            py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"))
-      .def("all_reduce", [](const Comm& c, ptr_t p, long long n, int dtype, ptr_t s) {
+      .def_static("shm", [](const std::string& name, int world, int rank, int device,
+                            long long slot_bytes, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return std::shared_ptr<Comm>(Comm::shm(name, world, rank, device, (size_t)slot_bytes,
+                                                    timeout_s));
+           },
+           py::arg("name"), py::arg("world"), py::arg("rank"), py::arg("device"),
+           py::arg("slot_bytes") = 64ll << 20, py::arg("timeout_s") = 600.0)
+      .def_static("loopback", [](float factor) { return std::shared_ptr<Comm>(Comm::loopback(factor)); },
+                  py::arg("factor") = 2.0f)
+      .def("all_reduce", [](Comm& c, ptr_t p, long long n, int dtype, ptr_t s) {
+        py::gil_scoped_release nogil;
         c.all_reduce(P<void>(p), (size_t)n, dtype, S(s));
       })
-      .def("broadcast", [](const Comm& c, ptr_t p, long long n, int dtype, int root, ptr_t s) {
+      .def("broadcast", [](Comm& c, ptr_t p, long long n, int dtype, int root, ptr_t s) {
+        py::gil_scoped_release nogil;
         c.broadcast(P<void>(p), (size_t)n, dtype, root, S(s));
+      })
+      .def("host_all_reduce", [](Comm& c, ptr_t p, long long n, int dtype) {
+        py::gil_scoped_release nogil;
+        c.host_all_reduce(P<void>(p), (size_t)n, dtype);
+      })
+      .def("host_broadcast", [](Comm& c, ptr_t p, long long n, int dtype, int root) {
+        py::gil_scoped_release nogil;
+        c.host_broadcast(P<void>(p), (size_t)n, dtype, root);
       })
       .def("async_error", &Comm::async_error)
       .def("abort", &Comm::abort)
       .def_property_readonly("world", &Comm::world)
       .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("transport", &Comm::transport)
+      .def_property_readonly("library_path", &Comm::library_path)
       .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
-      .def_static("library", &Comm::library);
+      .def_static("library", &Comm::library)
+      .def_static("rccl_available", &Comm::rccl_available);
   m.attr("COMM_F32") = (int)COMM_F32;
   m.attr("COMM_BF16") = (int)COMM_BF16;
   m.attr("COMM_F64") = (int)COMM_F64;

@@ -6,6 +6,9 @@
 // launches on every stream, so that work a missing fork or join leaves unordered
 // really does overlap in a different order from run to run.  The clock read is
 // the only memory-side effect: no loads, no stores.
+#include <algorithm>
+
+#include "comm.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -20,6 +23,26 @@ void plan_delay(long long ticks, hipStream_t s) {
   if (ticks <= 0) return;
   hipLaunchKernelGGL(plan_delay_kernel, dim3(1), dim3(64), 0, s, ticks);
   DTR_CHECK_LAUNCH();
+}
+
+// Loopback communicator (comm.h): the diagnostics stand-in for an all-reduce,
+// buf *= factor in place.  A grid-stride loop; the factor of the tests (2) is
+// exact in fp32 and bf16, so any element the scale missed or saw twice differs.
+template <typename T>
+__global__ void __launch_bounds__(256) scale_inplace_kernel(T* p, size_t n, float f) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    p[i] = (T)((float)p[i] * f);
+}
+
+void comm_scale_inplace(void* buf, size_t count, int dtype, float factor, hipStream_t s) {
+  if (count == 0) return;
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, 2048);
+  if (dtype == 9)
+    hipLaunchKernelGGL(scale_inplace_kernel<bf16>, dim3(grid), dim3(256), 0, s,
+                       static_cast<bf16*>(buf), count, factor);
+  else
+    hipLaunchKernelGGL(scale_inplace_kernel<float>, dim3(grid), dim3(256), 0, s,
+                       static_cast<float*>(buf), count, factor);
 }
 
 }  // namespace dtr

@@ -11,11 +11,65 @@ MASTER_ADDR, MASTER_PORT) set by torchrun or parallel/launch.py.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
+import faulthandler
 import os
+import sys
+import threading
+import time
+import uuid
 
 import torch
 import torch.distributed as dist
+
+INIT_HANG_EXIT = 3   # same code as the step watchdog: the launcher restarts the job
+
+
+@contextlib.contextmanager
+def _deadline(seconds: float, what: str):
+    """End the process (exit 3) if the body has not returned within `seconds`:
+    a collective init that never completes (a rank that never joined) cannot be
+    aborted from Python, and a hung job is worse than a restartable one."""
+    def fire():
+        print(f"[dist] {what} did not complete within {seconds:.0f}s: exiting for restart",
+              file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        os._exit(INIT_HANG_EXIT)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    try:
+        yield
+    finally:
+        t.cancel()
+
+
+def _canary(nat, comm, world: int, device_index: int, timeout_s: float):
+    """One small all-reduce through a fresh communicator: None if every element
+    came back as 1 + 2 + ... + world, else the reason."""
+    try:
+        dev = torch.device("cuda", device_index)
+        x = torch.full((256,), float(comm.rank + 1), dtype=torch.float32, device=dev)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        comm.all_reduce(x.data_ptr(), x.numel(), nat.COMM_F32, s.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        t0 = time.monotonic()
+        while not ev.query():
+            if comm.async_error():
+                return f"canary: async error {comm.async_error()}"
+            if time.monotonic() - t0 > timeout_s:
+                comm.abort()
+                return f"canary all-reduce did not complete within {timeout_s:.0f}s"
+            time.sleep(0.001)
+        want = world * (world + 1) / 2
+        if not bool((x == want).all()):
+            return f"canary all-reduce returned {float(x[0])}, expected {want}"
+    except Exception as e:   # noqa: BLE001 - reported as the fallback reason
+        return f"canary raised: {e}"
+    return None
 
 
 def env_world() -> tuple[int, int, int]:
@@ -43,6 +97,8 @@ class DistContext:
         self.rank, self.world_size, self.local_rank = env_world()
         self.backend = backend
         self.device = device
+        self.timeout_s = float(timeout_s)
+        self.comm_fallback_reason = None
         self.initialized_here = False
         if self.world_size > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -61,35 +117,93 @@ class DistContext:
         elif dist.is_initialized():
             self.backend = dist.get_backend()
 
-    def native_comm(self, device_index: int, force: bool = False):
-        """The native RCCL communicator of this job (`_C.Comm`, csrc/comm.h) or None.
+    def comm_transport(self) -> str:
+        """Gradient-exchange transport of this job (env DTR_COMM_TRANSPORT):
+        ``auto`` (default) = ``rccl`` on the nccl backend, ``c10d`` otherwise;
+        ``rccl`` native RCCL communicator (plan ops on the comm stream);
+        ``shm`` native host-staged shared-memory rehearsal transport, the same
+        plan ops with several ranks folded onto one GPU (csrc/comm_shm.cpp);
+        ``c10d`` host-issued torch.distributed all-reduces between plan segments."""
+        t = os.environ.get("DTR_COMM_TRANSPORT", "auto")
+        if t not in ("auto", "rccl", "shm", "c10d"):
+            raise ValueError(f"DTR_COMM_TRANSPORT must be auto|rccl|shm|c10d, got {t!r}")
+        if t == "auto":
+            return "rccl" if self.backend == "nccl" else "c10d"
+        return t
 
-        Built when the job runs on RCCL ("nccl" backend) with more than one rank,
-        or when ``force`` (single-rank tests of the comm path).  Rank 0's
-        ncclUniqueId travels through the c10d TCP store, the same rendezvous the
-        process group used; each call makes a fresh communicator (the ranks must
-        call in the same order, as they build their engines in the same order).
-        DTR_NATIVE_COMM=0 keeps the gradient all-reduce on c10d instead."""
-        if os.environ.get("DTR_NATIVE_COMM", "1") == "0" and not force:
+    def _agree(self, ok: bool) -> bool:
+        """True iff every rank passed `ok` (a c10d MAX of the failure flags)."""
+        if not self.active:
+            return ok
+        dev = self.device if (self.backend == "nccl" and self.device is not None) else "cpu"
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item()) == 0
+
+    def native_comm(self, device_index: int, force: bool = False, transport: str | None = None):
+        """The native communicator of this job (`_C.Comm`, csrc/comm.h) or None
+        (then the engine issues c10d all-reduces from the host instead).
+
+        Built for world > 1 when the transport (``comm_transport``) is rccl or
+        shm, or when ``force`` (a single-rank RCCL communicator: tests of the comm
+        path).  Fail-safe and collective -- every rank takes the same decision:
+          1. preflight (the extension loads, RCCL's symbols resolve), agreed
+             over c10d;
+          2. rendezvous: rank 0's ncclUniqueId / shm segment name travels through
+             the c10d store; construction runs under a timer that ends the
+             process (exit 3, launcher restart) if the collective init hangs;
+          3. a canary all-reduce of (rank + 1) must return world(world+1)/2
+             within the timeout, agreed over c10d.
+        Any failure falls back to c10d on EVERY rank, with the reason in
+        ``self.comm_fallback_reason`` (bench.py JSON `comm.fallback_reason`)."""
+        self.comm_fallback_reason = None
+        kind = transport or ("rccl" if force and not self.active else self.comm_transport())
+        if kind == "c10d":
             return None
-        if not force and not (self.active and self.backend == "nccl"):
+        if not force and not self.active:
             return None
         from .. import native
 
         nat = native(required=True)
+        ok = kind != "rccl" or bool(nat.Comm.rccl_available())
+        if not self._agree(ok):
+            self.comm_fallback_reason = f"{kind} preflight failed on some rank"
+            return None
         self._comm_seq = getattr(self, "_comm_seq", 0) + 1
+        world, rank = (self.world_size, self.rank) if self.active else (1, 0)
+        key = f"dtr/comm_id/{self._comm_seq}"
+        if kind == "rccl":
+            ident = nat.Comm.unique_id() if rank == 0 else None
+        else:
+            ident = (f"/dtr-{os.getpid()}-{uuid.uuid4().hex[:16]}".encode()
+                     if rank == 0 else None)
         if self.active:
             store = dist.distributed_c10d._get_default_store()
-            key = f"dtr/rccl_uid/{self._comm_seq}"
-            if self.rank == 0:
-                uid = nat.Comm.unique_id()
-                store.set(key, uid)
+            if rank == 0:
+                store.set(key, ident)
             else:
-                uid = bytes(store.get(key))
-            world, rank = self.world_size, self.rank
-        else:
-            uid, world, rank = nat.Comm.unique_id(), 1, 0
-        return nat.Comm(uid, world, rank, device_index)
+                ident = bytes(store.get(key))
+        comm, err = None, None
+        with _deadline(self.timeout_s, f"{kind} communicator init"):
+            try:
+                if kind == "rccl":
+                    comm = nat.Comm(ident, world, rank, device_index)
+                else:
+                    comm = nat.Comm.shm(ident.decode(), world, rank, device_index,
+                                        timeout_s=self.timeout_s)
+            except Exception as e:   # noqa: BLE001 - reported as the fallback reason
+                err = f"{kind} init failed on rank {rank}: {e}"
+        if not self._agree(comm is not None):
+            self.comm_fallback_reason = err or f"{kind} init failed on another rank"
+            if comm is not None:
+                comm.abort()
+            return None
+        err = _canary(nat, comm, world, device_index, min(self.timeout_s, 120.0))
+        if not self._agree(err is None):
+            comm.abort()
+            self.comm_fallback_reason = err or f"{kind} canary failed on another rank"
+            return None
+        return comm
 
     @property
     def is_chief(self) -> bool:

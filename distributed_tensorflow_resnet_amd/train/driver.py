@@ -179,8 +179,11 @@ def main(argv=None, kind: str = "cifar") -> int:
                                                                  flags.fault_kill_rank))))
     if flags.profile_steps:
         hooks.append(H.ProfilerHook(flags.profile_steps))
-    if flags.step_watchdog_secs > 0:
-        hooks.append(H.StepWatchdogHook(flags.step_watchdog_secs))
+    # multi-rank jobs always watch the step and the communicator's async error
+    wd_secs = flags.step_watchdog_secs or (flags.comm_timeout_secs if world > 1 else 0.0)
+    if wd_secs > 0:
+        hooks.append(H.StepWatchdogHook(wd_secs, comm=getattr(getattr(backend, "engine", None),
+                                                              "comm", None)))
     sess = TrainingSession(backend, hooks, chief_hooks, checkpoint_dir=flags.train_dir or None,
                            is_chief=is_chief, rank=rank, feeder=feeder)
     t0 = time.time()

@@ -159,7 +159,7 @@ class Engine:
                  seed: int = 0,
                  input_mode: str = "auto", global_batch: int | None = None,
                  use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None,
-                 allreduce_dtype: str = "fp32", native_comm: bool | None = None):
+                 allreduce_dtype: str = "fp32", native_comm: bool | None = None, comm=None):
         self.nat = native(required=True)
         self.spec = spec
         self.N = batch_size
@@ -234,15 +234,22 @@ class Engine:
         self.scalars = torch.zeros(8, device=dev)  # loss_sum, correct, lr, l2
         self.side = torch.cuda.Stream(device=dev)   # weight-gradient stream
         self.comm_stream = torch.cuda.Stream(device=dev)   # RCCL all-reduces
-        # Native RCCL communicator: the bucket all-reduces are plan ops on the comm
-        # stream.  None: world 1 (nothing to reduce) or a gloo rehearsal (c10d
-        # all-reduces issued by the host between plan segments, _run_bwd).
-        # native_comm=True forces it on a single rank (tests of the comm path).
-        self.comm = None
+        # Native communicator (csrc/comm.h: RCCL, or the shm rehearsal transport):
+        # the bucket all-reduces are plan ops on the comm stream.  None: world 1
+        # (nothing to reduce), the c10d transport, or a fallback after a failed
+        # native init (c10d all-reduces issued by the host between plan segments,
+        # _run_bwd; the reason in comm_fallback_reason).  native_comm=True forces
+        # a single-rank RCCL communicator, `comm=` takes a prebuilt one (tests:
+        # _C.Comm.loopback(2), the doubling stand-in for an all-reduce).
+        self.comm = comm
+        self.comm_fallback_reason = None
         didx = dev.index if dev.index is not None else torch.cuda.current_device()
-        if self.dist is not None and (self.world > 1 or native_comm):
+        if comm is not None:
+            pass
+        elif self.dist is not None and (self.world > 1 or native_comm):
             if native_comm is not False:
                 self.comm = self.dist.native_comm(didx, force=bool(native_comm))
+                self.comm_fallback_reason = self.dist.comm_fallback_reason
         elif native_comm:
             from ..parallel.dist import DistContext
             self.comm = DistContext().native_comm(didx, force=True)
@@ -1403,12 +1410,16 @@ class Engine:
         """How the gradients are exchanged (bench.py JSON)."""
         nat = self.comm is not None
         per = 2 if self.grad_bf16 is not None else 4
-        return {"native_rccl": nat,
+        transport = self.comm.transport if nat else ("c10d" if self.bucket_sched else None)
+        return {"native_rccl": nat and transport == "rccl",
+                "native": nat,
+                "transport": transport,
+                "fallback_reason": self.comm_fallback_reason,
                 "buckets": len(self.buckets) if self.reduce_buckets else 0,
                 "allreduce_ops": self._n_allreduce if nat else len(self.bucket_sched),
                 "allreduce_bytes": (self._allreduce_bytes if nat else
                                     sum((hi - lo) * per for _, lo, hi in self.bucket_sched)),
-                "rccl_library": self.nat.Comm.library() if nat else None}
+                "rccl_library": self.comm.library_path if nat else None}
 
     def capture(self, warmup: int = 2):
         """Run `warmup` real steps on a side stream, then capture one step."""

@@ -14,12 +14,10 @@ Hooks only read device metrics when they are due (a read synchronises).
 """
 from __future__ import annotations
 
-import faulthandler
 import json
 import math
 import os
 import sys
-import threading
 import time
 
 
@@ -208,53 +206,45 @@ class NanGuardHook(Hook):
 
 
 class StepWatchdogHook(Hook):
-    """Failure detection for hung steps (SURVEY §5 failure-detection row): a daemon
-    thread aborts the process when no step has completed for `timeout_s` seconds
-    (a dead peer leaves the others blocked inside an RCCL collective; a faulting
-    kernel can leave the host blocked in a synchronisation).  It dumps every
-    thread's stack, then exits with code 3 so the launcher (parallel/launch.py
-    --max_restarts) restarts the job from the latest checkpoint.  The first step
-    gets `first_timeout_s` (plan build, kernel loading, rendezvous)."""
+    """Failure detection for hung steps and communicator errors (SURVEY §5
+    failure-detection row), parallel/watchdog.py's CommWatchdog driven by the
+    session: a daemon thread polls the native communicator's async error
+    (ncclCommGetAsyncError, or the shm transport's dead-peer state) and the time
+    since the last completed step (a dead peer leaves the others blocked inside a
+    collective; a faulting kernel can leave the host blocked in a
+    synchronisation).  On either it dumps every thread's stack, aborts the
+    communicator (ncclCommAbort) and exits with code 3 so the launcher
+    (parallel/launch.py --max_restarts) restarts the job from the latest
+    checkpoint.  The first step gets `first_timeout_s` (plan build, kernel
+    loading, rendezvous)."""
 
     EXIT_CODE = 3
 
     def __init__(self, timeout_s: float, first_timeout_s: float | None = None,
-                 _exit=os._exit, poll_s: float | None = None):
-        self.timeout_s = float(timeout_s)
-        self.first_timeout_s = float(first_timeout_s or max(600.0, 4 * timeout_s))
-        self._exit = _exit
-        self._poll = poll_s or min(5.0, max(self.timeout_s / 10, 0.01))
-        self._last = time.monotonic()
-        self._steps = 0
-        self._stop = threading.Event()
-        self._thread = None
-        self.fired = False
+                 _exit=os._exit, poll_s: float | None = None, comm=None):
+        from ..parallel.watchdog import CommWatchdog
+
+        self.wd = CommWatchdog(comm, timeout_s, first_timeout_s,
+                               poll_s or min(5.0, max(float(timeout_s) / 10, 0.01)),
+                               self.EXIT_CODE, _exit, log)
+        self.timeout_s = self.wd.timeout_s
+        self.first_timeout_s = self.wd.first_timeout_s
+
+    @property
+    def fired(self) -> bool:
+        return self.wd.fired is not None
 
     def begin(self, session):
-        self._last = time.monotonic()
-        self._thread = threading.Thread(target=self._watch, name="dtr-step-watchdog",
-                                        daemon=True)
-        self._thread.start()
+        if self.wd.comm is None and session is not None:
+            eng = getattr(getattr(session, "backend", None), "engine", None)
+            self.wd.comm = getattr(eng, "comm", None)
+        self.wd.start()
 
     def after_run(self, session, step):
-        self._steps += 1
-        self._last = time.monotonic()
+        self.wd.beat()
 
     def end(self, session):
-        self._stop.set()
-
-    def _watch(self):
-        while not self._stop.wait(self._poll):
-            limit = self.timeout_s if self._steps else self.first_timeout_s
-            idle = time.monotonic() - self._last
-            if idle > limit:
-                self.fired = True
-                log(f"[watchdog] no training step completed for {idle:.0f}s "
-                    f"(limit {limit:.0f}s): aborting for restart")
-                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
-                sys.stderr.flush()
-                self._exit(self.EXIT_CODE)
-                return
+        self.wd.stop()
 
 
 class FaultInjectionHook(Hook):

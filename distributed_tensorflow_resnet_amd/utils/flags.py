@@ -153,10 +153,13 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_argument("--fault_kill_rank", type=int, default=0)
     p.add_argument("--step_watchdog_secs", type=float, default=0.0,
                    help="If > 0, abort (exit 3, for the launcher to restart from the latest "
-                        "checkpoint) when no step completes for this many seconds.")
+                        "checkpoint) when no step completes for this many seconds.  Multi-rank "
+                        "jobs always run the watchdog (limit --comm_timeout_secs when this is 0), "
+                        "which also polls the native communicator's async error.")
     p.add_argument("--comm_timeout_secs", type=float, default=600.0,
-                   help="Collective timeout of the process group (RCCL watchdog aborts the "
-                        "communicator after it).")
+                   help="Collective timeout: the process group's, the native communicator's "
+                        "init / shm waits, and the multi-rank step watchdog's default limit "
+                        "(on expiry: ncclCommAbort, exit 3).")
     p.add_argument("--lr_schedule_scale", type=float, default=1.0,
                    help="Multiply the LR schedule's step boundaries (and warm-up) by this "
                         "factor: compressed schedules for short runs (convergence tests).")

@@ -72,7 +72,12 @@ def perturbation_check(make_engine: Callable[[], object], steps: int = 3, trials
             "prob": prob, "max_us": max_us}
 
 
-def _make_factory(model: str, batch: int, device):
+def _make_factory(model: str, batch: int, device, loopback: bool = False,
+                  allreduce_dtype: str = "fp32", bucket_mb: float = 0.0):
+    """Engine factory; ``loopback``: with the comm stream active -- every bucket
+    all-reduced (x2, csrc/comm.h loopback transport) on stream 2 between its
+    side-stream producers and the optimizer, bf16 casts included if asked."""
+    from .. import native
     from ..models.spec import cifar_spec, imagenet_spec
     from ..train.engine import Engine, cifar_lr_schedule
 
@@ -84,8 +89,12 @@ def _make_factory(model: str, batch: int, device):
         raise SystemExit(f"unknown model {model!r}")
 
     def make():
+        kw = {}
+        if loopback:
+            kw = dict(comm=native().Comm.loopback(2.0), allreduce_dtype=allreduce_dtype,
+                      bucket_mb=bucket_mb or None)
         eng = Engine(spec, batch, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
-                     device=device, seed=7, data_seed=99, use_graph=False)
+                     device=device, seed=7, data_seed=99, use_graph=False, **kw)
         eng.fill_synthetic(3)
         return eng
     return make
@@ -101,10 +110,16 @@ def main(argv=None):
     ap.add_argument("--prob", type=float, default=0.3)
     ap.add_argument("--max_us", type=float, default=20.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--loopback", action="store_true",
+                    help="comm stream active: loopback (x2) all-reduce of every bucket")
+    ap.add_argument("--allreduce_dtype", default="fp32", choices=("fp32", "bf16"))
+    ap.add_argument("--bucket_mb", type=float, default=0.0)
     a = ap.parse_args(argv)
-    res = perturbation_check(_make_factory(a.model, a.batch, torch.device("cuda", 0)), a.steps,
-                             a.trials, a.prob, a.max_us, a.seed)
-    print(json.dumps(dict(res, model=a.model, batch=a.batch)))
+    res = perturbation_check(_make_factory(a.model, a.batch, torch.device("cuda", 0), a.loopback,
+                                           a.allreduce_dtype, a.bucket_mb),
+                             a.steps, a.trials, a.prob, a.max_us, a.seed)
+    print(json.dumps(dict(res, model=a.model, batch=a.batch, loopback=a.loopback,
+                          allreduce_dtype=a.allreduce_dtype)))
     return 0 if res["ok"] else 1
 
 

@@ -3,13 +3,18 @@
 
 Every rank trains the same random-init model on its own synthetic shard.  After
 one step the all-reduced gradient of the DP engine must equal, bit for bit, the
-sum over ranks of a second, non-distributed engine's local gradient on the same
-shard (2-rank fp32 sums are order-free), and after further steps every rank
-must hold identical fp32 master weights and momentum (BN moving statistics stay
-per-replica, as with Horovod).
+rank-order sum of a second, non-distributed engine's local gradients on the same
+shards (fp32; with a bf16 exchange: the rank-order fp32 sum of the bf16-rounded
+local gradients, rounded to bf16 once -- what the shm transport computes; the
+c10d/gloo bf16 path is checked to 1e-2 relative), and after further steps every
+rank must hold identical fp32 master weights and momentum (BN moving statistics
+stay per-replica, as with Horovod).
 
     DTR_DIST_BACKEND=gloo torchrun --nproc-per-node 2 --master-addr 127.0.0.1 \
-        scripts/dp_check.py            # 2 ranks rehearsed on one GPU
+        scripts/dp_check.py            # 2 ranks rehearsed on one GPU, c10d transport
+    DTR_DIST_BACKEND=gloo DTR_COMM_TRANSPORT=shm torchrun ... scripts/dp_check.py
+                                       # the native plan-op path (comm stream, issue
+                                       # threads, bf16 casts) over the shm transport
 """
 import os
 import sys
@@ -44,13 +49,31 @@ def main() -> int:
     eng.step()
     ref.step()
     torch.cuda.synchronize()
-    g = ref.grad.clone()
-    ctx.all_reduce_sum(g)
-    if ar_dtype == "bf16":   # bf16 exchange: equal up to bf16 rounding of the summands
-        grad_ok = bool(((g - eng.grad).norm() / g.norm()) < 1e-2)
+    info = eng.comm_info()
+    if ctx.backend == "gloo":
+        local = ref.grad.cpu()
+        parts = [torch.empty_like(local) for _ in range(world)]
+        torch.distributed.all_gather(parts, local)
+    else:   # nccl: gather through the device
+        dparts = [torch.empty_like(ref.grad) for _ in range(world)]
+        torch.distributed.all_gather(dparts, ref.grad)
+        parts = [p.cpu() for p in dparts]
+    got = eng.grad.cpu()
+    if ar_dtype == "bf16":
+        acc = parts[0].to(torch.bfloat16).float()
+        for p in parts[1:]:
+            acc = acc + p.to(torch.bfloat16).float()
+        want = acc.to(torch.bfloat16).float()
+        if info["native"]:   # exact: the native transports' rank-order bf16 sum
+            grad_ok = torch.equal(want, got)
+        else:                # c10d: the backend's own bf16 summation
+            grad_ok = bool(((want - got).norm() / want.norm()) < 1e-2)
     else:
-        grad_ok = torch.equal(g, eng.grad)
-    maxdiff = float((g - eng.grad).abs().max())
+        want = parts[0].clone()
+        for p in parts[1:]:
+            want = want + p
+        grad_ok = torch.equal(want, got)
+    maxdiff = float((want - got).abs().max())
     for _ in range(3):
         eng.step()
     torch.cuda.synchronize()
@@ -62,7 +85,9 @@ def main() -> int:
     ctx.all_reduce_sum(flags)
     m = eng.metrics()
     if ctx.is_chief:
-        print(f"dp_check world={world} buckets={len(eng.bucket_sched)} grad_equal_ranks_failing="
+        print(f"dp_check world={world} transport={info['transport']} "
+              f"native={info['native']} allreduce_ops={info['allreduce_ops']} "
+              f"fallback={info['fallback_reason']} grad_equal_ranks_failing="
               f"{int(flags[0])} (max|diff|={maxdiff:.3g}) replicas_diverged={int(flags[1])} "
               f"loss={m['cross_entropy']:.4f} step={m['global_step']}", flush=True)
         ok = int(flags.sum()) == 0

@@ -1,12 +1,16 @@
-"""The native RCCL communicator (csrc/comm.h) inside the training plan.
+"""The native communicator (csrc/comm.h) inside the training plan, one process.
 
 RCCL refuses two ranks on one device, so on the one-GPU box the comm path runs
-as a single-rank communicator (`native_comm=True`): the plan carries the same
-comm-stream forks, bucket all-reduces, bf16 casts and final join as on 8 GPUs,
-and a one-rank SUM all-reduce is the identity -- so the step must match an
-engine without communicator bit for bit (fp32) or up to the bf16 rounding of
-the exchanged buckets (bf16).  Multi-rank RCCL runs in the driver's 8-GPU
-scaling bench; the multi-rank logic is rehearsed over gloo in test_dp_gpu.py."""
+here as (a) a single-rank RCCL communicator (`native_comm=True`): the plan
+carries the same comm-stream forks, bucket all-reduces, bf16 casts and final
+join as on 8 GPUs, and a one-rank SUM all-reduce is the identity -- the step
+must match an engine without communicator bit for bit (fp32) or up to the bf16
+rounding of the exchanged buckets (bf16); and (b) the loopback transport, a
+stand-in all-reduce that doubles each bucket in place on the comm stream: a
+bucket reduced before its last (side-stream) gradient writer finished, or a
+writer landing on an already-reduced range, leaves an element that is not
+exactly 2x -- checked under the race check's schedule jitter too.  The world > 1
+plan path (shm transport, two processes on this GPU) is in test_dp_gpu.py."""
 import json
 import os
 import subprocess
@@ -100,3 +104,82 @@ def test_bench_self_spawn_two_gloo_ranks(gpu):
     assert out["n_gpus"] == 2 and out["pg_world_size"] == 2 and out["dist_backend"] == "gloo"
     assert out["config"]["per_gpu_batch"] == 64 and out["config"]["comm"]["buckets"] >= 1
     assert out["phase_ms"]["allreduce_exposed"] >= 0.0
+
+
+def _loopback_engines(gpu, dtype, seed_eng=3):
+    import distributed_tensorflow_resnet_amd as dtr
+    from distributed_tensorflow_resnet_amd.models.spec import build_spec
+    from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule
+
+    nat = dtr.native()
+    spec = build_spec("cifar10", 14)
+    common = dict(weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu, seed=seed_eng,
+                  data_seed=11)
+    ref = Engine(spec, 16, **common)
+    eng = Engine(spec, 16, comm=nat.Comm.loopback(2.0), bucket_mb=0.05, allreduce_dtype=dtype,
+                 **common)
+    for e in (ref, eng):
+        e.fill_synthetic(5)
+    return ref, eng
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_loopback_doubling_standin_orders_every_bucket(gpu, dtype):
+    """grad == 2 x the no-comm engine's grad, bitwise, plain and under jitter."""
+    for trial in range(4):
+        ref, eng = _loopback_engines(gpu, dtype)
+        info = eng.comm_info()
+        assert info["transport"] == "loopback" and info["allreduce_ops"] >= 4, info
+        if trial:   # schedule perturbation: random delays in front of launches, every stream
+            eng.plan.set_perturb(2, 1000 + trial, 0.35, 25.0)
+        ref.step()
+        eng.step()
+        torch.cuda.synchronize()
+        base = ref.grad if dtype == "fp32" else ref.grad.to(torch.bfloat16).float()
+        bad = (eng.grad != 2 * base).nonzero()
+        assert bad.numel() == 0, (trial, f"{bad.numel()} elements not exactly doubled, first at "
+                                  f"{bad[:4].flatten().tolist()}")
+
+
+@pytest.mark.gpu
+def test_racecheck_with_comm_stream_active(gpu):
+    """utils/racecheck with the comm stream in the plan (bf16 exchange: casts that
+    read the gradients, an all-reduce, casts back): perturbed == serialized."""
+    from distributed_tensorflow_resnet_amd.utils.racecheck import _make_factory, perturbation_check
+
+    res = perturbation_check(_make_factory("cifar_resnet14", 16, gpu, loopback=True,
+                                           allreduce_dtype="bf16", bucket_mb=0.05),
+                             steps=3, trials=3, prob=0.3, max_us=20.0, seed=5)
+    assert res["ok"], res
+
+
+@pytest.mark.gpu
+def test_comm_transports_and_host_errors(gpu):
+    import distributed_tensorflow_resnet_amd as dtr
+
+    nat = dtr.native()
+    assert nat.Comm.rccl_available()
+    lb = nat.Comm.loopback(2.0)
+    assert lb.transport == "loopback" and lb.world == 1
+    x = torch.arange(1000, dtype=torch.float32, device=gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    lb.all_reduce(x.data_ptr(), x.numel(), nat.COMM_F32, st)
+    torch.cuda.synchronize()
+    assert torch.equal(x, 2 * torch.arange(1000, dtype=torch.float32, device=gpu))
+    # a one-rank shm communicator on the device: stream-ordered D2H / sum / H2D
+    import uuid
+
+    sh = nat.Comm.shm(f"/dtr-t-{uuid.uuid4().hex[:10]}", 1, 0, 0, slot_bytes=4096, timeout_s=10)
+    y = torch.randn(5000, device=gpu)
+    y0 = y.clone()
+    s2 = torch.cuda.Stream()
+    s2.wait_stream(torch.cuda.current_stream())
+    sh.all_reduce(y.data_ptr(), y.numel(), nat.COMM_F32, s2.cuda_stream)   # 5 chunks
+    sh.broadcast(y.data_ptr(), y.numel(), nat.COMM_F32, 0, s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0) and sh.async_error() == 0
+    sh.abort()
+    assert sh.async_error() == 6
+    with pytest.raises(RuntimeError):
+        sh.all_reduce(y.data_ptr(), y.numel(), nat.COMM_F32, s2.cuda_stream)

@@ -1,11 +1,17 @@
 """Multi-rank data parallelism of the GPU engine, rehearsed on the one-GPU box.
 
 RCCL refuses two ranks on one device, so these runs use DTR_DIST_BACKEND=gloo
-(CUDA tensors, host-staged) with both ranks folded onto cuda:0.  What they pin
-is the engine's DP logic: bucket cut points, all-reduce placement relative to
-the side-stream weight gradients, broadcast-on-init, metric reduction, and the
-bench.py multi-rank contract.  The RCCL/xGMI path itself runs in the driver's
-8-GPU scaling bench."""
+with both ranks folded onto cuda:0, over two gradient transports:
+  * c10d (default for gloo): host-issued all-reduces between plan segments;
+  * shm (DTR_COMM_TRANSPORT=shm): the NATIVE world > 1 path -- bucket
+    all-reduces as plan ops on the comm stream issued by its own host thread,
+    event fork/join against the compute streams, bf16 casts, native
+    broadcast-on-init, the init canary -- over the host-staged shared-memory
+    transport that sits behind the same Comm interface as RCCL (csrc/comm_shm.cpp).
+What they pin: gradients equal the exact rank-order sum of the local ones,
+replicas stay identical, the bench.py multi-rank contract, and failure handling
+(a killed peer makes the survivor exit non-zero fast; the launcher restarts the
+job from the checkpoint).  RCCL/xGMI itself runs in the driver's 8-GPU bench."""
 import json
 import os
 import subprocess
@@ -14,6 +20,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+SHM = {"DTR_COMM_TRANSPORT": "shm"}
 
 
 def _torchrun(args, port, timeout=600, extra_env=None):
@@ -59,3 +68,92 @@ def test_bench_two_ranks_contract(gpu):
     assert out["n_gpus"] == 2 and out["steps"] == 5 and out["config"]["global_batch"] == 128
     assert out["config"]["per_gpu_batch"] == 64 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,port", [("fp32", 29721), ("bf16", 29722)])
+def test_native_plan_path_two_ranks_shm(gpu, dtype, port):
+    r = _torchrun(["scripts/dp_check.py"], port,
+                  extra_env=dict(SHM, DP_CHECK_ALLREDUCE=dtype, DP_CHECK_BUCKET_MB="0.1"))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "DP_CHECK_OK" in r.stdout, r.stdout[-3000:]
+    assert "transport=shm native=True" in r.stdout and "fallback=None" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_bench_self_spawn_two_ranks_native_shm(gpu):
+    """`bench.py --gpus 2` (self-spawned ranks) over the native plan path."""
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **SHM)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "3",
+                        "--model", "cifar_resnet20"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    c = out["config"]["comm"]
+    assert c["native"] and c["transport"] == "shm" and c["fallback_reason"] is None, c
+    assert c["allreduce_ops"] >= 2 and c["buckets"] == c["allreduce_ops"], c
+    assert out["n_gpus"] == 2 and out["pg_world_size"] == 2
+    assert out["phase_ms"]["allreduce_exposed"] >= 0.0
+
+
+def _spawn_ranks(args, port, extra_env):
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **extra_env)
+        procs.append(subprocess.Popen([sys.executable] + args, cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    return procs
+
+
+@pytest.mark.gpu
+def test_killed_peer_makes_survivor_exit_nonzero_fast(gpu, tmp_path):
+    """Rank 1 dies at step 3 (fault injection); rank 0, with no launcher to stop
+    it, must notice inside its next gradient all-reduce and exit non-zero well
+    before the 120 s collective timeout."""
+    import time
+
+    args = ["resnet_cifar_main.py", "--device", "gpu", "--resnet_size", "8", "--batch_size", "8",
+            "--synthetic", "--train_steps", "50", "--variable_update", "horovod",
+            "--log_every", "1000", "--comm_timeout_secs", "120", "--fault_kill_step", "3",
+            "--fault_kill_rank", "1"]
+    t0 = time.time()
+    procs = _spawn_ranks(args, 29731, SHM)
+    try:
+        out1, _ = procs[1].communicate(timeout=240)
+        t1 = time.time()
+        out0, _ = procs[0].communicate(timeout=200)
+        t_exit = time.time() - t1
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert procs[1].returncode == 17, out1[-2000:]
+    assert procs[0].returncode != 0, out0[-3000:]
+    assert t_exit < 60, f"survivor exited {t_exit:.0f}s after the peer died"
+    assert "is gone" in out0 or "aborted by rank" in out0, out0[-3000:]
+    assert time.time() - t0 < 400
+
+
+@pytest.mark.gpu
+def test_launcher_restarts_native_job_from_checkpoint(gpu, tmp_path):
+    """2 ranks on the native shm path: rank 1 killed at step 3, the launcher
+    restarts the job, the ranks resume from the step-2 checkpoint and finish."""
+    import distributed_tensorflow_resnet_amd.utils.tensor_bundle as tb
+
+    td = str(tmp_path / "train")
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **SHM)
+    r = subprocess.run([sys.executable, "-m", "distributed_tensorflow_resnet_amd.parallel.launch",
+                        "--nproc", "2", "--master_port", "29741", "--max_restarts", "1",
+                        "resnet_cifar_main.py", "--device", "gpu", "--resnet_size", "8",
+                        "--batch_size", "8", "--synthetic", "--train_steps", "6",
+                        "--train_dir", td, "--save_checkpoint_steps", "2",
+                        "--variable_update", "horovod", "--log_every", "1",
+                        "--comm_timeout_secs", "120",
+                        "--fault_kill_step", "3", "--fault_kill_rank", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "restarting job" in r.stdout and "Restoring parameters from" in r.stdout, r.stdout[-3000:]
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-6")
