@@ -158,10 +158,9 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
       const int C = c.K;   // A channels of the dgrad
       if (g.abwd.acc == nullptr && (g.abwd.cnt < 0 || g.abwd.cnt > pfin_cap(C)))   // 0: coef precomputed
         throw std::invalid_argument("abwd: partial count exceeds the prologue bound");
-    } else if (!conv_gemm_abwd_covers(g)) {
-      throw std::invalid_argument("abwd: this dgrad is covered neither by the direct 3x3 kernel "
-                                  "nor by the implicit-GEMM ABWD loop (needs K % 64 == 0, "
-                                  "K <= 512, no add, precomputed coefficients)");
+    } else {
+      throw std::invalid_argument("abwd: the fused BN-backward prologue needs the direct 3x3 "
+                                  "dgrad (CIFAR shapes)");
     }
   }
   if (g.pfin.cnt > 0 && g.pfin.acc == nullptr) {
@@ -199,46 +198,6 @@ static Launch mk_conv_wgrad(ptr_t dy, ptr_t x, ptr_t pre_scale, ptr_t pre_shift,
   if (w.g.C % 8 || w.g.K % 16) throw std::invalid_argument("wgrad: C%8 and K%16 required");
   if (px_per_split % 64) throw std::invalid_argument("wgrad: px_per_split % 64");
   return [w](hipStream_t s) { conv_wgrad(w, s); };
-}
-
-// Same-shape weight gradients of several layers: one grouped direct launch when the
-// direct kernel covers the shape, else one conv_wgrad per member.
-static Launch mk_conv_wgrad_group(std::vector<ptr_t> dy, std::vector<ptr_t> x,
-                                  std::vector<ptr_t> pre_scale, std::vector<ptr_t> pre_shift,
-                                  std::vector<ptr_t> part, std::vector<int> geom, int splits,
-                                  int px_per_split) {
-  const size_t n = dy.size();
-  if (n < 1 || n > (size_t)WGRAD_GROUP_MAX || x.size() != n || pre_scale.size() != n ||
-      pre_shift.size() != n || part.size() != n)
-    throw std::invalid_argument("conv_wgrad_group: 1..8 members, equal-length operand lists");
-  std::vector<WgradArgs> ws;
-  WgradGroup grp{};
-  grp.n = (int)n;
-  for (size_t i = 0; i < n; ++i) {
-    WgradArgs w{};
-    w.dy = P<const bf16>(dy[i]);
-    w.x = P<const bf16>(x[i]);
-    w.pre_scale = P<const float>(pre_scale[i]);
-    w.pre_shift = P<const float>(pre_shift[i]);
-    w.part = P<float>(part[i]);
-    w.g = geom_from(geom);
-    w.splits = splits;
-    w.px_per_split = px_per_split;
-    if (w.g.C % 8 || w.g.K % 16) throw std::invalid_argument("wgrad: C%8 and K%16 required");
-    if (px_per_split % 64) throw std::invalid_argument("wgrad: px_per_split % 64");
-    if ((pre_scale[i] != 0) != (pre_scale[0] != 0))
-      throw std::invalid_argument("conv_wgrad_group: members must all (or none) fuse BN+ReLU");
-    grp.dy[i] = w.dy;
-    grp.x[i] = w.x;
-    grp.scale[i] = w.pre_scale;
-    grp.shift[i] = w.pre_shift;
-    grp.part[i] = w.part;
-    ws.push_back(w);
-  }
-  return [ws, grp](hipStream_t s) {
-    if (ws.size() > 1 && conv_wgrad_direct_group(ws[0], grp, s)) return;
-    for (const auto& w : ws) conv_wgrad(w, s);
-  };
 }
 
 static Launch mk_wgrad_reduce(ptr_t part, ptr_t grad, int splits, int K, int K_valid, int taps,
@@ -970,13 +929,14 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"))
       .def_static("shm", [](const std::string& name, int world, int rank, int device,
-                            long long slot_bytes, double timeout_s) {
+                            long long slot_bytes, double timeout_s, double init_timeout_s) {
              py::gil_scoped_release nogil;
              return std::shared_ptr<Comm>(Comm::shm(name, world, rank, device, (size_t)slot_bytes,
-                                                    timeout_s));
+                                                    timeout_s, init_timeout_s));
            },
            py::arg("name"), py::arg("world"), py::arg("rank"), py::arg("device"),
-           py::arg("slot_bytes") = 64ll << 20, py::arg("timeout_s") = 600.0)
+           py::arg("slot_bytes") = 64ll << 20, py::arg("timeout_s") = 600.0,
+           py::arg("init_timeout_s") = 0.0)
       .def_static("loopback", [](float factor) { return std::shared_ptr<Comm>(Comm::loopback(factor)); },
                   py::arg("factor") = 2.0f)
       .def("all_reduce", [](Comm& c, ptr_t p, long long n, int dtype, ptr_t s) {
@@ -1011,7 +971,6 @@ PYBIND11_MODULE(_C, m) {
 
   def_op(m, plan, "conv_gemm", mk_conv_gemm);
   def_op(m, plan, "conv_wgrad", mk_conv_wgrad);
-  def_op(m, plan, "conv_wgrad_group", mk_conv_wgrad_group);
   def_op(m, plan, "wgrad_reduce", mk_wgrad_reduce);
   def_op(m, plan, "wgrad_reduce_grouped", mk_wgrad_reduce_grouped);
   def_op(m, plan, "bn_finalize", mk_bn_finalize);
@@ -1063,30 +1022,29 @@ PYBIND11_MODULE(_C, m) {
   }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
   m.def("set_direct_probe", [](ptr_t p) { set_direct_probe(P<long long>(p)); },
         "diagnostics: direct-conv workgroups write 4 wall-clock stamps each to p (0 = off)");
-  m.def("conv_gemm_abwd_covers", [](std::vector<int> geom, bool has_add) {
-    GemmArgs g{};
-    g.g = geom_from(geom);
-    g.M = g.g.N * g.g.H * g.g.W;
-    g.Ncol = g.g.C;
-    g.Kdim = g.g.kh * g.g.kw * g.g.K;
-    // opt-in (DTR_GEMM_ABWD=1): measured 3x slower per dgrad on ImageNet RN50 (the
-    // per-element BN-backward VALU work is repeated per column tile and per tap and
-    // outweighs the MFMAs it feeds: 13.3 -> 17.8 ms/step), so the step keeps the
-    // separate bandwidth-bound bn_bwd_apply (profiles/bn_bwd_apply_bandwidth.md)
-    const char* e = std::getenv("DTR_GEMM_ABWD");
-    if (e == nullptr || e[0] != '1') return false;
-    return !has_add && conv_gemm_abwd_covers(g);
-  }, "whether the implicit-GEMM dgrad of geom can apply a pending BN backward itself");
   m.def("set_wgrad_direct", &set_wgrad_direct,
-        "enable/disable the direct 3x3 small-C wgrad kernel (default: on unless "
-        "DTR_DIRECT_WGRAD=0); changes wgrad_pick_splits, so set it before planning");
+        "enable/disable the direct 3x3 small-C wgrad kernel (tune direct_wgrad); changes "
+        "wgrad_pick_splits, so set it before planning");
   m.def("set_conv_direct", &set_conv_direct,
-        "enable/disable the direct 3x3 small-C conv kernel (default: on unless DTR_DIRECT_CONV=0)");
-  m.def("set_conv_wide_tile", &set_conv_wide_tile,
-        "bit 0: forward, bit 1: dgrad -- 128x64 tiles for > 64 output columns (DTR_WIDE_128x64)");
+        "enable/disable the direct 3x3 small-C conv kernel (tune direct_conv)");
   m.def("set_conv_pipeline", &set_conv_pipeline,
-        "enable/disable the 2-deep pipelined implicit-GEMM loop for C % 64 == 0 "
-        "(default: on unless DTR_CONV_PIPE=0)");
+        "enable/disable the 2-deep pipelined implicit-GEMM / wgrad loops (tune conv_pipe)");
+  m.def("tune_table", []() {
+    py::list out;
+    const TuneEntry* t = tune_table();
+    for (int i = 0; i < T_COUNT; ++i)
+      out.append(py::make_tuple(t[i].key, t[i].dflt, t[i].doc, tune((TuneId)i)));
+    return out;
+  }, "(key, default, doc, current value) of every native tuning entry (csrc/tune.h)");
+  m.def("tune_set", [](const std::string& key, long v) {
+    const TuneEntry* t = tune_table();
+    for (int i = 0; i < T_COUNT; ++i)
+      if (key == t[i].key) {
+        tune_set((TuneId)i, v);
+        return;
+      }
+    throw std::invalid_argument("unknown native tuning key " + key);
+  }, py::arg("key"), py::arg("value"), "set a native tuning entry (tests, A/B scripts)");
   m.def("set_fin_version", &set_fin_version,
         "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
   m.def("bn_acc_rep", []() { return BN_ACC_REP; }, "fp64 accumulator replicas per BatchNorm");
@@ -1096,9 +1054,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("l2_workspace_floats", &l2_workspace_floats);
   m.def("softmax_xent_ws_floats", &softmax_xent_ws_floats);
   m.def("set_conv_parity", &set_conv_parity, py::arg("enabled"),
-        "stride-2 dgrads as 4 output-parity classes (DTR_PARITY_DGRAD)");
+        "stride-2 dgrads as 4 output-parity classes (tune parity_dgrad)");
   m.def("set_conv_splitk", &set_conv_splitk, py::arg("max_slices"),
-        "max split-K slices of under-filled implicit-GEMM grids (1 = off; DTR_SPLITK)");
+        "max split-K slices of under-filled implicit-GEMM grids (1 = off; tune splitk)");
   m.def("wgrad_reduce_chunks", &wgrad_reduce_chunks, py::arg("splits"), py::arg("K"),
         py::arg("taps"), py::arg("C"),
         "work chunks of one conv's slabs in wgrad_reduce_grouped (its desc's chunk0 stride)");

@@ -163,18 +163,10 @@ bn_bwd_finalize_chan_kernel(const float* __restrict__ part, int tiles, int M, in
 
 // Variant choice (measured, scripts/fin_bench.py): the per-channel one-round
 // kernels win once there are many partials per channel; the LDS-tree kernels
-// below win for few partials or many channels.  DTR_FIN_V=0/2 forces one.
-static int g_fin_version = -1;
-static int fin_version() {
-  if (g_fin_version < 0) {
-    const char* e = std::getenv("DTR_FIN_V");
-    g_fin_version = e ? std::atoi(e) : 1;
-  }
-  return g_fin_version;
-}
-void set_fin_version(int v) { g_fin_version = v; }
+// below win for few partials or many channels.  tune fin_v = 0 / 2 forces one.
+void set_fin_version(int v) { tune_set(T_FIN_V, v); }
 static bool fin_use_v2(int tiles, int C, bool bwd) {
-  const int v = fin_version();
+  const int v = (int)tune(T_FIN_V);
   if (v != 1) return v == 2;
   return C <= 512 && tiles >= (bwd ? 256 : 1024);
 }
@@ -679,14 +671,10 @@ static bool bwd_fin_small(int M, int C) {
   return C <= BWD_ACC_FIN_MAXC && ((long)M * C / 8 + 511) / 512 <= 1024;
 }
 
-// DTR_BWD_APPLY_FIN: 0 = only C <= 64 (round-1 rule), 1 (default) = when the grid's
+// tune bwd_apply_fin: 0 = only C <= 64 (round-1 rule), 1 (default) = when the grid's
 // redundant finalize reads stay <= 1/4 of the apply's streamed bytes, 2 = always.
 bool bn_bwd_apply_acc_fits(int M, int C) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = std::getenv("DTR_BWD_APPLY_FIN");
-    mode = e ? std::atoi(e) : 1;
-  }
+  const long mode = tune(T_BWD_APPLY_FIN);
   const long nvec = (long)M * C / 8;
   if (C % 8 != 0 || 256 % (C / 8) != 0 || C > 2048) return false;
   if (bwd_fin_small(M, C)) return true;

@@ -174,10 +174,11 @@ Comm::Comm(std::unique_ptr<Transport> t, int world, int rank)
 Comm::~Comm() = default;
 
 std::unique_ptr<Comm> Comm::shm(const std::string& name, int world, int rank, int device,
-                                size_t slot_bytes, double timeout_s) {
+                                size_t slot_bytes, double timeout_s, double init_timeout_s) {
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("Comm: bad rank/world");
-  return std::unique_ptr<Comm>(
-      new Comm(make_shm_transport(name, world, rank, device, slot_bytes, timeout_s), world, rank));
+  return std::unique_ptr<Comm>(new Comm(
+      make_shm_transport(name, world, rank, device, slot_bytes, timeout_s, init_timeout_s), world,
+      rank));
 }
 
 std::unique_ptr<Comm> Comm::loopback(float factor) {

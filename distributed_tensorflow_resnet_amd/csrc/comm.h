@@ -62,8 +62,10 @@ class Comm {
 
   // Collective (every rank, same name): the shared-memory rehearsal transport.
   // device < 0: host buffers only (host_all_reduce; CPU tests).
+  // timeout_s bounds every collective's waits; init_timeout_s (<= 0: timeout_s) the
+  // attach, i.e. the ranks' start-up skew.
   static std::unique_ptr<Comm> shm(const std::string& name, int world, int rank, int device,
-                                   size_t slot_bytes, double timeout_s);
+                                   size_t slot_bytes, double timeout_s, double init_timeout_s);
   static std::unique_ptr<Comm> loopback(float factor);
 
   void all_reduce(void* buf, size_t count, int dtype, hipStream_t s);
@@ -89,7 +91,8 @@ class Comm {
 
 // shm transport factory (comm_shm.cpp)
 std::unique_ptr<Transport> make_shm_transport(const std::string& name, int world, int rank,
-                                              int device, size_t slot_bytes, double timeout_s);
+                                              int device, size_t slot_bytes, double timeout_s,
+                                              double init_timeout_s);
 // host entry points of the shm transport (throw if `t` is not one)
 void shm_host_all_reduce(Transport* t, void* buf, size_t count, int dtype);
 void shm_host_broadcast(Transport* t, void* buf, size_t count, int dtype, int root);

@@ -107,9 +107,9 @@ bool pid_alive(pid_t p) {
 class ShmTransport final : public Transport {
  public:
   ShmTransport(const std::string& name, int world, int rank, int device, size_t slot_bytes,
-               double timeout_s)
+               double timeout_s, double init_timeout_s)
       : name_(name), world_(world), rank_(rank), device_(device),
-        slot_bytes_((slot_bytes + 63) & ~size_t(63)), timeout_s_(timeout_s) {
+        slot_bytes_((slot_bytes + 63) & ~size_t(63)), timeout_s_(init_timeout_s) {
     if (world < 1 || world > kMaxRanks) throw std::invalid_argument("shm comm: world out of range");
     if (slot_bytes_ < 4096) throw std::invalid_argument("shm comm: slot_bytes < 4096");
     if (name.empty() || name[0] != '/' || name.find('/', 1) != std::string::npos)
@@ -181,11 +181,12 @@ class ShmTransport final : public Transport {
       res_ = host_res_.data();
     }
     try {
-      barrier("attach");
-    } catch (...) {   // no destructor runs for a throwing constructor
+      barrier("attach");   // (the ranks' process start-up skew: the init timeout)
+    } catch (...) {        // no destructor runs for a throwing constructor
       release();
       throw;
     }
+    timeout_s_ = timeout_s;
     if (owner_) {
       ::shm_unlink(name_.c_str());
       unlinked_ = true;
@@ -400,9 +401,11 @@ ShmTransport* as_shm(Transport* t) {
 }  // namespace
 
 std::unique_ptr<Transport> make_shm_transport(const std::string& name, int world, int rank,
-                                              int device, size_t slot_bytes, double timeout_s) {
+                                              int device, size_t slot_bytes, double timeout_s,
+                                              double init_timeout_s) {
   return std::unique_ptr<Transport>(new ShmTransport(name, world, rank, device, slot_bytes,
-                                                     timeout_s));
+                                                     timeout_s,
+                                                     init_timeout_s > 0 ? init_timeout_s : timeout_s));
 }
 
 void shm_host_all_reduce(Transport* t, void* buf, size_t count, int dtype) {

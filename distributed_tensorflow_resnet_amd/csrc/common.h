@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tune.h"
+
 namespace dtr {
 
 typedef __bf16 bf16;
@@ -128,17 +130,10 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// Host: conv epilogue / dh stores write-through (sc1).  DTR_WT_STORE=1 forces it on for
-// every conv, =0 off; unset: the direct 3x3 convs decide by output size
+// Host: conv epilogue / dh stores write-through (sc1).  tune wt_store = 1 forces it on
+// for every conv, 0 off; -1 (default): the direct 3x3 convs decide by output size
 // (wt_store_direct), the implicit-GEMM convs store normally.
-inline int wt_store_mode() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = std::getenv("DTR_WT_STORE");
-    v = e == nullptr ? -1 : (e[0] == '1' ? 1 : 0);
-  }
-  return v;
-}
+inline int wt_store_mode() { return (int)tune(T_WT_STORE); }
 inline bool wt_store_enabled() { return wt_store_mode() == 1; }
 // Direct convs: write-through once a launch writes >= 2 MB.  A kernel boundary pays
 // ~bytes / 6 TB/s to write back the dirty lines its predecessor left in L2

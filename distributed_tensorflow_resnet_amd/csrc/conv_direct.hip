@@ -319,11 +319,10 @@ conv3x3_direct_kernel(GemmArgs args) {
 static long long* g_probe = nullptr;   // set_direct_probe (diagnostics only): each launch
 void set_direct_probe(long long* p) { g_probe = p; }   // advances it past its own stamps
 
-// DTR_DIRECT_LDSW bitmask (1: C16, 2: C32, 4: C64) of the layers whose weights are
+// tune direct_ldsw: bitmask (1: C16, 2: C32, 4: C64) of the layers whose weights are
 // staged through LDS.  Default 4, measured (CIFAR RN50, probe + bench): C64 stage
 // phase 4.8 -> 4.0 us (dgrad) and 3.5 -> 3.1 (fwd); step bs16 0.978 -> 0.955 ms,
 // bs128 unchanged (1.293 / 1.300); C16/C32 add LDS reads without a gain.
-static int g_direct_ldsw = -1;   // -1: read DTR_DIRECT_LDSW once
 
 template <int CA, int WI, int BM, int BN, int WM, int WN, int MODE, int FLAGS, bool LW>
 static void launch_direct_lw(const GemmArgs& a, hipStream_t s) {
@@ -344,11 +343,7 @@ static void launch_direct_cfg(const GemmArgs& a0, hipStream_t s) {
   a.probe = g_probe;
   const long out_bytes = (long)a.M * a.Ncol * 2;
   a.wt = wt_store_direct(out_bytes) && out_bytes < (1L << 31) ? 1 : 0;
-  if (g_direct_ldsw < 0) {
-    const char* e = std::getenv("DTR_DIRECT_LDSW");
-    g_direct_ldsw = e ? std::atoi(e) : 4;
-  }
-  if (g_direct_ldsw & (CA / 16)) launch_direct_lw<CA, WI, BM, BN, WM, WN, MODE, FLAGS, true>(a, s);
+  if (tune(T_DIRECT_LDSW) & (CA / 16)) launch_direct_lw<CA, WI, BM, BN, WM, WN, MODE, FLAGS, true>(a, s);
   else launch_direct_lw<CA, WI, BM, BN, WM, WN, MODE, FLAGS, false>(a, s);
   if (g_probe) g_probe += 8L * (a.M / BM) * ((a.Ncol + BN - 1) / BN);
 }
@@ -373,36 +368,27 @@ static void launch_direct_flags(const GemmArgs& a, hipStream_t s) {
   }
 }
 
-static int g_direct_enabled = -1;   // -1: read DTR_DIRECT_CONV once
-static int g_direct_split = -2;     // -2: read DTR_DIRECT_SPLITN once (bit 0: C32, bit 1: C64)
-
-// Column-split mask for this launch.  Default (DTR_DIRECT_SPLITN unset): always for the
+// Column-split mask for this launch (tune direct_splitn: bit 0 C32, bit 1 C64 in two, bit 2
+// C64 in four).  Default (-1): always for the
 // 8x8x64 layers, for 16x16x32 only while its grid has fewer workgroups than CUs
 // (measured, CIFAR RN50 step: bs128 1.444 -> 1.400 ms, bs32 1.135 -> 1.077, bs16
 // 1.074 -> 1.022; splitting 16x16x32 at bs128, 512 -> 1024 workgroups, cost 8 %).
 static int direct_split_mask(const GemmArgs& a, int bm) {
-  if (g_direct_split == -2) {
-    const char* e = std::getenv("DTR_DIRECT_SPLITN");
-    g_direct_split = e ? std::atoi(e) : -1;
-  }
-  if (g_direct_split >= 0) return g_direct_split;
+  const long forced = tune(T_DIRECT_SPLITN);
+  if (forced >= 0) return (int)forced;
   // four column tiles of the 8x8x64 layers at <= 32 images (<= 32 row tiles; measured
   // step: bs16 0.952 -> 0.951 / bs32 0.994 -> 0.977 ms; at 128 images 1.273 -> 1.291)
   const bool c64_4way = a.g.C == 64 || a.g.K == 64 ? (a.M / bm) <= 32 : false;
   return 2 | ((a.M / bm) < 256 ? 1 : 0) | (c64_4way ? 4 : 0);
 }
 
-void set_conv_direct(int enabled) { g_direct_enabled = enabled ? 1 : 0; }
+void set_conv_direct(int enabled) { tune_set(T_DIRECT_CONV, enabled ? 1 : 0); }
 
 // Whether the direct kernel covers this conv: 3x3, stride 1, pad 1, A channels ==
 // output channels == {16 @ W 32, 32 @ W 16, 64 @ W 8}, and the tile height BM
 // (= conv_gemm_bm, so the BN-stat partial layout is unchanged) divides the image.
 bool conv_direct_covers(const GemmArgs& a, int mode) {
-  if (g_direct_enabled < 0) {
-    const char* e = std::getenv("DTR_DIRECT_CONV");
-    g_direct_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  if (!g_direct_enabled) return false;
+  if (!tune(T_DIRECT_CONV)) return false;
   const ConvGeom& g = a.g;
   if (g.kh != 3 || g.kw != 3 || g.stride != 1 || g.pad != 1 || g.H != g.Ho || g.W != g.Wo)
     return false;
@@ -435,7 +421,7 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s) {
   // two column tiles (half the weights and MFMAs per workgroup, twice the workgroups)
   // for the layers whose grids are small: 8x8x64 (16 workgroups per image batch of 16)
   // and, at small batch, 16x16x32
-  if (split & 4) {   // four column tiles of the 8x8x64 layers (sweep: DTR_DIRECT_SPLITN=5|7)
+  if (split & 4) {   // four column tiles of the 8x8x64 layers
     DTR_DIRECT_BN(64, 8, 64, 16, 4, 1)
   }
   if (split & 2) {

@@ -61,12 +61,7 @@ conv_gemm_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
-  // ABWD (dgrad, FAST loop only): the A operand is the pending BatchNorm+ReLU backward
-  // of the produced gradient, dh = a*g - b - c*xhat with g = da*[x*scale+shift > 0],
-  // applied while staging A (coefficients precomputed by bn_bwd_finalize); the
-  // workgroups of column tile 0 also write dh once (center tap) for the weight
-  // gradient -- no separate bn_bwd_apply pass over da / x / dh.
-  constexpr bool ABWD = (FLAGS & F_ABWD) != 0;
+  static_assert((FLAGS & F_ABWD) == 0, "the fused BN backward prologue is direct-conv only");
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MR = WTM / 16, NR = WTN / 16;
@@ -107,20 +102,7 @@ conv_gemm_kernel(GemmArgs args) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  // Tile order.  Workgroups are dispatched x-fastest and dealt round-robin to the 8
-  // XCDs, each with its own L2; with `swz` the logical tile of linear id L is
-  // chunk (L % 8) of the tile list, walked N-fastest, so the workgroups resident on
-  // one XCD at a time cover a few A row blocks with ALL their column tiles (A read
-  // once per XCD from HBM instead of once per column tile).
-  int tm = blockIdx.x, tn = blockIdx.y;
-  if (args.swz) {
-    const int TMn = gridDim.x, TNn = gridDim.y;
-    const int L = blockIdx.x + TMn * blockIdx.y;
-    const int full = (TMn * TNn) & ~7;
-    const int lg = L < full ? (L & 7) * (full >> 3) + (L >> 3) : L;
-    tm = lg / TNn;
-    tn = lg - tm * TNn;
-  }
+  const int tm = blockIdx.x, tn = blockIdx.y;
   const int m0 = tm * BM;
   const int n0 = tn * BN;
 
@@ -359,12 +341,6 @@ conv_gemm_kernel(GemmArgs args) {
   bf16x8 pa[2][A_PER_T], pb[2][B_PER_T];
   unsigned pmask[2] = {0u, 0u};
   int pci[2] = {0, 0};
-  bf16x8 px[ABWD ? 2 : 1][ABWD ? A_PER_T : 1];   // ABWD: BN input rows of the A chunks
-  int poff[ABWD ? 2 : 1][ABWD ? A_PER_T : 1];    // ABWD: their byte offsets (dh write)
-  bool pctr[2] = {false, false};                 // ABWD: the tile is the center tap
-  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16*>(ABWD ? args.abwd.x : args.a), 0, (int)(fast && ABWD ? a_elems * 2 : 0),
-      0x00020000);
   // split-K slice of this workgroup: K tiles [t_beg, t_end)
   const int KT_all = (KD + BK - 1) / BK;
   const int sk_n = args.ksplit > 1 ? args.ksplit : 1, sk_z = sk_n > 1 ? (int)blockIdx.z : 0;
@@ -381,10 +357,6 @@ conv_gemm_kernel(GemmArgs args) {
     if (MODE == MODE_DGRAD && args.par) class_tap(tap, rr, cc);
     const int gtap = rr * g.kw + cc;   // kernel tap (weight layout)
     unsigned msk = 0u;
-    if constexpr (ABWD) {
-      pci[p] = kv ? ci : 0;
-      pctr[p] = kv && rr == g.kh / 2 && cc == g.kw / 2;
-    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       int off = kOOB;
@@ -406,12 +378,8 @@ conv_gemm_kernel(GemmArgs args) {
         msk |= ok ? (1u << i) : 0u;
       }
       pa[p][i] = bload(rs_a, off);
-      if constexpr (ABWD) {
-        px[p][i] = bload(rs_x, off);
-        poff[p][i] = off;
-      }
     }
-    if constexpr (PRE || ABWD) pmask[p] = msk;
+    if constexpr (PRE) pmask[p] = msk;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int q = tid + i * 256;
@@ -427,26 +395,6 @@ conv_gemm_kernel(GemmArgs args) {
     constexpr int p = decltype(P)::value;
     bf16* A = As + buf * BM * BK;
     bf16* B = Bs + buf * BN * BK;
-    float ca[8], ccr[8], cd[8], csc[8], csh[8];   // ABWD: this thread's 8 channels
-    if constexpr (ABWD) {
-      const float* T = pre_s + pci[p];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 va = *reinterpret_cast<const f32x4*>(T + 4 * h);
-        const f32x4 vc = *reinterpret_cast<const f32x4*>(T + Acin + 4 * h);
-        const f32x4 vd = *reinterpret_cast<const f32x4*>(T + 2 * Acin + 4 * h);
-        const f32x4 vs = *reinterpret_cast<const f32x4*>(T + 3 * Acin + 4 * h);
-        const f32x4 vh = *reinterpret_cast<const f32x4*>(T + 4 * Acin + 4 * h);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ca[4 * h + j] = va[j];
-          ccr[4 * h + j] = vc[j];
-          cd[4 * h + j] = vd[j];
-          csc[4 * h + j] = vs[j];
-          csh[4 * h + j] = vh[j];
-        }
-      }
-    }
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int q = tid + i * 256;
@@ -456,19 +404,6 @@ conv_gemm_kernel(GemmArgs args) {
         if constexpr (PRE) {
           const unsigned sel = 0u - ((pmask[p] >> i) & 1u);   // all-ones: real pixel
           v = affine_relu8_sel(v, s0, s1, b0, b1, sel);
-        }
-        if constexpr (ABWD) {
-          const bool real = (pmask[p] >> i) & 1u;   // padding / out-of-range stays zero
-          bf16x8 dh;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xv = (float)px[p][i][j];
-            const float gg = (xv * csc[j] + csh[j] > 0.f) ? (float)v[j] : 0.f;
-            dh[j] = (bf16)(real ? ca[j] * gg - ccr[j] * xv - cd[j] : 0.f);
-          }
-          v = dh;
-          if (real && pctr[p] && tn == 0)   // each dh element once: center tap, column tile 0
-            *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(args.abwd.a_out) + poff[p][i]) = dh;
         }
         *reinterpret_cast<bf16x8*>(A + r * BK + ((kg ^ (r & 7)) << 3)) = v;
       }
@@ -525,21 +460,7 @@ conv_gemm_kernel(GemmArgs args) {
     using I1 = std::integral_constant<int, 1>;
     issue(t_beg, I0{});
     issue(t_beg + 1, I1{});
-    if constexpr (BNB && !ABWD) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
-    if constexpr (ABWD) {   // [5][Acin]: a, c*rstd, b - c*rstd*mean, scale, shift
-      // dh = a*g - b - c*(x - mean)*rstd = a*g - (c*rstd)*x - (b - c*rstd*mean)
-      const BnBwdPre& Q = args.abwd;
-      for (int c = tid; c < Acin; c += 256) {
-        const float a = Q.coef[c], bb = Q.coef[Acin + c], cc = Q.coef[2 * Acin + c];
-        const float cr = cc * Q.rstd[c];
-        pre_s[c] = a;
-        pre_s[Acin + c] = cr;
-        pre_s[2 * Acin + c] = bb - cr * Q.mean[c];
-        pre_s[3 * Acin + c] = Q.scale[c];
-        pre_s[4 * Acin + c] = Q.shift[c];
-      }
-      __syncthreads();
-    }
+    if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
     if constexpr (PRE) {
       if (args.pfin.cnt > 0) {
         bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
@@ -657,59 +578,36 @@ conv_gemm_kernel(GemmArgs args) {
   }
   }
 
-  if constexpr (BNB && EP::ON && !ABWD)
+  if constexpr (BNB && EP::ON)
     conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre, tm, tn);
   else
     conv_epilogue<BM, BN, WM, WN, FLAGS, false>(args, acc, smem, m0, n0, nullptr, tm, tn);
 }
 
 // ---------------------------------------------------------------------------
-// host-side dispatch
+// host-side dispatch (tile / schedule parameters: tune.h)
 // ---------------------------------------------------------------------------
-static int g_pipe_enabled = -1;   // -1: read DTR_CONV_PIPE once (default on)
-void set_conv_pipeline(int enabled) {
-  g_pipe_enabled = enabled ? 1 : 0;
-  set_wgrad_pipeline(enabled);
-}
+void set_conv_pipeline(int enabled) { tune_set(T_CONV_PIPE, enabled ? 1 : 0); }
 
 // Split-K of the FAST loop for under-filled grids (the 7x7 stage: 196 tiles of 128x128
-// for 256 CUs, each a 32-72 K-tile loop at one workgroup per CU).  DTR_SPLITK = max
-// slices (default 2; 0 or 1 = off).  Workspace: one fp32 tile per slice and tile plus a
-// ticket per tile, allocated on first need (never while a graph is being captured --
-// the launch then runs unsplit) and grown, never freed.
-static int g_splitk = -1;
-static float* g_sk_part = nullptr;
-static size_t g_sk_part_bytes = 0;
-static unsigned* g_sk_cnt = nullptr;
-static size_t g_sk_cnt_n = 0;
-
-void set_conv_splitk(int max_slices) { g_splitk = max_slices < 1 ? 1 : max_slices; }
+// for 256 CUs, each a 32-72 K-tile loop at one workgroup per CU): up to `splitk` slices
+// for grids of <= `splitk_tiles` tiles.  Workspace: one fp32 tile per slice and tile plus
+// a ticket per tile, per device, allocated on first need (never while a graph is being
+// captured -- the launch then runs unsplit) and grown, never freed.  The launches that
+// use it are ordered on one stream (the training plan issues every conv_gemm on the main
+// stream); the ticket of a tile is reset by its last slice.
+void set_conv_splitk(int max_slices) { tune_set(T_SPLITK, max_slices < 1 ? 1 : max_slices); }
 
 static int pick_ksplit(long tiles, int KT) {
-  // DTR_SPLITK_TILES: largest grid (tiles) that is split.  Default 256 (one tile per
-  // CU or fewer): splitting the 392-tile 14x14 grids measured slower (3x3 fwd 72 -> 82
-  // us, 1x1 40 -> 53; ImageNet step 12.93 -> 13.24 ms)
-  static long max_tiles = -1;
-  if (g_splitk < 0) {
-    const char* e = std::getenv("DTR_SPLITK");
-    g_splitk = e ? std::atoi(e) : 2;
-  }
-  if (max_tiles < 0) {
-    const char* e = std::getenv("DTR_SPLITK_TILES");
-    max_tiles = e ? std::atol(e) : 256;
-  }
+  const long smax = tune(T_SPLITK), max_tiles = tune(T_SPLITK_TILES);
   int S = 1;
-  while (S * 2 <= g_splitk && tiles * S <= max_tiles && KT / (S * 2) >= 8) S *= 2;
+  while (S * 2 <= smax && tiles * S <= max_tiles && KT / (S * 2) >= 8) S *= 2;
   return S;
 }
 
 // FAST-path eligibility (see the kernel): must match the kernel's own `fast` test.
 static bool conv_gemm_fast(const GemmArgs& a, int mode) {
-  if (g_pipe_enabled < 0) {
-    const char* e = std::getenv("DTR_CONV_PIPE");
-    g_pipe_enabled = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!g_pipe_enabled) return false;
+  if (!tune(T_CONV_PIPE)) return false;
   const ConvGeom& g = a.g;
   const int Acin = (mode == MODE_FWD) ? g.C : g.K;
   const long a_elems = (mode == MODE_FWD) ? (long)g.N * g.H * g.W * g.C
@@ -721,47 +619,53 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   //   forward: >= 128 output channels (1.02-1.24x; the 64-column 56x56 convs
   //            run 0.81-0.83x: their single-set loop keeps more tiles per CU);
   //   dgrad:   >= 16k rows (1.06-1.16x at 14x14..56x56; the 7x7 grids of <= 200
-  //            tiles run 0.88-0.95x).
+  //            tiles run 0.88-0.95x) -- and the 7x7 dgrads once split-K doubles their grid.
   if (a.Kdim < 256) return false;
   if (mode == MODE_FWD) return a.Ncol >= 128;
   if (a.M >= 16384) return true;
-  // the 7x7 dgrads: pipelined once split-K doubles their grid (DTR_DGRAD_SPLITK=0: off)
-  static int dsk = -1;
-  if (dsk < 0) {
-    const char* e = std::getenv("DTR_DGRAD_SPLITK");
-    dsk = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!dsk || a.Ncol < 128) return false;
+  if (!tune(T_DGRAD_SPLITK) || a.Ncol < 128) return false;
   const int bm = conv_gemm_bm(a.M, a.Ncol), bn = conv_gemm_bn(a.M, a.Ncol);
   const long tiles = (long)((a.M + bm - 1) / bm) * ((a.Ncol + bn - 1) / bn);
   return pick_ksplit(tiles, (a.Kdim + 63) / 64) > 1;
 }
 
-static int g_xcd_swz = -1;   // DTR_XCD_SWZ: 0 off, 1 on (default: see launch_cfg)
+struct SplitKWorkspace {
+  float* part = nullptr;
+  size_t part_bytes = 0;
+  unsigned* cnt = nullptr;
+  size_t cnt_n = 0;
+};
 
-static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s) {
-  if (part_bytes <= g_sk_part_bytes && tiles <= g_sk_cnt_n) return true;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(s, &cap);
-  if (cap != hipStreamCaptureStatusNone) return false;
-  if (part_bytes > g_sk_part_bytes) {
-    void* p = nullptr;
-    if (hipMalloc(&p, part_bytes) != hipSuccess) return false;
-    g_sk_part = static_cast<float*>(p);   // the old buffer may still be read in flight: kept
-    g_sk_part_bytes = part_bytes;
+static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s, float** part,
+                             unsigned** cnt) {
+  static SplitKWorkspace ws[64];   // per device
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return false;
+  if (dev < 0 || dev >= 64) return false;
+  SplitKWorkspace& w = ws[dev];
+  if (part_bytes > w.part_bytes || tiles > w.cnt_n) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cap);
+    if (cap != hipStreamCaptureStatusNone) return false;
+    if (part_bytes > w.part_bytes) {
+      void* p = nullptr;
+      if (hipMalloc(&p, part_bytes) != hipSuccess) return false;
+      w.part = static_cast<float*>(p);   // the old buffer may still be read in flight: kept
+      w.part_bytes = part_bytes;
+    }
+    if (tiles > w.cnt_n) {
+      void* p = nullptr;
+      const size_t n = tiles < 4096 ? 4096 : tiles;
+      if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return false;
+      if (hipMemsetAsync(p, 0, n * sizeof(unsigned), s) != hipSuccess) return false;
+      w.cnt = static_cast<unsigned*>(p);
+      w.cnt_n = n;
+    }
   }
-  if (tiles > g_sk_cnt_n) {
-    void* p = nullptr;
-    const size_t n = tiles < 4096 ? 4096 : tiles;
-    if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return false;
-    if (hipMemsetAsync(p, 0, n * sizeof(unsigned), s) != hipSuccess) return false;
-    g_sk_cnt = static_cast<unsigned*>(p);
-    g_sk_cnt_n = n;
-  }
+  *part = w.part;
+  *cnt = w.cnt;
   return true;
 }
-
-static int g_nbuf1 = -1;   // DTR_NBUF1_KT: single-buffered LDS when the K loop has <= this many tiles
 
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
 static void launch_nbuf(const GemmArgs& a0, hipStream_t s);
@@ -772,21 +676,8 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
   // ImageNet 56x56 stage) double-buffers nothing: one LDS buffer halves the main-loop
   // LDS, so the 128x128 tiles fit 4 workgroups per CU instead of 2 and the
   // load -> MFMA -> epilogue phases of co-resident workgroups overlap.
-  if (g_nbuf1 < 0) {
-    const char* e = std::getenv("DTR_NBUF1_KT");
-    g_nbuf1 = e ? std::atoi(e) : 1;
-  }
-  // The narrow stem operand (8 / 16 channels, K <= 4-7 tiles, 12.5k workgroups of pure
-  // load latency): single-buffered too, for more co-resident workgroups per CU
-  // (DTR_NARROW_NBUF1=1: on; A/B pending)
-  static int narrow_nbuf1 = -1;
-  if (narrow_nbuf1 < 0) {
-    const char* e = std::getenv("DTR_NARROW_NBUF1");
-    narrow_nbuf1 = (e && e[0] == '1') ? 1 : 0;
-  }
-  const bool narrow = MODE == MODE_FWD && (FLAGS & F_PRE) == 0 && a.g.C < 64 && narrow_nbuf1;
-  if constexpr (BM * BN >= 128 * 64 && (FLAGS & F_ABWD) == 0) {
-    if (((a.Kdim + 63) / 64 <= g_nbuf1 || narrow) && !conv_gemm_fast(a, MODE)) {
+  if constexpr (BM * BN >= 128 * 64) {
+    if ((a.Kdim + 63) / 64 <= tune(T_NBUF1_KT) && !conv_gemm_fast(a, MODE)) {
       launch_nbuf<BM, BN, WM, WN, MODE, FLAGS, 1>(a, s);
       return;
     }
@@ -796,46 +687,31 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
 static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
-  if (g_xcd_swz < 0) {
-    const char* e = std::getenv("DTR_XCD_SWZ");
-    g_xcd_swz = e ? std::atoi(e) : 0;
-  }
   GemmArgs a = a0;
-  a.swz = (g_xcd_swz && (a.Ncol + BN - 1) / BN > 1) ? 1 : 0;
   a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)NBUF * (BM + BN) * 64 * sizeof(bf16);
   if (FLAGS & F_PRE) lds += (size_t)2 * Acin * sizeof(float);
-  if (FLAGS & F_ABWD) lds += (size_t)5 * Acin * sizeof(float);
   lds = std::max(lds, EpiLayout<BM, BN, WM>::BYTES);
   lds = (lds + 15) & ~(size_t)15;
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN, a.par ? 4 : 1);
-  // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles; the
-  // fused BN backward (ABWD) exists only there
+  // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles
   if constexpr (NBUF == 1) {   // general loop only (launch_cfg: one-tile K loops)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, 1>), grid,
                        dim3(256), lds, s, a);
     DTR_CHECK_LAUNCH();
   } else {
-    if constexpr ((FLAGS & F_ABWD) != 0) {
-      if constexpr (BN >= 64) {
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
-                           dim3(256), lds, s, a);
-        DTR_CHECK_LAUNCH();
-      } else {
-        throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
-      }
-      return;
-    }
     if constexpr (BN >= 64) {
       if (conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
         const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
+        float* part = nullptr;
+        unsigned* cnt = nullptr;
         if (S > 1 && splitk_workspace((size_t)S * tiles * BM * BN * sizeof(float),
-                                      (size_t)tiles, s)) {
+                                      (size_t)tiles, s, &part, &cnt)) {
           a.ksplit = S;
-          a.sk_part = g_sk_part;
-          a.sk_cnt = g_sk_cnt;
+          a.sk_part = part;
+          a.sk_cnt = cnt;
           grid.z = S;
         }
         hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
@@ -860,15 +736,6 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
     else if (st) launch_cfg<BM, BN, WM, WN, MODE, F_STATS>(a, s);
     else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   } else {
-    const bool ab = a.abwd.x != nullptr;
-    if constexpr (BN >= 64) {
-      if (ab) {
-        if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB | F_ABWD>(a, s);
-        else launch_cfg<BM, BN, WM, WN, MODE, F_ABWD>(a, s);
-        return;
-      }
-    }
-    if (ab) throw std::runtime_error("conv_gemm: fused BN backward needs a >= 64-column tile");
     if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB>(a, s);
     else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   }
@@ -876,48 +743,17 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
 
 // Tile selection by output width; BM shrinks for small M so the grid still
 // covers the 256 CUs.  Shared by the launcher and by the host (the BN-stat
-// partial buffer has one row per M tile).
+// partial buffer has one row per M tile).  Row thresholds: tune.h.
 int conv_gemm_bm(int M, int nc) {
   const long m = M;
-  // DTR_SMALLC_BM="b16,b32": the large-M tile heights of the 16- / 32-column convs
-  // (the CIFAR stages 1 / 2; sweeps of rows per workgroup vs workgroups per CU)
-  static int b16 = -1, b32 = -1;
-  if (b16 < 0) {
-    b16 = 256, b32 = 128;
-    if (const char* e = std::getenv("DTR_SMALLC_BM")) std::sscanf(e, "%d,%d", &b16, &b32);
-    if (b16 != 256 && b16 != 128 && b16 != 64) b16 = 256;
-    if (b32 != 128 && b32 != 64) b32 = 128;
-  }
-  // DTR_C16_MID: rows from which (below 256 x 512) the 16-column convs use 128-row
-  // tiles.  Default 32768: the CIFAR stage-1 grids then stay near 2 workgroups per CU
-  // at 32-64 images (measured, CIFAR RN50 step: bs64 1.233 -> 1.08 ms, bs32 1.013 ->
-  // 1.004; bs16 keeps 64-row tiles, 256 workgroups: 0.953 vs 0.965 with 128)
-  static long mid16 = -2;
-  if (mid16 == -2) {
-    const char* e = std::getenv("DTR_C16_MID");
-    mid16 = e ? std::atol(e) : 32768;
-  }
-  if (nc <= 16) return m >= 256L * 512 ? b16 : (mid16 >= 0 && m >= mid16) ? 128 : 64;
-  // DTR_C32_MID: likewise for the 32-column convs.  Default 32768 (the stage-2 convs
-  // at 128 images: 256 instead of 512 workgroups, step 1.303 -> 1.273 ms; at 64
-  // images 128-row tiles measured 1.126 vs 1.088 ms, so smaller grids keep 64 rows)
-  static long mid32 = -2;
-  if (mid32 == -2) {
-    const char* e = std::getenv("DTR_C32_MID");
-    mid32 = e ? std::atol(e) : 32768;
-  }
-  if (nc <= 32) return m >= 128L * 512 ? b32 : (mid32 >= 0 && m >= mid32) ? 128 : 64;
+  long b16 = tune(T_SMALLC_BM16), b32 = tune(T_SMALLC_BM32);
+  if (b16 != 256 && b16 != 128 && b16 != 64) b16 = 256;
+  if (b32 != 128 && b32 != 64) b32 = 128;
+  const long mid16 = tune(T_C16_MID), mid32 = tune(T_C32_MID);
+  if (nc <= 16) return m >= 256L * 512 ? (int)b16 : (mid16 >= 0 && m >= mid16) ? 128 : 64;
+  if (nc <= 32) return m >= 128L * 512 ? (int)b32 : (mid32 >= 0 && m >= mid32) ? 128 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
-  // DTR_BM128_MIN: rows from which the 128x128 tile is used.  Default 4096: the
-  // 7x7 stage (6272 rows) too -- its 64x64 grids re-read A and B 2x more from L2 /
-  // HBM (measured, bench_kernels.py: 7x7 fwd 118 -> 87 / 59 -> 46 us, dgrad 93 -> 84
-  // / 40 -> 33 us despite 196 tiles for 256 CUs; ImageNet RN50 step -0.6 %)
-  static long min128 = -1;
-  if (min128 < 0) {
-    const char* e = std::getenv("DTR_BM128_MIN");
-    min128 = e ? std::atol(e) : 4096;
-  }
-  return (m >= min128 && nc % 128 == 0) ? 128 : 64;
+  return (m >= tune(T_BM128_MIN) && nc % 128 == 0) ? 128 : 64;
 }
 
 int conv_gemm_bn(int M, int nc) {
@@ -927,29 +763,13 @@ int conv_gemm_bn(int M, int nc) {
   return conv_gemm_bm(M, nc) == 128 ? 128 : 64;
 }
 
-// Wide-output tile experiment knob (>64 output columns): bit 0 = forward,
-// bit 1 = dgrad use 128x64 (4x1 waves, single-phase epilogue) instead of 128x128.
-static int g_wide_mask = -1;
-void set_conv_wide_tile(int mask) { g_wide_mask = mask; }
-static int wide_mask() {
-  if (g_wide_mask < 0) {
-    const char* e = std::getenv("DTR_WIDE_128x64");
-    g_wide_mask = e ? std::atoi(e) : 0;
-  }
-  return g_wide_mask;
-}
-
 template <int MODE>
 static void launch_mode(const GemmArgs& a, hipStream_t s) {
   const int nc = a.Ncol;
   const int bm = conv_gemm_bm(a.M, nc);
-  if (nc > 64 && bm == 128 && (wide_mask() & (MODE == MODE_FWD ? 1 : 2))) {
-    launch_flags<128, 64, 4, 1, MODE>(a, s);
-    return;
-  }
   if (nc <= 16) {
     if (bm == 256) launch_flags<256, 16, 4, 1, MODE>(a, s);
-    else if (bm == 128) launch_flags<128, 16, 4, 1, MODE>(a, s);   // DTR_SMALLC_BM sweeps
+    else if (bm == 128) launch_flags<128, 16, 4, 1, MODE>(a, s);
     else launch_flags<64, 16, 4, 1, MODE>(a, s);
   } else if (nc <= 32) {
     if (bm == 128) launch_flags<128, 32, 4, 1, MODE>(a, s);
@@ -963,46 +783,25 @@ static void launch_mode(const GemmArgs& a, hipStream_t s) {
   }
 }
 
-// Whether the implicit-GEMM dgrad can apply a pending BN backward (ABWD) itself: the
-// FAST loop's structure (A channels a multiple of 64, tensors < 2^30 elements), a
-// >= 64-column tile, the [5][C] coefficient table within 10 KB of LDS (C <= 512, the
-// bottleneck's inner BNs), no residual add (the block-input BNs), coefficients
-// precomputed by bn_bwd_finalize (cnt 0).
-bool conv_gemm_abwd_covers(const GemmArgs& a) {
-  const ConvGeom& g = a.g;
-  const long a_elems = (long)g.N * g.Ho * g.Wo * g.K;
-  const long b_elems = (long)g.kh * g.kw * g.C * g.K;
-  if (g.K % 64 != 0 || g.K > 512 || a_elems >= (1L << 30) || b_elems >= (1L << 30)) return false;
-  if (a.Ncol < 64 || a.Ncol % 16 != 0) return false;
-  if (a.abwd.x != nullptr && (a.abwd.add != nullptr || a.abwd.cnt != 0 || a.abwd.acc != nullptr))
-    return false;
-  return true;
-}
-
-static int g_parity = -1;   // DTR_PARITY_DGRAD: stride-2 dgrads by output parity class
-void set_conv_parity(int enabled) { g_parity = enabled ? 1 : 0; }
+void set_conv_parity(int enabled) { tune_set(T_PARITY_DGRAD, enabled ? 1 : 0); }
 
 // Stride-2 dgrad as 4 parity classes of output pixels (one launch, blockIdx.z = class):
 // a pixel with (h + pad, w + pad) = (ph, pw) mod 2 only receives the filter taps r = ph,
 // ph + 2, .. and s = pw, pw + 2, .., so each class is a dense implicit GEMM over a
 // quarter of the rows and its own taps -- instead of every pixel running all kh x kw
 // taps with 3/4 of the (pixel, tap) pairs masked to zero (ImageNet's stride-2 dgrads
-// ran 3-3.5x slower than their forward convs).  Not with the fused BN backward (ABWD)
-// or tile-partial BN sums (their layouts are per row tile of the whole output).
+// ran 3-3.5x slower than their forward convs).  Not with tile-partial BN sums (their
+// layout is per row tile of the whole output).
 static bool parity_dgrad(const GemmArgs& a) {
-  if (g_parity < 0) {
-    const char* e = std::getenv("DTR_PARITY_DGRAD");
-    g_parity = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_parity && a.g.stride == 2 && a.abwd.x == nullptr &&
+  return tune(T_PARITY_DGRAD) && a.g.stride == 2 &&
          (a.bnb_part == nullptr || a.bnb_acc != nullptr) && a.out_f32 == nullptr &&
          a.bias == nullptr && a.residual == nullptr;
 }
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
   if (conv_direct(a, mode, s)) return;
-  if (a.abwd.x != nullptr && (mode != MODE_DGRAD || !conv_gemm_abwd_covers(a)))
-    throw std::runtime_error("conv_gemm: fused BN backward (abwd) not covered for this dgrad");
+  if (a.abwd.x != nullptr)
+    throw std::runtime_error("conv_gemm: the fused BN backward (abwd) is direct-conv only");
   if (mode == MODE_FWD) {
     launch_mode<MODE_FWD>(a, s);
   } else if (parity_dgrad(a)) {

@@ -388,42 +388,26 @@ conv_wgrad_kernel(WgradArgs args) {
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * WTM + a * 16 + gq * 4 + i;
         if (m < Cout && n < NT) {
-          if (args.wt) __hip_atomic_store(out + (long)m * NT + n, acc[a][b][i], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
-          else out[(long)m * NT + n] = acc[a][b][i];
+          out[(long)m * NT + n] = acc[a][b][i];
         }
       }
   }
 }
 
-static int g_wpipe_enabled = -1;   // -1: read DTR_CONV_PIPE once (default on)
-void set_wgrad_pipeline(int enabled) { g_wpipe_enabled = enabled ? 1 : 0; }
-
 // FAST eligibility: 32-bit buffer offsets, C % 8 == 0 (16-B channel chunks), and the
 // branch-free pixel stepping's 3 image-wrap rounds cover BK = 64 pixels.
 static bool wgrad_fast(const WgradArgs& a) {
-  if (g_wpipe_enabled < 0) {
-    const char* e = std::getenv("DTR_CONV_PIPE");
-    g_wpipe_enabled = (e && e[0] == '0') ? 0 : 1;
-  }
   const ConvGeom& g = a.g;
   const long x_elems = (long)g.N * g.H * g.W * g.C;
   const long dy_elems = (long)g.N * g.Ho * g.Wo * g.K;
   // (A/B on the ImageNet shapes: 1.05-1.2x at 14x14 / 7x7 outputs, 0.91-1.04x at
   // 56x56 / 28x28, where the occupancy of the one-set loop hides the latency)
-  return g_wpipe_enabled && x_elems < (1L << 30) && dy_elems < (1L << 30) &&
+  return tune(T_CONV_PIPE) && x_elems < (1L << 30) && dy_elems < (1L << 30) &&
          64 / g.Wo + 1 <= 3 * g.Ho && g.Ho <= 14;
 }
 
 template <int BM, int BN, int WM, int WN>
-static void wg_launch(const WgradArgs& a0, hipStream_t s) {
-  static int wt = -1;   // DTR_WG_WT=1: split-K partials stored write-through (A/B knob)
-  if (wt < 0) {
-    const char* e = std::getenv("DTR_WG_WT");
-    wt = (e && e[0] == '1') ? 1 : 0;
-  }
-  WgradArgs a = a0;
-  a.wt = wt;
+static void wg_launch(const WgradArgs& a, hipStream_t s) {
   const int NT = a.g.kh * a.g.kw * a.g.C;
   size_t lds = (size_t)2 * 64 * (BM + BN) * sizeof(bf16);
   dim3 grid((NT + BN - 1) / BN, (a.g.K + BM - 1) / BM, a.splits);
@@ -466,14 +450,9 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   const long P = (long)g.N * g.Ho * g.Wo;
   // ~768 workgroups (3 per CU) hide the per-tile load latency; cap the fp32
   // partial slabs at ~32 MB so the split-K reduce stays cheap, and keep >= 256
-  // pixels (4 K-tiles) per split.  (Measured sweep: scripts/sweep_wgrad.py.)
-  static long target = -1, cap_mb = -1;   // DTR_WGRAD_TARGET_WG / DTR_WGRAD_SLAB_MB (sweeps)
-  if (target < 0) {
-    const char* t = std::getenv("DTR_WGRAD_TARGET_WG");
-    const char* c = std::getenv("DTR_WGRAD_SLAB_MB");
-    target = t ? std::atol(t) : 768;
-    cap_mb = c ? std::atol(c) : 32;
-  }
+  // pixels (4 K-tiles) per split.  (Measured sweep: scripts/sweep_wgrad.py; tune
+  // wgrad_target_wg / wgrad_slab_mb.)
+  const long target = tune(T_WGRAD_TARGET_WG), cap_mb = tune(T_WGRAD_SLAB_MB);
   long splits = (target + tiles / 2) / tiles;
   const long slab = (long)g.K * NT * 4;
   const long cap_bytes = (cap_mb << 20) / (slab > 0 ? slab : 1);

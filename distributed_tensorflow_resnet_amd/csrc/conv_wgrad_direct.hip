@@ -31,7 +31,7 @@ namespace dtr {
 
 template <int C, int KO, int WI, int HI, int BMP, int TJ, bool PRE>
 __global__ void __launch_bounds__(256)
-conv_wgrad_direct_kernel(WgradArgs args, WgradGroup grp) {
+conv_wgrad_direct_kernel(WgradArgs args) {
   constexpr int HW = HI * WI;
   constexpr int NIMG = BMP >= HW ? BMP / HW : 1;
   constexpr int RH = BMP >= HW ? HI : BMP / WI;       // rows per image in the tile
@@ -54,14 +54,6 @@ conv_wgrad_direct_kernel(WgradArgs args, WgradGroup grp) {
   bf16* halo = dys + BMP * KO;                                // [NIMG][RH+2][W2][C]
   float* pre_s = reinterpret_cast<float*>(halo + HU * 8);     // [2][C]
 
-  if (grp.n > 0) {   // grouped launch: this workgroup's member (uniform)
-    const int z = blockIdx.z;
-    args.dy = grp.dy[z];
-    args.x = grp.x[z];
-    args.pre_scale = grp.scale[z];
-    args.pre_shift = grp.shift[z];
-    args.part = grp.part[z];
-  }
   const int split = blockIdx.x, tj = blockIdx.y;
   const int p0 = split * BMP;                                 // first pixel of the tile
   const int img0 = p0 / HW, h0 = (p0 - img0 * HW) / WI;       // h0 = 0 for whole images
@@ -183,18 +175,12 @@ conv_wgrad_direct_kernel(WgradArgs args, WgradGroup grp) {
 
 // (C, W, H, BMP, TJ) variants; BMP pixels per split, TJ taps per workgroup.
 template <int C, int WI, int HI, int BMP, int TJ>
-static void wgd_launch(const WgradArgs& a0, hipStream_t s, const WgradGroup& grp = WgradGroup{}) {
-  // Partial slabs stored write-through (sc1): the grouped reduce reads them from
-  // another launch, and no dirty slab lines are left for the kernel boundary to write
-  // back.  Measured, CIFAR RN50 step: bs128 1.315 / 1.316 -> 1.310 / 1.302 ms, bs16
-  // 0.950 -> 0.947.  DTR_WGD_WT=0: plain stores.
-  static int wt = -1;
-  if (wt < 0) {
-    const char* e = std::getenv("DTR_WGD_WT");
-    wt = (e && e[0] == '0') ? 0 : 1;
-  }
+static void wgd_launch(const WgradArgs& a0, hipStream_t s) {
+  // Partial slabs stored write-through (sc1, tune wgd_wt): the grouped reduce reads
+  // them from another launch, and no dirty slab lines are left for the kernel boundary
+  // to write back.
   WgradArgs a = a0;
-  a.wt = wt;
+  a.wt = tune(T_WGD_WT) ? 1 : 0;
   constexpr int NIMG = BMP >= HI * WI ? BMP / (HI * WI) : 1;
   constexpr int RH = BMP >= HI * WI ? HI : BMP / WI;
   constexpr size_t MAIN = (size_t)BMP * C * 2 + (size_t)NIMG * (RH + 2) * (WI + 2) * C * 2 +
@@ -202,33 +188,24 @@ static void wgd_launch(const WgradArgs& a0, hipStream_t s, const WgradGroup& grp
   constexpr int WK = 4 / (C / 16);
   constexpr size_t RED = (size_t)WK * C * TJ * C * sizeof(float);
   const size_t lds = ((MAIN > RED ? MAIN : RED) + 15) & ~(size_t)15;
-  dim3 grid(a.splits, 9 / TJ, grp.n > 0 ? grp.n : 1);
+  dim3 grid(a.splits, 9 / TJ);
   if (a.pre_scale)
     hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, true>), grid, dim3(256),
-                       lds, s, a, grp);
+                       lds, s, a);
   else
     hipLaunchKernelGGL((conv_wgrad_direct_kernel<C, C, WI, HI, BMP, TJ, false>), grid,
-                       dim3(256), lds, s, a, grp);
+                       dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
 }
 
-static int g_wgd_enabled = -1;
+void set_wgrad_direct(int enabled) { tune_set(T_DIRECT_WGRAD, enabled ? 1 : 0); }
 
-void set_wgrad_direct(int enabled) { g_wgd_enabled = enabled ? 1 : 0; }
-
-// Workgroups the direct kernel should at least launch (DTR_WGD_TARGET, default
-// 96): below it the tile shrinks (fewer pixels per split, then fewer taps per
-// workgroup).  At 16-32 images per rank (the 8-GPU strong-scaling share of the
-// global batch 128) the bs128-tuned tiles left 12-32 workgroups per stage-3/2
-// wgrad, ~10 us each, and the side stream became the backward's critical path.
-static int wgd_target() {
-  static int t = -1;
-  if (t < 0) {
-    const char* e = std::getenv("DTR_WGD_TARGET");
-    t = e ? std::atoi(e) : 96;
-  }
-  return t;
-}
+// Workgroups the direct kernel should at least launch (tune wgd_target): below it
+// the tile shrinks (fewer pixels per split, then fewer taps per workgroup).  At 16-32
+// images per rank (the 8-GPU strong-scaling share of the global batch 128) the
+// bs128-tuned tiles left 12-32 workgroups per stage-3/2 wgrad, ~10 us each, and the
+// side stream became the backward's critical path.
+static int wgd_target() { return (int)tune(T_WGD_TARGET); }
 
 // smallest pixel tile instantiated per channel count
 static int wgd_min_bmp(int C) { return C == 16 ? 128 : 64; }
@@ -244,27 +221,16 @@ static int wgd_taps(const ConvGeom& g, int bmp) {
 
 // Pixels per split of the direct kernel for this conv, 0 if not covered.
 int wgrad_direct_bmp(const ConvGeom& g) {
-  if (g_wgd_enabled < 0) {
-    const char* e = std::getenv("DTR_DIRECT_WGRAD");
-    g_wgd_enabled = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  if (!g_wgd_enabled) return 0;
+  if (!tune(T_DIRECT_WGRAD)) return 0;
   if (g.kh != 3 || g.kw != 3 || g.stride != 1 || g.pad != 1 || g.C != g.K || g.H != g.W ||
       g.Ho != g.H || g.Wo != g.W)
     return 0;
   // pixels per split (= per workgroup): larger -> fewer split-K slabs for the grouped
-  // reduce to read, fewer workgroups.  DTR_WGD_BMP="c16,c32,c64" overrides (sweeps).
-  static int bm16 = -1, bm32 = -1, bm64 = -1;
-  if (bm16 < 0) {
-    // measured (CIFAR RN50 step, bs128): 256/256/128 -> 512/512/256 = 1.396 -> 1.320 ms
-    // (the grouped reduce reads half the slabs; the side stream has the slack)
-    bm16 = 512, bm32 = 512, bm64 = 256;
-    if (const char* e = std::getenv("DTR_WGD_BMP")) std::sscanf(e, "%d,%d,%d", &bm16, &bm32, &bm64);
-  }
+  // reduce to read, fewer workgroups (tune wgd_bmp16 / 32 / 64)
   int bmp = 0;
-  if (g.C == 16 && g.W == 32) bmp = bm16;
-  else if (g.C == 32 && g.W == 16) bmp = bm32;
-  else if (g.C == 64 && g.W == 8) bmp = bm64;
+  if (g.C == 16 && g.W == 32) bmp = (int)tune(T_WGD_BMP16);
+  else if (g.C == 32 && g.W == 16) bmp = (int)tune(T_WGD_BMP32);
+  else if (g.C == 64 && g.W == 8) bmp = (int)tune(T_WGD_BMP64);
   const long P = (long)g.N * g.H * g.W;
   const int lo = wgd_min_bmp(g.C);               // smallest instantiated tile
   const int hi = g.C == 16 ? 1024 : g.C == 32 ? 512 : 256;
@@ -276,40 +242,29 @@ int wgrad_direct_bmp(const ConvGeom& g) {
   return bmp;
 }
 
-static bool wgd_dispatch(const WgradArgs& a, hipStream_t s, const WgradGroup& grp) {
+bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) {
   const int bmp = wgrad_direct_bmp(a.g);
   if (bmp == 0 || a.px_per_split != bmp) return false;
   const ConvGeom& g = a.g;
   const int tj = wgd_taps(g, bmp);
   if (g.C == 16) {
-    if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s, grp);
-    else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s, grp);
-    else if (bmp == 256) wgd_launch<16, 32, 32, 256, 9>(a, s, grp);
-    else wgd_launch<16, 32, 32, 128, 9>(a, s, grp);
+    if (bmp == 1024) wgd_launch<16, 32, 32, 1024, 9>(a, s);
+    else if (bmp == 512) wgd_launch<16, 32, 32, 512, 9>(a, s);
+    else if (bmp == 256) wgd_launch<16, 32, 32, 256, 9>(a, s);
+    else wgd_launch<16, 32, 32, 128, 9>(a, s);
   } else if (g.C == 32) {
-    if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s, grp);
-    else if (bmp == 256) wgd_launch<32, 16, 16, 256, 3>(a, s, grp);
-    else if (bmp == 128) wgd_launch<32, 16, 16, 128, 3>(a, s, grp);
-    else if (tj == 3) wgd_launch<32, 16, 16, 64, 3>(a, s, grp);
-    else wgd_launch<32, 16, 16, 64, 1>(a, s, grp);
+    if (bmp == 512) wgd_launch<32, 16, 16, 512, 3>(a, s);
+    else if (bmp == 256) wgd_launch<32, 16, 16, 256, 3>(a, s);
+    else if (bmp == 128) wgd_launch<32, 16, 16, 128, 3>(a, s);
+    else if (tj == 3) wgd_launch<32, 16, 16, 64, 3>(a, s);
+    else wgd_launch<32, 16, 16, 64, 1>(a, s);
   } else {
-    if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s, grp);
-    else if (bmp == 128) wgd_launch<64, 8, 8, 128, 3>(a, s, grp);
-    else if (tj == 3) wgd_launch<64, 8, 8, 64, 3>(a, s, grp);
-    else wgd_launch<64, 8, 8, 64, 1>(a, s, grp);
+    if (bmp == 256) wgd_launch<64, 8, 8, 256, 3>(a, s);
+    else if (bmp == 128) wgd_launch<64, 8, 8, 128, 3>(a, s);
+    else if (tj == 3) wgd_launch<64, 8, 8, 64, 3>(a, s);
+    else wgd_launch<64, 8, 8, 64, 1>(a, s);
   }
   return true;
-}
-
-bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s) { return wgd_dispatch(a, s, WgradGroup{}); }
-
-// All members share a's geometry and split layout and either all or none carry the
-// fused BN+ReLU of x (the PRE template flag comes from a.pre_scale).
-bool conv_wgrad_direct_group(const WgradArgs& a, const WgradGroup& grp, hipStream_t s) {
-  if (grp.n < 1 || grp.n > WGRAD_GROUP_MAX) return false;
-  for (int i = 0; i < grp.n; ++i)
-    if ((grp.scale[i] != nullptr) != (a.pre_scale != nullptr)) return false;
-  return wgd_dispatch(a, s, grp);
 }
 
 }  // namespace dtr

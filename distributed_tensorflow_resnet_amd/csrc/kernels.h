@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tune.h"
+
 namespace dtr {
 
 typedef __bf16 bf16;
@@ -126,9 +128,8 @@ struct GemmArgs {
   int accumulate;           // out += result
   ConvGeom g;
   int M, Ncol, Kdim;
-  int swz = 0;              // conv_gemm: XCD-grouped tile order (set by the launcher)
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
-  int wt = 0;                   // epilogue output stores write-through (sc1): DTR_WT_STORE
+  int wt = 0;                   // epilogue output stores write-through (sc1): tune wt_store
   // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
   // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
   // (sk_cnt) sums the slices in slice order and runs the epilogue
@@ -149,14 +150,11 @@ void set_conv_parity(int enabled);      // stride-2 dgrads by output parity clas
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.
 bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
-bool conv_gemm_abwd_covers(const GemmArgs& a);   // generic dgrad with the fused BN backward
 void set_direct_probe(long long* p);   // per-workgroup phase stamps of the direct conv (diag)
 void plan_delay(long long ticks, hipStream_t s);   // spin one wave for ticks x 10 ns (diag.hip)
 void set_conv_direct(int enabled);
-void set_conv_wide_tile(int mask);     // 128x64 tiles for > 64 output columns (experiment)
-void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM loops (DTR_CONV_PIPE)
-void set_wgrad_pipeline(int enabled);  // (the wgrad half of it)
-void set_fin_version(int v);   // BN finalize kernel variant (DTR_FIN_V)
+void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM / wgrad loops (tune conv_pipe)
+void set_fin_version(int v);   // BN finalize kernel variant (tune fin_v)
 int conv_gemm_bm(int M, int Ncol);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 
@@ -169,23 +167,11 @@ struct WgradArgs {
   ConvGeom g;
   int splits;
   int px_per_split;         // multiple of 64
-  int wt = 0;               // direct kernel: partials stored write-through (set by the launcher)
+  int wt = 0;               // partials stored write-through (direct kernel; set by the launcher)
 };
 void conv_wgrad(const WgradArgs& a, hipStream_t s);
 // Direct halo-tiled wgrad for 3x3/s1 small C (conv_wgrad_direct.hip).
 bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s);
-// Several same-shape direct wgrads in ONE launch (blockIdx.z = member): the
-// operands of member z replace a's dy / x / pre_scale / pre_shift / part.
-constexpr int WGRAD_GROUP_MAX = 8;
-struct WgradGroup {
-  int n = 0;
-  const bf16* dy[WGRAD_GROUP_MAX];
-  const bf16* x[WGRAD_GROUP_MAX];
-  const float* scale[WGRAD_GROUP_MAX];
-  const float* shift[WGRAD_GROUP_MAX];
-  float* part[WGRAD_GROUP_MAX];
-};
-bool conv_wgrad_direct_group(const WgradArgs& a, const WgradGroup& grp, hipStream_t s);
 int wgrad_direct_bmp(const ConvGeom& g);   // pixels per split, 0 = not covered
 void set_wgrad_direct(int enabled);
 // grad[tap][ci][co] (+)= scale * sum_s part[s][co][tap*C+ci] for co < K_valid, ci < C_valid

@@ -1,0 +1,107 @@
+// Tuning registry (see tune.h).  Every default below was chosen by measurement on
+// MI355X; the doc string names the measurement (profiles/, README "Tuning").
+#include "tune.h"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+namespace dtr {
+
+namespace {
+
+const TuneEntry kTable[T_COUNT] = {
+    {"conv_pipe", 1,
+     "2-deep pipelined (FAST) implicit-GEMM / wgrad loops where they pay: K loops >= 4 tiles, "
+     "fwd >= 128 output channels, dgrad >= 16k rows (1.02-1.24x on the ImageNet shapes)"},
+    {"splitk", 2,
+     "max split-K slices of FAST grids with <= splitk_tiles tiles (the 7x7 stage: 196 tiles "
+     "for 256 CUs)"},
+    {"splitk_tiles", 256,
+     "largest grid (tiles) that is split; splitting the 392-tile 14x14 grids measured slower "
+     "(ImageNet step 12.93 -> 13.24 ms)"},
+    {"dgrad_splitk", 1, "the 7x7 dgrads take the FAST loop once split-K doubles their grid"},
+    {"nbuf1_kt", 1,
+     "single-buffered LDS for K loops of <= this many 64-wide tiles: the 64-channel 1x1 convs "
+     "fit 4 workgroups per CU instead of 2"},
+    {"smallc_bm16", 256, "tile rows of the large-M 16-column convs (CIFAR stage 1 at 128 images)"},
+    {"smallc_bm32", 128, "tile rows of the large-M 32-column convs (CIFAR stage 2)"},
+    {"c16_mid", 32768,
+     "rows from which mid-size 16-column grids use 128-row tiles (CIFAR RN50 bs64 1.233 -> "
+     "1.08 ms)"},
+    {"c32_mid", 32768, "likewise for 32 columns (CIFAR RN50 bs128 1.303 -> 1.273 ms)"},
+    {"bm128_min", 4096,
+     "rows from which >= 128-column convs use 128x128 tiles (7x7 fwd 118 -> 87 us)"},
+    {"parity_dgrad", 1,
+     "stride-2 dgrads as 4 output-parity classes of dense implicit GEMMs (3-3.5x faster than "
+     "masked taps)"},
+    {"direct_conv", 1, "direct halo 3x3 conv kernel for the CIFAR shapes (16@32, 32@16, 64@8)"},
+    {"direct_splitn", -1,
+     "column-split mask of the direct conv (bit 0: 32 ch, 1: 64 ch in 2, 2: 64 ch in 4); -1 "
+     "auto by grid size"},
+    {"direct_ldsw", 4,
+     "direct conv weights staged through LDS, mask (1: 16 ch, 2: 32, 4: 64); C64 only: bs16 "
+     "step 0.978 -> 0.955 ms"},
+    {"direct_wgrad", 1, "direct halo wgrad for the CIFAR 3x3 shapes"},
+    {"wgd_wt", 1,
+     "direct wgrad split partials stored write-through (bs128 step 1.315 -> 1.302 ms)"},
+    {"wgd_target", 96,
+     "workgroups the direct wgrad launches at least (small per-rank batches shrink its tiles)"},
+    {"wgd_bmp16", 512, "direct wgrad pixels per split, 16 channels (256 -> 512: 1.396 -> 1.320 ms)"},
+    {"wgd_bmp32", 512, "... 32 channels"},
+    {"wgd_bmp64", 256, "... 64 channels"},
+    {"wgrad_target_wg", 768,
+     "split-K wgrad: target workgroups (3 per CU hide the per-tile load latency)"},
+    {"wgrad_slab_mb", 32, "split-K wgrad: cap of one layer's fp32 partial slabs, MB"},
+    {"fin_v", 1,
+     "BN finalize variant: 1 auto (per-channel one-round kernel for many partials), 0 LDS "
+     "tree, 2 one-round"},
+    {"bwd_apply_fin", 1,
+     "BN backward apply finalizes in-kernel: 0 only C <= 64, 1 when the redundant reads stay "
+     "<= 1/4 of the streamed bytes, 2 always"},
+    {"wt_store", -1,
+     "conv epilogue write-through stores: -1 auto (direct convs writing >= 2 MB: bs128 step "
+     "1.304 -> 1.282 ms), 0 off, 1 on"},
+};
+
+std::atomic<long> g_val[T_COUNT];
+std::once_flag g_once;
+
+void load() {
+  for (int i = 0; i < T_COUNT; ++i) g_val[i].store(kTable[i].dflt);
+  const char* env = std::getenv("DTR_TUNE");
+  if (!env) return;
+  std::string s(env);
+  size_t p = 0;
+  while (p < s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    const std::string item = s.substr(p, q - p);
+    const size_t eq = item.find('=');
+    if (eq != std::string::npos) {
+      const std::string k = item.substr(0, eq);
+      for (int i = 0; i < T_COUNT; ++i)
+        if (k == kTable[i].key) g_val[i].store(std::strtol(item.c_str() + eq + 1, nullptr, 10));
+      // keys of the Python engine (utils/tune.py) are validated there
+    }
+    p = q + 1;
+  }
+}
+
+}  // namespace
+
+long tune(TuneId id) {
+  std::call_once(g_once, load);
+  return g_val[id].load(std::memory_order_relaxed);
+}
+
+void tune_set(TuneId id, long v) {
+  std::call_once(g_once, load);
+  g_val[id].store(v);
+}
+
+const TuneEntry* tune_table() { return kTable; }
+
+}  // namespace dtr

@@ -126,9 +126,7 @@ def conv2d_dgrad(dy, w_hwio, x_shape, stride: int, *, out=None, accumulate=False
     BN+ReLU backward partials of dx (per tile: sum g, sum g*xhat, g = dx*[relu]).
     ``abwd=[x, add, mean, rstd, scale, shift, gamma, part, cnt, a_out, dgamma, dbeta,
     coef]``: ``dy`` is the gradient BEFORE its BatchNorm+ReLU backward, which the kernel
-    applies while staging (writing the result to a_out) -- the direct 3x3 kernel, or the
-    implicit-GEMM loop when ``conv_gemm_abwd_covers`` (no add, cnt 0: coefficients from
-    bn_bwd_finalize)."""
+    applies while staging (writing the result to a_out) -- direct 3x3 kernel only."""
     _check(dy, BF16, 4, "dy")
     _check(w_hwio, BF16, 4, "w_hwio")
     N, H, W, C = x_shape

@@ -41,6 +41,7 @@ from .. import native
 from ..models.params import ParamStore
 from ..models.spec import BNSpec, ConvSpec, ModelSpec
 from ..parallel.buckets import assign_buckets, schedule_buckets
+from ..utils import tune
 from ..utils.streamcheck import check_plan
 
 BF16 = torch.bfloat16
@@ -132,9 +133,7 @@ class _BN:
     pending: tuple = None
     names: tuple = ()
     part: torch.Tensor = None     # this BN's forward tile partials [T][2][C]
-    gpart: torch.Tensor = None    # level-1 group partials [groups][2][C]
-    bpart: torch.Tensor = None    # backward partial sums [T][2][C] and their groups
-    bgpart: torch.Tensor = None
+    bpart: torch.Tensor = None    # backward partial sums [T][2][C]
     acc: torch.Tensor = None      # accumulator mode: fp64 [REP][2][C] sum y, sum y^2
     bacc: torch.Tensor = None     # ... and sum g, sum g*xhat (zeroed once per step)
 
@@ -161,6 +160,7 @@ class Engine:
                  use_graph: bool = False, data_seed: int = 1234, fork_wgrad: bool | None = None,
                  allreduce_dtype: str = "fp32", native_comm: bool | None = None, comm=None):
         self.nat = native(required=True)
+        tune.validate(k for k, *_ in self.nat.tune_table())
         self.spec = spec
         self.N = batch_size
         self.device = torch.device(device or "cuda")
@@ -181,20 +181,11 @@ class Engine:
         if fork_wgrad is None:
             # measured: eager + forked wgrad stream beats hipGraph replay (which
             # handles the cross-stream event edges poorly); graphs stay single-stream
-            fork_wgrad = os.environ.get("DTR_FORK_WGRAD", "0" if use_graph else "1") != "0"
-        # residual blocks per side-stream fork.  Measured with the tail split and the
-        # tail reduces on main (ms/step, every 2 / 4 / 8): CIFAR bs16 0.959 / 0.948 /
-        # 1.012, bs128 1.301 / 1.299 / 1.350; ImageNet RN50 12.81 / 12.91 (2 / 4)
-        self.fork_every = max(1, int(os.environ.get(
-            "DTR_FORK_EVERY", "4" if spec.dataset.startswith("cifar") else "2")))
-        # same-shape weight gradients per grouped launch (_emit_wgrads; 1 = ungrouped).
-        # Default 1, measured (CIFAR RN50 step, ms): bs16 0.958 ungrouped vs 0.987 / 0.978
-        # / 0.983 grouping 2 / 8 stage-1 only / 8 all; bs128 1.298 vs 1.296-1.306.  The
-        # grouped launch does shorten the side stream's tail (4 layers in one 5-7 us
-        # kernel), but its 4x wider grids delay the main stream's critical dgrads.
-        self.wgrad_group = min(8, max(1, int(os.environ.get("DTR_WGRAD_GROUP", "1"))))
-        # which input-channel counts group (bit 0: 16, 1: 32, 2: 64, 3: others; -1 all)
-        self.wgrad_group_cmask = int(os.environ.get("DTR_WGRAD_GROUP_C", "-1"))
+            fw = tune.get("fork_wgrad")
+            fork_wgrad = (not use_graph) if fw < 0 else bool(fw)
+        # residual blocks per side-stream fork (tune fork_every)
+        fe = tune.get("fork_every")
+        self.fork_every = max(1, fe if fe > 0 else (4 if spec.dataset.startswith("cifar") else 2))
         # Backward tail: the weight gradients still queued for the side stream when the
         # main stream's dgrad chain ends (the first stage's) are shared out -- this
         # fraction of them, the last-queued ones, runs on the otherwise idle main stream
@@ -202,14 +193,10 @@ class Engine:
         # ms/step, 0 / 0.5 / 0.75 / 1): bs16 0.978 / 0.972 / 0.972 / 0.970, bs32 1.002 /
         # 0.994 / 1.017 / 1.011, bs64 1.128 / 1.131 / 1.131 / 1.130, bs128 1.326 / 1.316 /
         # 1.314 / 1.303 (scripts/ab_tail.sh)
-        self.tail_main = min(1.0, max(0.0, float(os.environ.get("DTR_TAIL_MAIN", "1"))))
+        self.tail_main = min(1.0, max(0.0, tune.get("tail_main")))
         # ...and the last reduces then run on the main stream behind one join
-        # (DTR_REDUCE_MAIN_TAIL=0: forked to the side stream like the earlier buckets)
-        self.reduce_main_tail = os.environ.get("DTR_REDUCE_MAIN_TAIL", "1") != "0"
-        # ...and its same-shape weight gradients go out grouped, up to this many per launch
-        # (measured neutral, ms/step 1 vs 8: bs16 0.947 / 0.946 vs 0.945 / 0.952, bs32 0.988 /
-        # 0.984 vs 0.983 / 0.965, bs128 1.294 / 1.286 vs 1.289 / 1.290: off)
-        self.tail_group = min(8, max(1, int(os.environ.get("DTR_TAIL_GROUP", "1"))))
+        # (reduce_main_tail=0: forked to the side stream like the earlier buckets)
+        self.reduce_main_tail = bool(tune.get("reduce_main_tail"))
         self.markers = os.environ.get("DTR_ROCTX", "0") != "0"
         self.fork_wgrad = fork_wgrad
         if input_mode == "auto":
@@ -220,7 +207,7 @@ class Engine:
         # ImageNet stem as a space-to-depth 4x4/1 conv over [N, H/2, W/2, 16] (data.hip
         # stem_s2d_*: K 392 -> 256, stride-1 gathers, a 2-tile weight gradient instead of 4)
         st = spec.stem
-        self.stem_s2d = (os.environ.get("DTR_STEM_S2D", "1") != "0" and st.kh == 7 and
+        self.stem_s2d = (bool(tune.get("stem_s2d")) and st.kh == 7 and
                          st.kw == 7 and st.stride == 2 and st.cin <= 3 and
                          spec.image_h % 2 == 0 and spec.image_w % 2 == 0 and
                          2 * st.ho == spec.image_h and 2 * st.wo == spec.image_w)
@@ -282,7 +269,8 @@ class Engine:
             # 0.5 MB groups -2.3 % step time vs one group, whose 78 us reduce of 290 MB
             # of split-K slabs sat alone at the end of backward)
             reduce_mb = min(4.0, 4.0 * self.params.n_train / 2 ** 20 / 6)
-        reduce_mb = float(os.environ.get("DTR_REDUCE_MB", str(reduce_mb)))
+        if tune.get("reduce_mb") > 0:
+            reduce_mb = tune.get("reduce_mb")
         slot_of = {s.name: s for s in self.params.train_slots}
         self.reduce_groups = []
         for lo, hi, names in self.buckets:
@@ -389,9 +377,6 @@ class Engine:
         self.bnbuf = torch.zeros(4 * total_c, device=self.device)
         # last-arriver counters for the in-kernel BN finalize (bump-allocated per fused
         # launch at plan build; the kernels leave them zeroed) + group-partial scratch
-        self.bn_counters = torch.zeros(1 << 18, dtype=torch.int32, device=self.device)
-        self._cnt_next = 0
-        self.bn_gpart = torch.empty(2, 128 * 2 * 2048, device=self.device)
         off = 0
         for b in bn_specs:
             g = ps.slot(f"{b.name}/gamma")
@@ -406,7 +391,6 @@ class Engine:
             e.rstd = self.bnbuf[total_c + off:total_c + off + C]
             e.scale = self.bnbuf[2 * total_c + off:2 * total_c + off + C]
             e.shift = self.bnbuf[3 * total_c + off:3 * total_c + off + C]
-            e.fused_fwd = False
             off += C
             self.bns[b.name] = e
 
@@ -466,19 +450,15 @@ class Engine:
             M = N * b.spec.h * b.spec.w
             bm = min(self.nat.conv_gemm_bm(M, C), self.nat.bn_stats_tile_rows())
             b.part = torch.empty(_ceil(M, bm) * 2 * C, device=dev)
-            b.gpart = torch.empty(max(_ceil(M, bm) // 2, 1) * 2 * C, device=dev)
             tb = max(self.nat.bn_bwd_tiles(M, C), _ceil(M, self.nat.conv_gemm_bm(M, C)))
             b.bpart = torch.empty(tb * 2 * C, device=dev)
-            b.bgpart = torch.empty(max(tb // 2, 1) * 2 * C, device=dev)
-        # Accumulator mode (DTR_BN_ACC, default on): the producing conv's workgroups add
+        # Accumulator mode (tune bn_acc, default on): the producing conv's workgroups add
         # their tile sums into BN_ACC_REP fp64 replicas per BatchNorm with memory-side
         # atomics, and the consumer reads 2 x REP values per channel instead of
         # combining every tile partial in its prologue or a finalize launch (measured on
         # the CIFAR direct convs: ~4 us per consumer prologue at 512 tiles).  All the
         # replicas live in one buffer zeroed by one memset at the start of the step.
-        acc_mode = os.environ.get("DTR_BN_ACC", "1")   # 1 | 0 | fwd | bwd (diagnostics)
-        self.bn_acc_on = acc_mode in ("1", "fwd")
-        self.bn_bacc_on = acc_mode in ("1", "bwd")
+        self.bn_acc_on = self.bn_bacc_on = bool(tune.get("bn_acc"))
         rep = self.nat.bn_acc_rep()
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
         self.bn_acc = torch.zeros(max(_ceil(tot, 2) * 2, 2), dtype=torch.float64, device=dev)
@@ -536,43 +516,16 @@ class Engine:
     def _dense_geom(self, N):
         return [N, 1, 1, self.spec.dense_in, 1, 1, self.kpad, 1, 1, 1, 0]
 
-    def _fuse_finalize(self, M: int, nc: int):
-        """Plan for the in-kernel (last-arriver) BN finalize of a conv producing M x nc:
-        None (separate finalize kernel), 0 (one level: every tile partial combined by the
-        last workgroup) or GS (two levels: groups of GS tiles, then the groups).  Each
-        level must be one round of loads: items <= (256 / BN) * FIN_UNROLL(8)."""
-        if os.environ.get("DTR_FUSED_BN_FINALIZE", "1") == "0":
-            return None
-        bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
-        T, cap = _ceil(M, bm), (256 // bn) * 8
-        if T <= cap:
-            return 0
-        gs = 16
-        if gs <= cap and _ceil(T, gs) <= cap:
-            return gs
-        return None
-
-    def _counters(self, M: int, nc: int, group: int) -> int:
-        """Device address of a fresh zeroed counter block for one fused launch."""
-        bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
-        ny = _ceil(nc, bn)
-        n = ny * (1 + (_ceil(_ceil(M, bm), group) if group else 0))
-        off = self._cnt_next
-        self._cnt_next += _ceil(n, 16) * 16
-        assert self._cnt_next <= self.bn_counters.numel(), "BN counter pool exhausted"
-        return self.bn_counters.data_ptr() + 4 * off
-
     def _consumer_cap(self, C: int) -> int:
         """Max partials a consumer prologue combines (bn_prefin_table / _sums)."""
         return self.nat.pfin_cap(C)
 
     def _conv_fwd(self, plan, c: _Conv, x, out, N, pre: _BN | None = None, residual=None,
                   stats_for: _BN | None = None):
-        """One conv launch.  BatchNorm statistics of the output (``stats_for``) are
-        finalized, in order of preference, by (a) the BN's first consumer's prologue
-        reading the tile partials (few tiles), (b) the same after this kernel's
-        last-arriving workgroups folded groups of tiles, (c) this kernel's last
-        arriver (full), (d) a separate bn_finalize launch."""
+        """One conv launch.  BatchNorm statistics of the output (``stats_for``) go
+        into the BN's fp64 accumulators (bn_acc, default), which its first consumer
+        reads; or, as per-tile partials, are finalized by the first consumer's prologue
+        (few tiles) or else by a separate bn_finalize launch."""
         geom = self._geom(c, N)
         stat_ptr = 0
         fin, pfin = [], []
@@ -592,40 +545,14 @@ class Engine:
             bm, bn = self.nat.conv_gemm_bm(M, nc), self.nat.conv_gemm_bn(M, nc)
             T = _ceil(M, bm)
             stat_ptr = b.part.data_ptr()
-            b.pending, b.fused_fwd = (stat_ptr, T, bm, M), False
-            capc, capp = self._consumer_cap(nc), (256 // bn) * 8
-            # measured (CIFAR bs 128 / 32): "3" (consumer prologue when the tiles are few,
-            # else a separate finalize) beats adding producer-side last arrivers ("1")
-            mode = os.environ.get("DTR_FUSED_BN_FINALIZE", "3")
+            b.pending = (stat_ptr, T, bm, M)
+            # measured (CIFAR bs 128 / 32): the consumer prologue when the tiles are few,
+            # else a separate finalize, beats producer-side last-arriver finalizes
             if self.bn_acc_on:
                 fin = [b.acc.data_ptr()]
                 b.pending = ("acc", b.acc.data_ptr(), M)
-            elif mode == "0":
+            elif T > self._consumer_cap(nc):
                 b.pending = ("separate", stat_ptr, T, bm, M)
-            elif T <= capc:
-                pass                                    # (a)
-            elif capc and mode not in ("2", "3"):
-                gs = 2
-                while _ceil(T, gs) > capc:
-                    gs *= 2
-                if gs <= capp:                          # (b)
-                    fin = [self._counters(M, nc, gs), b.gamma, b.beta, b.mmean, b.mvar,
-                           b.mean.data_ptr(), b.rstd.data_ptr(), b.scale.data_ptr(),
-                           b.shift.data_ptr(), b.gpart.data_ptr(), gs, 1]
-                    b.pending = (b.gpart.data_ptr(), _ceil(T, gs), gs * bm, M)
-                else:
-                    b.pending = ("separate", stat_ptr, T, bm, M)
-            elif mode == "3":
-                b.pending = ("separate", stat_ptr, T, bm, M)
-            else:
-                grp = self._fuse_finalize(M, nc)
-                if grp is not None:                     # (c)
-                    b.fused_fwd, b.pending = True, None
-                    fin = [self._counters(M, nc, grp), b.gamma, b.beta, b.mmean, b.mvar,
-                           b.mean.data_ptr(), b.rstd.data_ptr(), b.scale.data_ptr(),
-                           b.shift.data_ptr(), self.bn_gpart[0].data_ptr(), grp, 0]
-                else:
-                    b.pending = ("separate", stat_ptr, T, bm, M)
         plan.conv_gemm(0, x.data_ptr(), c.ohwi, out.data_ptr(), 0,
                        0 if residual is None else residual.data_ptr(),
                        0 if pre is None else pre.scale.data_ptr(),
@@ -640,8 +567,7 @@ class Engine:
             self._bn_finalize(plan, bn)
             return x, bn
         C = bn.spec.channels
-        if (bn.pending is not None and bn.pending[0] == "acc"
-                and os.environ.get("DTR_FUSED_APPLY_FIN", "1") != "0"):
+        if bn.pending is not None and bn.pending[0] == "acc":
             # the apply pass finalizes too (no bn_finalize launch in between)
             _, part, M = bn.pending
             bn.pending = None
@@ -660,10 +586,10 @@ class Engine:
         output-column tile and, beside the MFMAs of the small 64x64 tiles of the 7x7
         layers, cost more than the MFMAs (3x3 512->512: 66 -> 103 us).  Materializing
         is one streaming pass: a win where the tensor is small and the consumers'
-        column tiles many (DTR_MAT_BN_ELEMS: M*C threshold, 0 = never; DTR_MAT_BN_MINC: min channels)."""
-        lim = int(os.environ.get("DTR_MAT_BN_ELEMS", "7000000"))
-        # measured (RN50 bs128): stages 3-4 (14x14 / 7x7) +1.3 %; adding stage 2 no gain
-        return C >= int(os.environ.get("DTR_MAT_BN_MINC", "256")) and M * C <= lim
+        column tiles many (tune mat_bn_elems: M*C threshold, 0 = never; mat_bn_minc: min
+        channels).  Measured (RN50 bs128): stages 3-4 (14x14 / 7x7) +1.3 %; adding stage 2
+        no gain."""
+        return C >= tune.get("mat_bn_minc") and M * C <= tune.get("mat_bn_elems")
 
     def _bn_finalize(self, plan, bn: _BN, train=True, consumer_conv: bool = True):
         """Called where the BN's statistics are next needed.  Deferred to the first
@@ -707,18 +633,15 @@ class Engine:
         a_src = dy
         pb = self._pending_bwd
         if pb is not None:
-            fuse = pb["out"] is dy and dx is not None and \
-                os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
-            direct = fuse and self.nat.conv_direct_covers(1, geom)
-            # the implicit-GEMM dgrad applies it too (1x1 / strided / ImageNet shapes),
-            # from coefficients finalized by a separate tiny launch
-            gemm = fuse and not direct and self.nat.conv_gemm_abwd_covers(geom,
-                                                                          pb["add"] is not None)
-            if direct or gemm:
+            fuse = pb["out"] is dy and dx is not None
+            # the direct (CIFAR) dgrad applies the pending BN backward while staging dy;
+            # the implicit-GEMM dgrads keep the separate apply (fusing it there repeated
+            # the per-element work per column tile and tap: ImageNet 13.3 -> 17.8 ms)
+            if fuse and self.nat.conv_direct_covers(1, geom):
                 bn = pb["bn"]
                 add = pb["add"]
                 part, cnt = pb["part"], pb["cnt"]
-                if gemm or (cnt != -1 and cnt > self._consumer_cap(s.cout)):
+                if cnt != -1 and cnt > self._consumer_cap(s.cout):
                     # too many partials for the prologue: finalize separately, the
                     # dgrad then reads the coefficients (cnt = 0)
                     plan.bn_bwd_finalize(part, cnt, pb["M"], bn.spec.channels, bn.gamma,
@@ -741,25 +664,13 @@ class Engine:
                 bn, bx = bnb
                 Mx = N * s.h * s.w
                 C = c.cin
-                bm, bnt = self.nat.conv_gemm_bm(Mx, C), self.nat.conv_gemm_bn(Mx, C)
-                T = _ceil(Mx, bm)
+                T = _ceil(Mx, self.nat.conv_gemm_bm(Mx, C))
                 bl = [bx.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
                       bn.shift.data_ptr(), bn.bpart.data_ptr()]
                 self._bnb_src = (bn.bpart.data_ptr(), T)
-                capc, capp = self._consumer_cap(C), (256 // bnt) * 8
                 if self.bn_bacc_on:
                     bfl = [bn.bacc.data_ptr()]
                     self._bnb_src = (bn.bacc.data_ptr(), -1)
-                elif (T > capc and capc and os.environ.get("DTR_FUSED_BN_APPLY", "1") != "0"
-                        and os.environ.get("DTR_BWD_GROUPS", "0") == "1"):
-                    gs = 2
-                    while _ceil(T, gs) > capc:
-                        gs *= 2
-                    if gs <= capp:   # last arrivers fold groups of gs tiles for the consumer
-                        bfl = [self._counters(Mx, C, gs), bn.gamma, bn.rstd.data_ptr(),
-                               bn.dgamma, bn.dbeta, self.coef.data_ptr(),
-                               bn.bgpart.data_ptr(), gs, 1]
-                        self._bnb_src = (bn.bgpart.data_ptr(), _ceil(T, gs))
             if "dgrad" not in _DIAG_SKIP:
                 plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0,
                                0, int(accumulate), geom, bl, [], bfl, [], abw, BN_DECAY, BN_EPS,
@@ -866,67 +777,14 @@ class Engine:
             self._side_blocks = 0
         return q[k:]
 
-    def _wgrad_matpre(self, geom) -> bool:
-        """Materialize the BN+ReLU of a wgrad's input first (DTR_WGRAD_MATPRE=1): 3x3
-        convs on the generic split-K kernel only (the direct CIFAR kernel stages a halo
-        and applies it once per element already).  Off by default: it removes the 9x
-        VALU of the im2col staging (those wgrads issue ~19 VALU per MFMA), but the
-        extra read + write pass cost more on the shared HBM (ImageNet RN50 13.05 ->
-        13.10 ms)."""
-        if os.environ.get("DTR_WGRAD_MATPRE", "0") != "1":
-            return False
-        return geom[7] * geom[8] > 1 and self.nat.wgrad_direct_bmp(list(geom)) == 0
-
-    def _matpre_buf(self, geom):
-        """Scratch relu(bn(x)) tensor for a materialized wgrad input: one per shape,
-        reused by every such wgrad on the stream that issues them in order."""
-        n = geom[0] * geom[1] * geom[2] * geom[3]
-        bufs = self.__dict__.setdefault("_matpre_bufs", {})
-        if n not in bufs:
-            bufs[n] = torch.empty(n, dtype=BF16, device=self.device)
-        return bufs[n].data_ptr()
-
     def _emit_wgrads(self, plan, descs):
-        """Weight-gradient launches on the current stream.  Runs of same-shape layers
-        (the residual blocks of a stage, queued together by _flush_side) go out as
-        ONE grouped launch (`conv_wgrad_group`, up to `wgrad_group` members): at 16-32
-        images per rank a CIFAR wgrad is a 4-6 us kernel, and its launch boundary cost
-        as much again on the side stream, which then trailed the backward pass."""
-        i = 0
-        while i < len(descs):
-            if callable(descs[i]):   # a queued non-wgrad side op (head reduce, dense wgrad)
-                descs[i]()
-                i += 1
-                continue
-            if "wgrad" in _DIAG_SKIP:   # diagnostics only (scripts/diag_step.py)
-                i += 1
-                continue
-            key = descs[i][5:] + (descs[i][2] != 0,)
-            j = i + 1
-            while (j < len(descs) and j - i < self.wgrad_group and not callable(descs[j])
-                   and descs[j][5:] + (descs[j][2] != 0,) == key):
-                j += 1
-            if self.wgrad_group_cmask >= 0 and not (
-                    self.wgrad_group_cmask >> {16: 0, 32: 1, 64: 2}.get(descs[i][5][3], 3) & 1):
-                j = i + 1   # this channel count stays ungrouped (DTR_WGRAD_GROUP_C)
-            run = descs[i:j]
-            geom, sp, pps = list(run[0][5]), run[0][6], run[0][7]
-            if len(run) == 1:
-                d = run[0]
-                x, sc, sh = d[1], d[2], d[3]
-                if sc and self._wgrad_matpre(geom):
-                    # relu(bn(x)) once into a scratch tensor, then a plain wgrad: the
-                    # generic kernel's im2col staging otherwise applies the BN+ReLU to
-                    # every element once per filter tap (9x VALU on the 3x3 convs)
-                    x = self._matpre_buf(geom)
-                    plan.bn_relu_apply(d[1], sc, sh, x, geom[0] * geom[1] * geom[2], geom[3])
-                    sc = sh = 0
-                plan.conv_wgrad(d[0], x, sc, sh, d[4], geom, sp, pps)
-            else:
-                plan.conv_wgrad_group([d[0] for d in run], [d[1] for d in run],
-                                      [d[2] for d in run], [d[3] for d in run],
-                                      [d[4] for d in run], geom, sp, pps)
-            i = j
+        """Weight-gradient launches on the current stream, in queue order (queued
+        non-wgrad side ops -- the head's batch folds, the dense wgrad -- are callables)."""
+        for d in descs:
+            if callable(d):
+                d()
+            elif "wgrad" not in _DIAG_SKIP:   # (diagnostics only: scripts/diag_step.py)
+                plan.conv_wgrad(d[0], d[1], d[2], d[3], d[4], list(d[5]), d[6], d[7])
 
     def _flush_buckets(self, plan, force: bool = False):
         """Emit the grouped split-K reduce of every reduce group whose gradients are
@@ -1022,9 +880,7 @@ class Engine:
         plan, spec, N = self.plan, self.spec, self.N
         self.seg = {}
         for e in self.bns.values():
-            e.fused_fwd = False
             e.pending = None
-        self._cnt_next = 0
         self._n_allreduce, self._allreduce_bytes = 0, 0
         b0 = plan.size()
         self._t_fwd0 = plan.timing_point("fwd_begin")
@@ -1098,8 +954,7 @@ class Engine:
         # sums (head_fused, head.hip) instead of 8 dependent launches; the batch folds
         # (loss, precision, dbias) and the dense wgrad go to the side stream.
         self._head_fused = (self.bn_acc_on and self.bn_bacc_on and fbn.pending is not None
-                            and fbn.pending[0] == "acc"
-                            and os.environ.get("DTR_FUSED_HEAD", "1") != "0"
+                            and fbn.pending[0] == "acc" and bool(tune.get("fused_head"))
                             and self.nat.head_fused_supported(N, HL * WL, F, spec.num_classes,
                                                               self.kpad))
         self._dact = self._g(0, (N, HL, WL, F))
@@ -1229,18 +1084,7 @@ class Engine:
         # left for it), running alongside the side stream's last weight gradients.
         self._conv_bwd(plan, stem, dstem_src, self.x_in, N, None, side=False)
         if main_tail:   # the main stream's share of the tail; the reduces fork after it
-            if self.tail_group > 1:
-                # nothing else runs now: same-shape layers side by side, one grouped
-                # launch per shape (conv_wgrad_group, bitwise equal to per-layer)
-                ops = [d for d in main_tail if callable(d)]
-                key = lambda d: (d[5:], d[2] != 0)  # noqa: E731
-                main_tail = ops + sorted((d for d in main_tail if not callable(d)), key=key)
-                g0, self.wgrad_group, cm = self.wgrad_group, self.tail_group, self.wgrad_group_cmask
-                self.wgrad_group_cmask = -1
-                self._emit_wgrads(plan, main_tail)
-                self.wgrad_group, self.wgrad_group_cmask = g0, cm
-            else:
-                self._emit_wgrads(plan, main_tail)
+            self._emit_wgrads(plan, main_tail)
             self._main_wgrad = True
         if self._split_tail_on() and self.reduce_main_tail:
             # the remaining reduces run on the main stream after ONE join of the side

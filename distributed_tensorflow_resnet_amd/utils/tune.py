@@ -1,0 +1,66 @@
+"""Tuning entries of the training engine (plan schedule and fusion choices).
+
+One environment variable carries every tuning override of the framework,
+Python engine and native kernels alike:
+
+    DTR_TUNE="fork_every=2,splitk=1"
+
+The engine keys are below (read when an Engine is built); the native keys
+(tile shapes, split-K, kernel variants) live in csrc/tune.h / tune.cpp, read
+once per process (tests flip those with ``_C.tune_set``).  An unknown key is an
+error.  README.md "Tuning" lists every key with its default; the CPU test
+tests/test_tune_cpu.py checks that the list, the tables and the code agree.
+"""
+from __future__ import annotations
+
+import os
+
+# key: (default, meaning + the measurement behind the default)
+ENGINE = {
+    "fork_wgrad": (-1, "weight gradients on the side stream: 1 on, 0 all on the main stream, "
+                       "-1 auto (on eagerly; off under hipGraph capture, which replays the "
+                       "cross-stream event edges poorly)"),
+    "fork_every": (-1, "residual blocks per side-stream fork, -1 auto: 4 CIFAR (bs16 0.948 vs "
+                       "0.959 / 1.012 ms at 2 / 8), 2 ImageNet (12.81 vs 12.91 ms at 4)"),
+    "tail_main": (1.0, "fraction of the backward tail's queued weight gradients run on the idle "
+                       "main stream after the stem (CIFAR bs128 1.326 -> 1.303 ms at 0 -> 1)"),
+    "reduce_main_tail": (1, "the last split-K reduces run on the main stream behind one join"),
+    "reduce_mb": (-1.0, "split-K reduce group size in MB, -1 auto (~6 groups, <= 4 MB: CIFAR "
+                        "RN50 -2.3 % step vs one group)"),
+    "stem_s2d": (1, "ImageNet 7x7/2 stem as a space-to-depth 4x4/1 conv (K 392 -> 256)"),
+    "bn_acc": (1, "BatchNorm sums as fp64 atomic accumulators (1) instead of per-tile "
+                  "partials combined by the consumer or a finalize launch (0)"),
+    "fused_head": (1, "CIFAR head in one launch (final BN finalize .. final BN backward "
+                      "sums) instead of eight"),
+    "mat_bn_elems": (7000000, "inner bottleneck BN-ReLU materialized once (instead of applied in "
+                              "the consumer's staging) up to this many elements ..."),
+    "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
+}
+
+
+def overrides() -> dict:
+    """The DTR_TUNE entries as {key: string value}."""
+    out = {}
+    for item in filter(None, os.environ.get("DTR_TUNE", "").split(",")):
+        k, sep, v = item.partition("=")
+        if not sep:
+            raise ValueError(f"DTR_TUNE entry {item!r} is not key=value")
+        out[k.strip()] = v.strip()
+    return out
+
+
+def validate(native_keys=()) -> None:
+    """Every DTR_TUNE key must be an engine or a native tuning key."""
+    known = set(ENGINE) | set(native_keys)
+    bad = sorted(set(overrides()) - known)
+    if bad:
+        raise ValueError(f"unknown DTR_TUNE key(s) {bad}; known: {sorted(known)}")
+
+
+def get(key: str):
+    """Current value of an engine key (its default's type)."""
+    default = ENGINE[key][0]
+    v = overrides().get(key)
+    if v is None:
+        return default
+    return type(default)(float(v)) if isinstance(default, int) else type(default)(v)

@@ -45,7 +45,7 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = 10
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
-    knob = os.environ.get("AB_KNOB", "pipe")   # pipe: FAST loop off/on; wide: 128x128/128x64
+    knob = os.environ.get("AB_KNOB", "pipe")   # pipe: FAST loop off/on; fuse: epilogue fusions
     only = os.environ.get("AB_SHAPES")   # e.g. "56,256,64,1,1;28,128,128,3,1"
     shapes = [tuple(int(v) for v in t.split(",")) for t in only.split(";")] if only else SHAPES
     for H, C, K, k, s in shapes:
@@ -88,14 +88,10 @@ def main():
                                     ("wgrad", pw)):
                         ts[(p, v)].append(dev_time(plan))
                     continue
-                if knob == "wide":
-                    nat.set_conv_wide_tile(3 * v)
-                else:
-                    nat.set_conv_pipeline(v)
+                nat.set_conv_pipeline(v)
                 for p, plan in passes:
                     ts[(p, v)].append(dev_time(plan))
         nat.set_conv_pipeline(1)
-        nat.set_conv_wide_tile(0)
         line = []
         for p, _ in passes:
             a, b = statistics.median(ts[(p, 0)]), statistics.median(ts[(p, 1)])

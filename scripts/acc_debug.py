@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Compare the engine with BN accumulator mode on/off (DTR_BN_ACC): per-BN forward
+"""Compare the engine with BN accumulator mode on/off (tune bn_acc): per-BN forward
 statistics after the forward segment, per-tensor gradients after the backward."""
 import os
 import sys
@@ -12,7 +12,7 @@ from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_sche
 
 
 def run(acc, size, N):
-    os.environ["DTR_BN_ACC"] = acc
+    os.environ["DTR_TUNE"] = f"bn_acc={acc}"
     spec = cifar_spec(size) if size < 0 or size % 6 == 2 else imagenet_spec(size, image_hw=64)
     dev = torch.device("cuda", 0)
     eng = Engine(spec, N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=dev,

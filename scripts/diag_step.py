@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase timing (HIP events) of the CIFAR training step: forward, backward,
-optimizer -- averaged over 100 steps.  Combine with DTR_DIAG_SKIP / DTR_FORK_WGRAD
+optimizer -- averaged over 100 steps.  Combine with DTR_DIAG_SKIP / DTR_TUNE=fork_wgrad=0
 to find the critical path (timing only: skipped launches make the math wrong)."""
 import os
 import sys

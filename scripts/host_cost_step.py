@@ -16,7 +16,7 @@ def main():
     dev = torch.device("cuda", 0)
     for batch in (128, 32):
         for fork in ("1", "0"):
-            os.environ["DTR_FORK_WGRAD"] = fork
+            os.environ["DTR_TUNE"] = f"fork_wgrad={fork}"
             eng = Engine(build_spec("cifar10", 50), batch, weight_decay=2e-4,
                          lr_schedule=cifar_lr_schedule(), device=dev)
             eng.fill_synthetic(0)

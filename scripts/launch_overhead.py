@@ -27,7 +27,7 @@ def main():
     batch = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     dev = torch.device("cuda", 0)
     for graph, fork in ((False, True), (False, False), (True, False), (True, True)):
-        os.environ["DTR_FORK_WGRAD"] = "1" if fork else "0"
+        os.environ["DTR_TUNE"] = f"fork_wgrad={int(bool(fork))}"
         eng = Engine(build_spec("cifar10", 50), batch, weight_decay=2e-4,
                      lr_schedule=cifar_lr_schedule(), device=dev, use_graph=graph)
         eng.fill_synthetic(0)

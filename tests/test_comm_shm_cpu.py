@@ -49,7 +49,8 @@ def _worker(kind, name, world, rank, n, dtype, slot, q, extra):
         nat = _nat()
         code = {"f32": nat.COMM_F32, "f64": nat.COMM_F64, "bf16": nat.COMM_BF16}[dtype]
         timeout = extra.get("timeout", 30.0)
-        comm = nat.Comm.shm(name, world, rank, -1, slot_bytes=slot, timeout_s=timeout)
+        comm = nat.Comm.shm(name, world, rank, -1, slot_bytes=slot, timeout_s=timeout,
+                            init_timeout_s=120.0)
         assert comm.transport == "shm" and comm.world == world and comm.rank == rank
         if kind == "sum":
             x = _data(rank, n, dtype)

@@ -42,10 +42,10 @@ def test_dp_gradients_equal_sum_of_local_and_replicas_stay_identical(gpu):
 
 @pytest.mark.gpu
 def test_dp_reduce_groups_nested_in_buckets(gpu):
-    # split-K reduce groups (DTR_REDUCE_MB) smaller than the all-reduce buckets:
+    # split-K reduce groups (tune reduce_mb) smaller than the all-reduce buckets:
     # several grouped reduces per bucket, the bucket joined after its last one
     r = _torchrun(["scripts/dp_check.py"], 29713,
-                  extra_env={"DTR_REDUCE_MB": "0.05", "DP_CHECK_BUCKET_MB": "0.5"})
+                  extra_env={"DTR_TUNE": "reduce_mb=0.05", "DP_CHECK_BUCKET_MB": "0.5"})
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     assert "DP_CHECK_OK" in r.stdout, r.stdout[-3000:]
 

@@ -171,13 +171,13 @@ def test_eval_plan_matches_autograd_eval(gpu):
 
 
 def test_bn_accumulator_mode_matches_partials(gpu, monkeypatch):
-    """DTR_BN_ACC=1 (fp64 atomic accumulators per BatchNorm) vs the per-tile partial
+    """tune bn_acc=1 (fp64 atomic accumulators per BatchNorm) vs the per-tile partial
     path: same loss, gradients and BN statistics up to rounding (shallow net; deep
     nets are chaotic under bf16 and covered by the oracle tests above)."""
     spec = cifar_spec(8)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DTR_BN_ACC", mode)
+        monkeypatch.setenv("DTR_TUNE", f"bn_acc={mode}")
         eng, _, _, _ = _make(spec, 64, gpu)
         st = torch.cuda.current_stream().cuda_stream
         eng._run("fwd", st)
@@ -196,7 +196,7 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
     spec = cifar_spec(8)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DTR_FUSED_HEAD", mode)
+        monkeypatch.setenv("DTR_TUNE", f"fused_head={mode}")
         eng, _, _, _ = _make(spec, 64, gpu)
         assert eng._head_fused == (mode == "1")
         st = torch.cuda.current_stream().cuda_stream
@@ -223,7 +223,7 @@ def test_built_plans_pass_stream_order_check(gpu, monkeypatch, spec_fn, N, fork_
     check sees side-stream work at all (otherwise it would pass vacuously)."""
     from distributed_tensorflow_resnet_amd.utils.streamcheck import check_plan
 
-    monkeypatch.setenv("DTR_FORK_EVERY", fork_every)
+    monkeypatch.setenv("DTR_TUNE", f"fork_every={fork_every}")
     eng = Engine(spec_fn(), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
                  device=gpu, use_graph=False)
     assert eng.fork_wgrad

@@ -542,91 +542,6 @@ def test_direct_dgrad_fused_bn_backward_precomputed_coef(gpu):
     assert _rel(dx, fn.conv2d_dgrad(dh2, w, tuple(x.shape), 1)) < 5e-3
 
 
-@pytest.mark.parametrize("N,H,Cin,K,k,s,bnb", [
-    (8, 14, 256, 64, 1, 1, False),     # bottleneck conv1 dgrad (1x1): A = dh1, 64 channels
-    (8, 14, 64, 64, 3, 1, True),       # conv2 dgrad (3x3 / 1), with the next BN's sums
-    (8, 28, 128, 128, 3, 2, True),     # conv2 dgrad of a stage's first block (3x3 / 2)
-    (4, 7, 2048, 512, 1, 1, True),     # stage-4 conv1: 128x128 tiles, K = 512 (table limit)
-    (2, 7, 64, 128, 1, 1, False),      # small M: the FAST loop forced for the fused path
-])
-def test_gemm_dgrad_fused_bn_backward(gpu, N, H, Cin, K, k, s, bnb, monkeypatch):
-    """ABWD in the implicit-GEMM dgrad (conv_gemm.hip): the pending BN+ReLU backward
-    dh = a*g - b - c*xhat (coefficients from bn_bwd_finalize) applied while staging
-    A, dh written once for the wgrad; == bn_bwd_apply + plain dgrad."""
-    monkeypatch.setenv("DTR_GEMM_ABWD", "1")   # opt-in path (the step keeps bn_bwd_apply)
-    torch.manual_seed(17)
-    nat = fn.native()
-    Ho = (H - 1) // s + 1
-    M2 = N * Ho * Ho
-    da = torch.randn(N, Ho, Ho, K, device=gpu).to(BF)     # grad wrt relu(bn(x)), conv output shape
-    x = torch.randn(N, Ho, Ho, K, device=gpu).to(BF)      # that BN's input
-    w = (torch.randn(k, k, Cin, K, device=gpu) / math.sqrt(k * k * K)).to(BF)
-    mean, rstd = torch.randn(K, device=gpu) * 0.1, torch.rand(K, device=gpu) + 0.5
-    gamma = torch.rand(K, device=gpu) + 0.5
-    scale, shift = gamma * rstd, torch.randn(K, device=gpu) * 0.2
-    part = torch.randn(4, 2, K, device=gpu).contiguous() * 50
-    st = torch.cuda.current_stream().cuda_stream
-    dg, db, coef = (torch.empty(n, device=gpu) for n in (K, K, 3 * K))
-    nat.bn_bwd_finalize(part.data_ptr(), 4, M2, K, gamma.data_ptr(), rstd.data_ptr(),
-                        dg.data_ptr(), db.data_ptr(), coef.data_ptr(), st)
-    geom = [N, H, H, Cin, Ho, Ho, K, k, k, s, (k - 1) // 2]
-    assert not nat.conv_direct_covers(1, geom) and nat.conv_gemm_abwd_covers(geom, False)
-    assert not nat.conv_gemm_abwd_covers(geom, True)
-    dh = torch.full_like(da, float("nan"))
-    bx = torch.randn(N, H, H, Cin, device=gpu).to(BF) if bnb else None
-    bvec = [torch.rand(Cin, device=gpu) + 0.5 for _ in range(4)]
-    bpart_a = torch.zeros(4096 * 2 * Cin, device=gpu)
-    bpart_b = torch.zeros(4096 * 2 * Cin, device=gpu)
-    kw = {}
-    if bnb:
-        kw["bnb"] = [bx] + bvec + [bpart_a]
-    dx = fn.conv2d_dgrad(da, w, (N, H, H, Cin), s,
-                         abwd=[x, 0, mean, rstd, scale, shift, gamma, 0, 0, dh, dg, db, coef], **kw)
-    dh2 = torch.empty_like(da)
-    nat.bn_bwd_apply(da.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                     scale.data_ptr(), shift.data_ptr(), coef.data_ptr(), 0, dh2.data_ptr(),
-                     M2, K, st)
-    if bnb:
-        kw["bnb"] = [bx] + bvec + [bpart_b]
-    dx2 = fn.conv2d_dgrad(dh2, w, (N, H, H, Cin), s, **kw)
-    torch.cuda.synchronize()
-    assert not torch.isnan(dh).any()                     # every element written exactly once
-    assert (dh.float() - dh2.float()).abs().max().item() <= 2 * 2 ** -8 * dh2.float().abs().max().item()
-    assert _rel(dx, dx2) < 5e-3
-    if bnb:
-        assert _rel(bpart_a, bpart_b) < 5e-3
-
-
-@pytest.mark.parametrize("N,H,C,pre", [(16, 32, 16, True), (16, 16, 32, False), (128, 8, 64, True),
-                                       (32, 16, 32, True)])
-def test_grouped_direct_wgrad_equals_per_layer(gpu, N, H, C, pre):
-    """conv_wgrad_group: several same-shape layers' direct wgrads in ONE launch
-    (blockIdx.z = layer) write exactly the slabs the per-layer launches write."""
-    torch.manual_seed(16)
-    nat = fn.native()
-    geom = [N, H, H, C, H, H, C, 3, 3, 1, 1]
-    sp, pps = nat.wgrad_pick_splits(geom)
-    G = 3
-    xs = [torch.randn(N, H, H, C, device=gpu).to(BF) for _ in range(G)]
-    dys = [torch.randn(N, H, H, C, device=gpu).to(BF) for _ in range(G)]
-    scs = [torch.rand(C, device=gpu) + 0.5 for _ in range(G)]
-    shs = [torch.randn(C, device=gpu) * 0.3 for _ in range(G)]
-    n = sp * C * 9 * C
-    one = torch.full((G, n), 7.0, device=gpu)
-    grp = torch.full((G, n), -7.0, device=gpu)
-    st = fn._stream()
-    for i in range(G):
-        nat.conv_wgrad(dys[i].data_ptr(), xs[i].data_ptr(), scs[i].data_ptr() if pre else 0,
-                       shs[i].data_ptr() if pre else 0, one[i].data_ptr(), geom, sp, pps, st)
-    nat.conv_wgrad_group([d.data_ptr() for d in dys], [x.data_ptr() for x in xs],
-                         [s.data_ptr() if pre else 0 for s in scs],
-                         [s.data_ptr() if pre else 0 for s in shs],
-                         [grp[i].data_ptr() for i in range(G)], geom, sp, pps, st)
-    torch.cuda.synchronize()
-    assert torch.equal(one, grp)
-    assert torch.isfinite(grp).all()
-
-
 def test_grouped_wgrad_reduce_wide_and_deep(gpu):
     """wgrad_reduce_grouped over convs of both work-unit shapes (few splits: the
     transposed 16x64 tile; many: the 256-column split-row form), with padded output

@@ -65,7 +65,7 @@ def test_stem_s2d_conv_matches_7x7_stride2(gpu, N, H):
 
 
 def _engine(spec, monkeypatch, gpu, s2d, imgs, labels, master, stats):
-    monkeypatch.setenv("DTR_STEM_S2D", "1" if s2d else "0")
+    monkeypatch.setenv("DTR_TUNE", f"stem_s2d={int(s2d)}")
     eng = Engine(spec, imgs.shape[0], weight_decay=1e-4, lr_schedule=imagenet_lr_schedule(),
                  device=gpu, input_mode="nhwc", use_graph=False)
     assert eng.stem_s2d == s2d
