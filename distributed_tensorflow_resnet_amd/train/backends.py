@@ -58,7 +58,11 @@ class GPUBackend:
         self._host_step += 1
 
     def metrics(self):
-        return self.engine.metrics()
+        # rank-local (the session's hooks read metrics on their own schedules, chief-only
+        # hooks on the chief only, so a collective here would be joined by nobody -- or,
+        # with the c10d transport, by another rank's gradient all-reduce).  Like the
+        # reference's per-worker LoggingTensorHook, each rank logs its own batch.
+        return self.engine.metrics(reduce=False)
 
     def synchronize(self):
         torch.cuda.synchronize()

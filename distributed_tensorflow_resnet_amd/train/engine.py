@@ -1321,16 +1321,18 @@ class Engine:
         self.labels.copy_(torch.randint(0, self.spec.num_classes, (self.N,), generator=g,
                                         dtype=torch.int32))
 
-    def metrics(self) -> dict:
+    def metrics(self, reduce: bool = True) -> dict:
         """Host read of the last step's scalars (synchronises).  The `cost` term
         wd * 1/2 sum v^2 is exact (pre-update weights) when the step ran with
-        need_cost=True; otherwise it is computed now from the updated weights."""
+        need_cost=True; otherwise it is computed now from the updated weights.
+        ``reduce``: loss and precision over the whole global batch -- a collective
+        that EVERY rank must call at the same point; False: this rank's batch."""
         if self._cost_at != self._steps_run:
             self._run("cost", torch.cuda.current_stream().cuda_stream)
             self._cost_at = self._steps_run
         v = self.scalars.detach().cpu().tolist()
         loss_sum, correct, lr, l2 = v[0], v[1], v[2], v[3]
-        if self.dist is not None and self.world > 1:
+        if reduce and self.dist is not None and self.world > 1:
             t = torch.tensor([loss_sum, correct], device=self.device)
             self.dist.all_reduce_sum(t)
             loss_sum, correct = t.tolist()
