@@ -788,9 +788,13 @@ class Engine:
 
     def _flush_buckets(self, plan, force: bool = False):
         """Emit the grouped split-K reduce of every reduce group whose gradients are
-        all produced (all remaining ones if `force`); a bucket whose groups are all
-        reduced is joined to the main stream and marked ready for its all-reduce
-        (world > 1; with one process the only join is the final one)."""
+        all produced (all remaining ones if `force`).  A bucket whose groups are all
+        reduced is ready for its all-reduce (world > 1): with the native communicator
+        the comm stream waits on the main stream (BN parameter gradients) AND on the
+        side stream (the bucket's reduces), so the main stream's dgrad chain never
+        waits for the side stream mid-backward; for host-issued c10d all-reduces the
+        side stream is joined into the main stream (the host issues on main).  With
+        one process the only join is the final one."""
         for bi, (lo, hi, names) in enumerate(self.buckets):
             if bi in self._flushed:
                 continue
@@ -804,6 +808,12 @@ class Engine:
                 self._reduced.add((bi, gi))
             if not all((bi, gi) in self._reduced for gi in range(len(self.reduce_groups[bi]))):
                 continue
+            if self.comm is not None:
+                self._mark(plan, *names)
+                self._flushed.add(bi)
+                self._emit_allreduce(plan, lo, hi,
+                                     side_dep=self.fork_wgrad and not self._reduce_main)
+                continue
             if self.reduce_buckets or force:
                 if self.fork_wgrad and not self._reduce_main:
                     # join: the main stream (and the bucket's all-reduce) waits for the side stream
@@ -814,17 +824,21 @@ class Engine:
                     plan.wait(ev)
                 self._mark(plan, *names)
                 self._flushed.add(bi)
-                if self.comm is not None:
-                    self._emit_allreduce(plan, lo, hi)
 
-    def _emit_allreduce(self, plan, lo: int, hi: int):
-        """Fork the comm stream off the main stream at the bucket's ready point and
-        all-reduce grad[lo:hi) there (bf16 exchange: cast kernels on the comm
-        stream around a bf16 all-reduce), while the compute streams continue."""
-        ev = plan.new_event()
-        plan.record(ev)
+    def _emit_allreduce(self, plan, lo: int, hi: int, side_dep: bool):
+        """Fork the comm stream off the main stream (and, with ``side_dep``, off the
+        side stream, where the bucket's split-K reduces ran) at the bucket's ready
+        point and all-reduce grad[lo:hi) there (bf16 exchange: cast kernels on the
+        comm stream around a bf16 all-reduce), while the compute streams continue."""
+        evs = [plan.new_event()]
+        plan.record(evs[0])
+        if side_dep:
+            evs.append(plan.new_event())
+            plan.use_stream(1)
+            plan.record(evs[1])
         plan.use_stream(2)
-        plan.wait(ev)
+        for ev in evs:
+            plan.wait(ev)
         n = hi - lo
         g = self.grad.data_ptr() + 4 * lo
         if self.grad_bf16 is not None:
