@@ -42,7 +42,12 @@ def record_parser(raw: bytes, is_training: bool, rng=None, label_offset: int = 1
     jpeg = ex["image/encoded"][0]
     label = int(ex["image/class/label"][0]) - label_offset
     img = Image.open(io.BytesIO(jpeg))
-    img.draft("RGB", (image_size * 2, image_size * 2))   # JPEG DCT-domain downscale when large
+    # JPEG DCT-domain downscale of large images, never below the preprocessing's
+    # resize target (train: shorter side up to 512, eval: 256): PIL's draft keeps both
+    # sides >= the request, so the aspect-preserving resize still only downsamples,
+    # as vgg_preprocessing.py does from the full decode
+    side = vgg._RESIZE_SIDE_MAX if is_training else vgg._RESIZE_SIDE_MIN
+    img.draft("RGB", (side, side))
     img = img.convert("RGB")
     if u8:
         return vgg.crop_u8(img, image_size, image_size, is_training, rng=rng), label

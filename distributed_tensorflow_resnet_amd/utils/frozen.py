@@ -22,6 +22,8 @@ the architecture from its Const set and returns the TF-named tensors that
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -198,9 +200,37 @@ def read_frozen(path: str):
     return meta, tensors
 
 
+def export_eval_meta_graph(spec: ModelSpec, tensors: dict) -> bytes:
+    """The eval graph BEFORE freezing, as a MetaGraphDef (reference
+    resnet_cifar_frozen_model.py:91-96, export_meta_graph ->
+    resnet50_cifar_eval_graph.meta): the frozen GraphDef's weight Consts are
+    VariableV2 nodes again (same names, dtypes and shapes, no values -- those
+    live in the checkpoint), plus `global_step`, and the variables /
+    trainable_variables collections.  Node names are exactly the `.pb`'s."""
+    graph = export_graphdef(spec, tensors)
+    params = {p.name: p for p in spec.params}
+    nodes = []
+    for n in graph.nodes:
+        if n.op == "Const" and n.name in params:
+            dims = list(np.asarray(n.attr["value"]).shape)
+            n = gd.Node(n.name, "VariableV2", [], n.device,
+                        {"container": b"", "dtype": ("type", 1), "shape": gd.Shape(dims),
+                         "shared_name": b"", "_output_shapes": [gd.Shape(dims)]})
+        nodes.append(n)
+    nodes.insert(0, gd.Node("global_step", "VariableV2", [], "",
+                            {"container": b"", "dtype": ("type", 9), "shape": gd.Shape([]),
+                             "shared_name": b"", "_output_shapes": [gd.Shape([])]}))
+    trainable = {p.name for p in spec.trainables}
+    variables = [("global_step", False)] + [(p.name, p.name in trainable) for p in spec.params]
+    return gd.encode_meta_graph(gd.Graph(nodes, graph.producer, graph.min_consumer), variables)
+
+
 def freeze(prefix: str, out_path: str, dataset: str, resnet_size: int,
-           num_classes: int | None = None) -> dict:
-    """Checkpoint (tensor bundle) -> frozen eval GraphDef `.pb` (freeze_graph equivalent)."""
+           num_classes: int | None = None, meta_path: str | None = "") -> dict:
+    """Checkpoint (tensor bundle) -> frozen eval GraphDef `.pb` (freeze_graph
+    equivalent), and the unfrozen eval graph's MetaGraphDef next to it
+    (``meta_path``; "" = <dir>/resnet<size>_<cifar|imagenet>_eval_graph.meta,
+    None = skip)."""
     spec = build_spec(dataset, resnet_size, num_classes)
     tensors = tb.read_bundle(prefix)
     missing = [p.name for p in spec.params if p.name not in tensors]
@@ -208,9 +238,18 @@ def freeze(prefix: str, out_path: str, dataset: str, resnet_size: int,
         raise KeyError(f"{missing[:3]}... missing from {prefix}")
     graph = export_graphdef(spec, tensors)
     gd.write_graph(graph, out_path)
+    if meta_path == "":
+        kind = "cifar" if spec.dataset.startswith("cifar") else "imagenet"
+        meta_path = os.path.join(os.path.dirname(os.path.abspath(out_path)),
+                                 f"resnet{resnet_size}_{kind}_eval_graph.meta")
+    if meta_path:
+        tmp = meta_path + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(export_eval_meta_graph(spec, tensors))
+        os.replace(tmp, meta_path)
     return {"dataset": spec.dataset, "resnet_size": resnet_size, "num_classes": spec.num_classes,
             "nodes": len(graph.nodes), "outputs": ["predictions", "precision"],
-            "global_step": int(tensors.get("global_step", 0))}
+            "global_step": int(tensors.get("global_step", 0)), "meta_graph": meta_path}
 
 
 class FrozenModel:

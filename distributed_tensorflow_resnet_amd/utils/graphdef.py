@@ -375,6 +375,65 @@ def encode_graph(g: Graph) -> bytes:
     return bytes(out)
 
 
+def encode_meta_graph(g: Graph, variables, tf_version: str = "1.12.0") -> bytes:
+    """MetaGraphDef (the `.meta` of tf.train.export_meta_graph): field 1
+    MetaInfoDef {meta_graph_version, tensorflow_version}, field 2 the GraphDef,
+    field 4 the collections "variables" / "trainable_variables" as serialized
+    VariableDef {variable_name "<v>:0", snapshot_name "<v>/read:0"} (bytes_list).
+    ``variables``: [(name, trainable)] in creation order."""
+    out = bytearray()
+    info = bytearray()
+    _bytes_field(info, 1, f"v{tf_version}".encode())
+    _bytes_field(info, 5, tf_version.encode())
+    _bytes_field(out, 1, bytes(info))
+    _bytes_field(out, 2, encode_graph(g))
+    for key, keep in (("trainable_variables", lambda t: t), ("variables", lambda t: True)):
+        blist = bytearray()
+        for name, trainable in variables:
+            if not keep(trainable):
+                continue
+            vdef = bytearray()
+            _bytes_field(vdef, 1, f"{name}:0".encode())
+            _bytes_field(vdef, 3, f"{name}/read:0".encode())
+            if trainable:
+                _varint_field(vdef, 7, 1)
+            _bytes_field(blist, 1, bytes(vdef))
+        coll = bytearray()
+        _bytes_field(coll, 2, bytes(blist))       # CollectionDef.bytes_list
+        entry = bytearray()
+        _bytes_field(entry, 1, key.encode())
+        _bytes_field(entry, 2, bytes(coll))
+        _bytes_field(out, 4, bytes(entry))
+    return bytes(out)
+
+
+def read_meta_info(path: str) -> dict:
+    """{"tensorflow_version", "collections": {key: [variable names]}} of a `.meta`."""
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    info = {"tensorflow_version": None, "collections": {}}
+    for f, _, v in _proto_fields(buf):
+        if f == 1:
+            for f2, _, v2 in _proto_fields(v):
+                if f2 == 5:
+                    info["tensorflow_version"] = v2.decode()
+        elif f == 4:
+            key, names = None, []
+            for f2, _, v2 in _proto_fields(v):
+                if f2 == 1:
+                    key = v2.decode()
+                elif f2 == 2:
+                    for f3, _, v3 in _proto_fields(v2):
+                        if f3 == 2:                   # bytes_list
+                            for f4, _, v4 in _proto_fields(v3):
+                                if f4 == 1:           # one VariableDef
+                                    for f5, _, v5 in _proto_fields(v4):
+                                        if f5 == 1:
+                                            names.append(v5.decode().rsplit(":", 1)[0])
+            info["collections"][key] = names
+    return info
+
+
 def write_graph(g: Graph, path: str) -> None:
     import os
 

@@ -101,5 +101,24 @@ def test_full_depth_training_step_from_trained_weights(gpu, trained):
     assert per["conv2d_51/kernel"] < 0.1
     assert err <= 1.15 * noise + 1e-3, (err, noise)
     assert cos > 0.98
+    # per stage (stem, the three block layers): a regression confined to the early
+    # layers must not hide behind the global bound
+    def stage(name):
+        base = name.split("/")[0]
+        if base.startswith("conv2d"):
+            i = int(base.split("_")[1]) if "_" in base else 0
+            return "stem" if i == 0 else f"stage{(i - 1) // 17 + 1}"
+        if base.startswith("batch_normalization"):
+            i = int(base.split("_")[2]) if base.count("_") == 2 else 0
+            return f"stage{i // 16 + 1}" if i < 48 else "head"
+        return "head"
+    groups = {}
+    for n, s_ in sl.items():
+        groups.setdefault(stage(n), []).append(s_)
+    for gname in ("stem", "stage1", "stage2", "stage3"):
+        idx = torch.cat([torch.arange(s_.start, s_.stop, device=gpu) for s_ in groups[gname]])
+        e_s, n_s = _rel(eng.grad[idx], g32[idx]), _rel(g_emu[idx], g32[idx])
+        print(f"{gname}: engine {e_s:.3f} vs bf16-emulation {n_s:.3f}")
+        assert e_s <= 1.15 * n_s + 1e-3, (gname, e_s, n_s)
     # BN moving statistics: one step of decay 0.997 towards the batch (Bessel) stats
     assert _rel(eng.params.stats, store.stats) < 1e-4

@@ -119,6 +119,29 @@ def test_cpu_model_matches_reference_graph(ref_graph, ref_tensors):
     assert probs.max(1).values.mean() > 0.3
 
 
+@needs_pb
+def test_public_generator_api_matches_reference_graph(ref_graph, ref_tensors):
+    """The resnet_model_official-compatible API (cifar10_resnet_v2_generator, TF
+    variable names, HWIO kernels) loaded with the reference's trained weights ==
+    the reference's own frozen graph run by the interpreter, in eval mode."""
+    from distributed_tensorflow_resnet_amd.models import resnet_model_official as rmo
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 32, 32, 3)
+    model = rmo.cifar10_resnet_v2_generator(50, 10)
+    with torch.no_grad():
+        model(x, False)                       # creates the variables (TF creation order)
+        vars_ = model.variables()
+        assert set(vars_) == set(ref_tensors)
+        for name, v in vars_.items():
+            v.copy_(torch.from_numpy(np.asarray(ref_tensors[name], dtype=np.float32)))
+        ours = model(x, False).double()
+    logits = Interpreter(ref_graph).run("final_dense", {"X": x})
+    rel = ((ours - logits).norm() / logits.norm()).item()
+    assert rel < 1e-5, rel
+    assert rmo._BATCH_NORM_EPSILON == BN_EPS
+
+
 def test_imagenet_export_matches_cpu_model():
     """Stem pad 3/3 + VALID, 3x3/2 SAME max-pool, bottleneck blocks: the exported
     GraphDef run by the interpreter == our CPU model."""
@@ -159,6 +182,34 @@ def test_freeze_writes_graphdef_and_predict_reads_reference(tmp_path, ref_tensor
     out = str(tmp_path / "frozen.pb")
     meta = frozen.freeze(prefix, out, "cifar10", 50)
     assert meta["nodes"] == 704 and meta["global_step"] == 107738
+    meta_path = meta["meta_graph"]
+    assert os.path.basename(meta_path) == "resnet50_cifar_eval_graph.meta"
+    mg = gd.read_meta_graph(meta_path)
+    pbg = gd.read_graph(out)
+    assert [n.name for n in mg.nodes if n.name != "global_step"] == [n.name for n in pbg.nodes]
+    pb_ops = pbg.by_name()
+    params = set(ref_tensors)
+    for n in mg.nodes:
+        if n.name in params:
+            assert n.op == "VariableV2" and pb_ops[n.name].op == "Const"
+            assert list(n.attr["shape"].dims) == list(np.asarray(ref_tensors[n.name]).shape)
+        elif n.name != "global_step":
+            assert n.op == pb_ops[n.name].op and n.inputs == pb_ops[n.name].inputs, n.name
+    info = gd.read_meta_info(meta_path)
+    assert info["tensorflow_version"] == "1.12.0"
+    assert len(info["collections"]["trainable_variables"]) == 152
+    assert len(info["collections"]["variables"]) == 251
+    if os.path.exists(os.path.join(REF_DIR, "resnet50_cifar_eval_graph.meta")):
+        # the reference's own eval meta graph: same variables, same creation order
+        ref_info = gd.read_meta_info(os.path.join(REF_DIR, "resnet50_cifar_eval_graph.meta"))
+        assert info["collections"]["trainable_variables"] == ref_info["collections"]["trainable_variables"]
+        assert info["collections"]["variables"] == ref_info["collections"]["variables"]
+        ref_mg = gd.read_meta_graph(os.path.join(REF_DIR, "resnet50_cifar_eval_graph.meta"))
+        ref_vars = {n.name: n for n in ref_mg.nodes if n.op == "VariableV2"}
+        for n in mg.nodes:
+            if n.op == "VariableV2":
+                assert n.attr["shape"].dims == ref_vars[n.name].attr["shape"].dims, n.name
+                assert n.attr["dtype"] == ref_vars[n.name].attr["dtype"], n.name
     meta2, t2 = frozen.read_frozen(out)
     assert meta2["resnet_size"] == 50
     for k, v in ref_tensors.items():
