@@ -51,6 +51,9 @@ def timed(fnc, reps):
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    # under rocprofv3 --pmc: write the (layer, pass) of every call in launch order, so
+    # scripts/pmc_roofline.py can attribute the per-dispatch counters
+    manifest = open(os.environ["ROOFLINE_MANIFEST"], "w") if os.environ.get("ROOFLINE_MANIFEST") else None
     N = int(os.environ.get("ROOFLINE_N", "128"))
     dev = torch.device("cuda")
     BF = torch.bfloat16
@@ -95,6 +98,10 @@ def main():
         for p, (f, byts) in passes.items():
             if p == "dgrad" and C < 64:
                 continue
+            name = f"{H}x{H} {C}->{K} {k}x{k}/{s}"
+            if manifest:
+                manifest.write(f"{name}|{p}|{reps + 1}|{byts}|{flop}\n")
+                manifest.flush()
             f()
             torch.cuda.synchronize()
             us = timed(f, reps)
