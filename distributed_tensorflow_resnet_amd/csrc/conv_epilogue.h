@@ -267,6 +267,64 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
   }
 }
 
+// Split-K combine of the implicit-GEMM loops (conv_gemm.hip FAST, conv_ring.hip):
+// slice blockIdx.z of args.ksplit publishes its fp32 tile (write-through, thread-native
+// order) and takes a ticket; the last slice of the tile sums all slices in slice order
+// (bitwise independent of arrival order) and alone returns true (runs the epilogue).
+// 256 threads, wave tile MR x NR fragments of 16x16; the caller's LDS must be dead.
+template <int MR, int NR>
+__device__ __forceinline__ bool splitk_combine(const GemmArgs& args, f32x4 (&acc)[MR][NR],
+                                               char* smem, int tm, int tn) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int tile = tm * gridDim.y + tn;
+  const int S = args.ksplit, z = blockIdx.z;
+  const long slab = (long)MR * NR * 1024;                 // floats per slice tile
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long)tile * S * slab, 0,
+                                                    0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4_t, acc[a][b]), rs,
+          (int)((((long)z * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16);
+  int* flag = reinterpret_cast<int*>(smem);
+  if (!last_arriver(args.sk_cnt + tile, (unsigned)S, flag)) return false;
+  f32x4 tot[MR][NR];
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) tot[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int zz = 0; zz < S; ++zz) {
+    if (zz == z) {
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) tot[a][b] += acc[a][b];
+    } else {
+      f32x4 v[MR][NR];
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b)
+          v[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+              rs, (int)((((long)zz * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16));
+#pragma unroll
+      for (int a = 0; a < MR; ++a)
+#pragma unroll
+        for (int b = 0; b < NR; ++b) tot[a][b] += v[a][b];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < MR; ++a)
+#pragma unroll
+    for (int b = 0; b < NR; ++b) acc[a][b] = tot[a][b];
+  reset_counter(args.sk_cnt + tile);
+  __syncthreads();   // the flag word's LDS is the epilogue's
+  return true;
+}
+
 // Shared epilogue of every conv kernel (implicit-GEMM and direct): the wave
 // fragments acc[MR][NR] of the BM x BN tile at (m0, n0) -> LDS-staged 16-byte
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN

@@ -495,59 +495,7 @@ conv_gemm_kernel(GemmArgs args) {
       body(t + 1, I1{});
     }
     if (t < t_end) body(t, I0{});
-    if (sk_n > 1) {
-      // split-K: publish this slice's fp32 tile (write-through, thread-native order),
-      // take a ticket; the last slice of the tile sums all slices in slice order
-      // (bitwise independent of arrival order) and alone runs the epilogue
-      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-      constexpr int NV = MR * NR;                           // f32x4 per thread
-      const int tile = tm * gridDim.y + tn;
-      const int S = sk_n, z = sk_z;
-      const long slab = (long)BM * BN;                     // floats per slice tile
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long)tile * S * slab, 0,
-                                                        0x7fffffff, 0x00020000);
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int b = 0; b < NR; ++b)
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u32x4_t, acc[a][b]), rs,
-              (int)((((long)z * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16);
-      int* flag = reinterpret_cast<int*>(smem);
-      if (!last_arriver(args.sk_cnt + tile, (unsigned)S, flag)) return;
-      f32x4 tot[MR][NR];
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int b = 0; b < NR; ++b) tot[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int zz = 0; zz < S; ++zz) {
-        if (zz == z) {
-#pragma unroll
-          for (int a = 0; a < MR; ++a)
-#pragma unroll
-            for (int b = 0; b < NR; ++b) tot[a][b] += acc[a][b];
-        } else {
-          f32x4 v[MR][NR];
-#pragma unroll
-          for (int a = 0; a < MR; ++a)
-#pragma unroll
-            for (int b = 0; b < NR; ++b)
-              v[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                  rs, (int)((((long)zz * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16));
-#pragma unroll
-          for (int a = 0; a < MR; ++a)
-#pragma unroll
-            for (int b = 0; b < NR; ++b) tot[a][b] += v[a][b];
-        }
-      }
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int b = 0; b < NR; ++b) acc[a][b] = tot[a][b];
-      reset_counter(args.sk_cnt + tile);
-      __syncthreads();   // the flag word's LDS is the epilogue's
-      (void)NV;
-    }
+    if (sk_n > 1 && !splitk_combine<MR, NR>(args, acc, smem, tm, tn)) return;
   } else {   // general gather (runtime `fast` only for the narrow-column tiles)
   load_tile(0);
   if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
@@ -702,7 +650,8 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
     DTR_CHECK_LAUNCH();
   } else {
     if constexpr (BN >= 64) {
-      if (conv_gemm_fast(a, MODE)) {
+      const bool ring = BM == 128 && BN == 128 && (FLAGS & F_PRE) == 0 && conv_ring_covers(a, MODE);
+      if (ring || conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
         const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
         float* part = nullptr;
@@ -713,6 +662,10 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
           a.sk_part = part;
           a.sk_cnt = cnt;
           grid.z = S;
+        }
+        if (ring) {
+          conv_ring(a, MODE, FLAGS, grid, s);
+          return;
         }
         hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, true, NBUF>), grid,
                            dim3(256), lds, s, a);
@@ -796,6 +749,20 @@ static bool parity_dgrad(const GemmArgs& a) {
   return tune(T_PARITY_DGRAD) && a.g.stride == 2 &&
          (a.bnb_part == nullptr || a.bnb_acc != nullptr) && a.out_f32 == nullptr &&
          a.bias == nullptr && a.residual == nullptr;
+}
+
+// Whether conv_gemm(a, mode) takes the LDS-DMA ring loop (tests, diagnostics): the
+// dispatcher's own decisions -- direct kernel, parity classes, tile, ring coverage.
+bool conv_gemm_uses_ring(const GemmArgs& a0, int mode) {
+  if (conv_direct_covers(a0, mode)) return false;
+  GemmArgs a = a0;
+  if (mode == MODE_DGRAD && parity_dgrad(a)) {
+    const ConvGeom& g = a.g;
+    a.par = 1;
+    a.M = g.N * ((g.H + 1) >> 1) * ((g.W + 1) >> 1);
+    a.Kdim = ((g.kh + 1) >> 1) * ((g.kw + 1) >> 1) * g.K;
+  }
+  return conv_gemm_bn(a.M, a.Ncol) == 128 && conv_ring_covers(a, mode);
 }
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {

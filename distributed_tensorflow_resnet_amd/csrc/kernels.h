@@ -156,6 +156,11 @@ void set_conv_direct(int enabled);
 void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM / wgrad loops (tune conv_pipe)
 void set_fin_version(int v);   // BN finalize kernel variant (tune fin_v)
 int conv_gemm_bm(int M, int Ncol);
+// LDS-DMA ring loop (conv_ring.hip) for the 128x128 non-PRE tiles: covers / launch on the
+// caller's grid (split-K / parity set up by the caller, conv_gemm.hip)
+bool conv_ring_covers(const GemmArgs& a, int mode);
+void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
+bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 
 struct WgradArgs {

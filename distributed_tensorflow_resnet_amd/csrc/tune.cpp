@@ -64,6 +64,12 @@ const TuneEntry kTable[T_COUNT] = {
     {"wt_store", -1,
      "conv epilogue write-through stores: -1 auto (direct convs writing >= 2 MB: bs128 step "
      "1.304 -> 1.282 ms), 0 off, 1 on"},
+    {"ring", 1,
+     "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128x128 non-PRE convs (RN50 bs128 "
+     "conv dgrads 4.51 -> 4.05 ms/step, forwards 3.94 -> 3.85)"},
+    {"ring_kt", 5,
+     "ring only for K loops of at least this many 64-deep tiles (the 4-tile 14x14 256->1024 "
+     "forward: 56 -> 61 us on the ring)"},
 };
 
 std::atomic<long> g_val[T_COUNT];

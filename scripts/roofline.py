@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from distributed_tensorflow_resnet_amd.ops import functional as fn  # noqa: E402
+from distributed_tensorflow_resnet_amd.utils import tune  # noqa: E402
 
 PEAK_FLOPS = 2.3e15   # dense bf16 MFMA, sustained (2.5 PF/s headline, no sparsity)
 PEAK_BYTES = 5.0e12   # HBM3E, achievable streaming
@@ -49,8 +50,18 @@ def timed(fnc, reps):
     return statistics.median(ts)
 
 
+def set_cfg(nat, cfg):
+    """Apply 'key=v,key=v' native tuning entries (in-process A/B)."""
+    for item in filter(None, cfg.split(",")):
+        k, v = item.split("=")
+        nat.tune_set(k, int(v))
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    # --ab CFG_A CFG_B ...: time every pass under each native tuning config in turn, in
+    # one process (run-to-run clock drift between processes reached 10-25 %)
+    ab = sys.argv[sys.argv.index("--ab") + 1:] if "--ab" in sys.argv else []
     # under rocprofv3 --pmc: write the (layer, pass) of every call in launch order, so
     # scripts/pmc_roofline.py can attribute the per-dispatch counters
     manifest = open(os.environ["ROOFLINE_MANIFEST"], "w") if os.environ.get("ROOFLINE_MANIFEST") else None
@@ -59,6 +70,7 @@ def main():
     BF = torch.bfloat16
     nat = fn.native()
     rows = []
+    ab_rows = []
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}
     for H, C, K, k, s, cnt in SHAPES:
         g = fn.ConvGeom(N, H, H, C, K, k, k, s)
@@ -84,9 +96,13 @@ def main():
         xb, yb, wb = N * H * H * C * 2, M * K * 2, K * k * k * C * 2
         sp, _ = nat.wgrad_pick_splits(g.as_list())
         slab = sp * K * k * k * C * 4
+        # the engine applies the input BN+ReLU in the conv (PRE) unless it materializes
+        # it (train/engine.py _materialize_bn: stages 3-4)
+        pre = dict(pre_scale=sc, pre_shift=sh)
+        if C >= tune.get("mat_bn_minc") and N * H * H * C <= tune.get("mat_bn_elems"):
+            pre = {}
         passes = {
-            "fwd": (lambda: fn.conv2d_fwd(x, w, s, stat_part=part, out=out, pre_scale=sc,
-                                          pre_shift=sh, fin=[acc]),
+            "fwd": (lambda: fn.conv2d_fwd(x, w, s, stat_part=part, out=out, fin=[acc], **pre),
                     xb + wb + yb),
             "dgrad": (lambda: fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx, bnb=bnb,
                                               bfin=[bacc]),
@@ -98,23 +114,53 @@ def main():
         for p, (f, byts) in passes.items():
             if p == "dgrad" and C < 64:
                 continue
-            name = f"{H}x{H} {C}->{K} {k}x{k}/{s}"
+            name = f"{H}x{H} {C}->{K} {k}x{k}/{s}" + (" PRE" if p == "fwd" and pre else "")
             if manifest:
                 manifest.write(f"{name}|{p}|{reps + 1}|{byts}|{flop}\n")
                 manifest.flush()
+            if ab:
+                dflt = {t[0]: t[3] for t in nat.tune_table()}
+                alts = []
+                for rnd in range(3):
+                    for i, cfg in enumerate(ab):
+                        set_cfg(nat, cfg)
+                        f()
+                        torch.cuda.synchronize()
+                        t_us = timed(f, reps)
+                        if rnd == 0:
+                            alts.append([])
+                        alts[i].append(t_us)
+                        set_cfg(nat, ",".join(f"{k}={v}" for k, v in dflt.items()))
+                ab_rows.append((name, p, cnt, [statistics.median(a) for a in alts]))
+                continue
             f()
             torch.cuda.synchronize()
             us = timed(f, reps)
             floor = max(flop / PEAK_FLOPS, byts / PEAK_BYTES) * 1e6
-            rows.append((f"{H}x{H} {C}->{K} {k}x{k}/{s}", p, cnt, flop, byts, floor, us))
+            rows.append((name, p, cnt, flop, byts, floor, us))
             tot[p][0] += cnt * floor
             tot[p][1] += cnt * us
         del x, w, whwio, dy, out, dx, bnb, gw, part
         torch.cuda.empty_cache()
+    if ab:
+        print(f"# In-process A/B, N = {N}: us per call (median of 3 alternating rounds x {reps})\n")
+        print("| layer | pass | x/step | " + " | ".join(ab) + " |")
+        print("|---|---|---|" + "---|" * len(ab))
+        sums = [0.0] * len(ab)
+        for name, p, cnt, ts in ab_rows:
+            print(f"| {name} | {p} | {cnt} | " + " | ".join(f"{t:.1f}" for t in ts) + " |")
+            for i, t in enumerate(ts):
+                sums[i] += cnt * t
+        print()
+        for p in ("fwd", "dgrad", "wgrad"):
+            per = [sum(cnt * ts[i] for name, pp, cnt, ts in ab_rows if pp == p) for i in range(len(ab))]
+            print(f"- {p}: " + ", ".join(f"{c}: {v / 1e3:.3f} ms/step" for c, v in zip(ab, per)))
+        return
     print(f"# ImageNet ResNet-50 v2 conv roofline, N = {N}, 1x MI355X\n")
     print("Floor = max(FLOP / 2.3 PF/s, unique bytes / 5 TB/s); unique bytes count each operand "
           "once (dgrad: dy, W, dx and the BN input x its epilogue reads; wgrad: dy, x, the fp32 "
-          "split-K slabs written and read back, dW).  `scripts/roofline.py`, HIP-event medians.\n")
+          "split-K slabs written and read back, dW).  Forward convs take the BN+ReLU prologue "
+          "(PRE) where the engine does.  `scripts/roofline.py`, HIP-event medians.\n")
     print("| layer | pass | x/step | GFLOP | MB | floor us | achieved us | x floor | TF/s | TB/s |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for name, p, cnt, flop, byts, floor, us in rows:
