@@ -660,10 +660,10 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
 // Grid of the finalize-fused apply: every workgroup re-reads 16 fp64 per channel, so
 // the grid is capped (BWD_FIN_BLOCKS, 4 vectors in flight per thread instead of 2).
 constexpr int BWD_FIN_U = 4;
-constexpr long BWD_FIN_BLOCKS = 256;
 static long bwd_fin_blocks(long nvec) {
   const long b = (nvec + 256L * BWD_FIN_U - 1) / (256L * BWD_FIN_U);
-  return b < BWD_FIN_BLOCKS ? b : BWD_FIN_BLOCKS;
+  const long cap = tune(T_BWD_FIN_BLOCKS);
+  return b < cap ? b : cap;
 }
 
 // round-1 rule (the CIFAR shapes): C <= 64 on the uncapped U = 2 grid of <= 1024 blocks
