@@ -650,7 +650,8 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
     DTR_CHECK_LAUNCH();
   } else {
     if constexpr (BN >= 64) {
-      const bool ring = BM == 128 && BN == 128 && (FLAGS & F_PRE) == 0 && conv_ring_covers(a, MODE);
+      const bool ring = BM == 128 && (BN == 128 || (BN == 64 && WM == 4)) && (FLAGS & F_PRE) == 0 &&
+                        conv_ring_covers(a, MODE);
       if (ring || conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
         const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
@@ -762,7 +763,7 @@ bool conv_gemm_uses_ring(const GemmArgs& a0, int mode) {
     a.M = g.N * ((g.H + 1) >> 1) * ((g.W + 1) >> 1);
     a.Kdim = ((g.kh + 1) >> 1) * ((g.kw + 1) >> 1) * g.K;
   }
-  return conv_gemm_bn(a.M, a.Ncol) == 128 && conv_ring_covers(a, mode);
+  return conv_ring_covers(a, mode);
 }
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {

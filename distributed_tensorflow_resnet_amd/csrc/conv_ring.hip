@@ -12,37 +12,33 @@
 // parallelism bound, not a byte or MFMA bound.
 //
 // Here both operands go global -> LDS by buffer_load ... lds (16 B per lane, no VGPR
-// destination, out-of-range padding reads land as zeros) into a ring of SLOTS 16 KiB
-// operand slots (one slot = the A or the B tile of one 64-deep K step); operand load j
-// (A of tile j / 2 for even j, B for odd j) goes to slot j % SLOTS:
+// destination, out-of-range padding reads land as zeros) into a 2-stage LDS ring:
 //
-//   prologue: issue operand loads 0 .. SLOTS-3
-//   tile t:   s_waitcnt vmcnt(4 (SLOTS-4))  this wave's DMAs of A_t and B_t have landed
-//             s_barrier                      ... every wave's; tile t-1's two slots are free
-//             issue the next two operand loads into them
-//             32 MFMA per wave on tile t's slots
+//   prologue: issue K tile 0 into stage 0
+//   tile t:   s_waitcnt vmcnt(0)   this wave's DMAs of tile t have landed
+//             s_barrier            ... every wave's; stage (t+1) % 2 (tile t-1) is free
+//             issue tile t+1 into stage (t+1) % 2
+//             MFMAs on stage t % 2
 //
-// so (SLOTS - 2) / 2 K tiles are in flight beside the one being multiplied.  Built with
-// SLOTS = 4 (64 KiB, two workgroups per CU, one tile ahead).  Measured alternatives
-// (profiles/imagenet_resnet50_ring.md, in-process A/B over the RN50 layers): 5 slots
-// (80 KiB, still two workgroups per CU, 1.5 tiles ahead) tie; 6 and 8 slots (one
-// workgroup per CU, 2-3 tiles ahead) are 10-50 % slower -- with one wave per SIMD
-// nothing covers the LDS-read latency after each barrier or the epilogue.  What the
-// ring wins over the register loop is issue work (no VGPR staging, ds_write pass or
-// per-chunk index math), not memory-level parallelism.
+// Tiles BM x BN = 128 x 128 (4 waves 2 x 2, 48-64 KiB LDS: two workgroups per CU) and
+// 128 x 64 (4 waves 4 x 1, the 64-channel stage-1 layers).  Measured alternatives
+// (profiles/imagenet_resnet50_ring.md, in-process A/B over the RN50 layers): a ring of
+// five 16 KiB operand slots (80 KiB, still two workgroups per CU, 1.5 tiles ahead) tied
+// this one; 3-4 stages (one workgroup per CU, 2-3 tiles ahead) were 10-50 % slower --
+// with one wave per SIMD nothing covers the LDS-read latency after each barrier or the
+// epilogue.  What the ring wins over the register loop is issue work (no VGPR staging,
+// no ds_write pass, no per-chunk index math), not memory-level parallelism.
 //
-// One raw barrier per K tile and counted waits only: __syncthreads() would add the
-// vmcnt(0) that drains the ring (cdna_hip_programming.md, "Pipelining across
-// barriers").  Every wave issues exactly 4 DMAs per operand load (loads past the end
-// are issued out of range), so the count is exact.  The LDS image is the XOR-swizzled
+// One raw barrier per K tile: __syncthreads() would add a vmcnt(0) that also drains the
+// epilogue operands prefetched at kernel start.  The LDS image is the XOR-swizzled
 // [row][64] bf16 layout of conv_gemm.hip; since a DMA's LDS destination is lane-linear
 // (wave base + 16 B x lane), the swizzle goes on the SOURCE: lane l of a 1 KiB piece
 // covers row l / 8, slot l % 8, and fetches k-chunk (l % 8) ^ (row % 8).
 //
 // Per lane and K tile the gather is one add (row offset + scalar tap offset) and a
 // tap-validity bit (a per-row mask of the filter taps, built once), instead of the
-// per-chunk index math of the register loop; the tap walks (tap, channel base) of the
-// A and B issue pointers advance on the scalar unit.
+// per-chunk index math of the register loop; the tap walk (tap, channel base) of the
+// issue pointer advances on the scalar unit.
 #include <algorithm>
 #include <cstdio>
 #include <stdexcept>
@@ -56,6 +52,7 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int kRingOOB = 0x7fff0000;   // buffer offset past every operand (reads zeros)
+constexpr int STAGE_A_BYTES = 128 * 64 * 2;   // the A tile (128 rows x 64 k) of a ring stage
 
 template <int n>
 __device__ __forceinline__ void ring_wait_vm() {
@@ -66,16 +63,17 @@ __device__ __forceinline__ void ring_wait_vm() {
 
 }  // namespace
 
-template <int MODE, int FLAGS, int SLOTS>
+template <int MODE, int FLAGS, int BN>
 __global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(SLOTS <= 5 ? 2 : 1, SLOTS <= 5 ? 2 : 1)))
+__attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_ring_kernel(GemmArgs args) {
-  constexpr int BM = 128, BN = 128, WM = 2, WN = 2, BK = 64;
+  constexpr int BM = 128, BK = 64;
+  constexpr int WM = BN == 128 ? 2 : 4, WN = 4 / WM;
   constexpr int MR = BM / WM / 16, NR = BN / WN / 16;
-  constexpr int OP_B = BM * BK * 2;      // bytes of one operand tile (one slot)
+  static_assert(BM * BK * 2 == STAGE_A_BYTES, "A tile bytes");   // stage: A, then B (BN x BK)
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
   static_assert((FLAGS & (F_PRE | F_ABWD)) == 0, "no A-operand prologue on the ring");
-  static_assert(SLOTS >= 4 && SLOTS <= 8, "4-8 operand slots");
+  static_assert(BN == 128 || BN == 64, "128 x 128 or 128 x 64 tiles");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ConvGeom& g = args.g;
@@ -107,6 +105,9 @@ conv_ring_kernel(GemmArgs args) {
   const int kg = (lane & 7) ^ lr;                 // source-side swizzle
   int a_off[4];                                    // bytes, valid-tap base
   unsigned a_mask[4];                              // bit tl: class-local tap tl is in range
+  // B DMAs (8 rows each) per wave and tile: BN / 32 of the 4 used.  Fixed size on purpose:
+  // a lambda capturing an array whose size depends on a template parameter made hipcc
+  // (ROCm 7.2) silently drop the kernel's host stub -- an undefined symbol at load time.
   int b_off[4];
   const int ntap = (par ? ((g.kh - par_ph + 1) >> 1) : g.kh) * taw;
 #pragma unroll
@@ -161,7 +162,10 @@ conv_ring_kernel(GemmArgs args) {
     }
     a_mask[i] = mask;
     a_off[i] = mask ? (int)((pix * Acin + kg * 8) * 2) : 0;
-    const int nrow = n0 + r;
+  }
+#pragma unroll
+  for (int i = 0; i < BN / 32; ++i) {
+    const int nrow = n0 + (wave * (BN / 32) + i) * 8 + lr;
     if constexpr (MODE == MODE_FWD) b_off[i] = nrow < NC ? (nrow * KD + kg * 8) * 2 : kRingOOB;
     else b_off[i] = nrow < NC ? (nrow * g.K + kg * 8) * 2 : kRingOOB;
   }
@@ -179,66 +183,43 @@ conv_ring_kernel(GemmArgs args) {
   const int t_beg = (int)(((long)sk_z * KT_all) / sk_n);
   const int t_end = (int)(((long)(sk_z + 1) * KT_all) / sk_n);
   const int cpt = Acin / BK;                       // K tiles per tap
-  struct Walk {                                    // issue pointer: tile, tap, channel base
-    int t, tl, c, ta, tb;
-  };
-  Walk wa, wb;
-  wa.t = t_beg;
-  wa.tl = t_beg / cpt;
-  wa.c = (t_beg - wa.tl * cpt) * BK;
-  wa.ta = wa.tl / taw;
-  wa.tb = wa.tl - wa.ta * taw;
-  wb = wa;
-  auto advance = [&](Walk& w) {
-    ++w.t;
-    w.c += BK;
-    if (w.c == Acin) {
-      w.c = 0;
-      ++w.tl;
-      if (++w.tb == taw) {
-        w.tb = 0;
-        ++w.ta;
-      }
+  int it_t = t_beg;                                // issue pointer: tile, tap, channel
+  int it_tl = t_beg / cpt;
+  int it_c = (t_beg - it_tl * cpt) * BK;
+  int it_ta = it_tl / taw, it_tb = it_tl - it_ta * taw;
+  auto issue = [&](int stage) {   // tile it_t -> stage: 4 A + BN / 32 B DMAs per wave
+    const int a_pix = MODE == MODE_FWD ? it_ta * g.W + it_tb : -(it_ta * g.Wo + it_tb);
+    const int sa = (a_pix * Acin + it_c) * 2;
+    int sb;
+    if constexpr (MODE == MODE_FWD) {
+      sb = (it_tl * Acin + it_c) * 2;
+    } else {
+      const int rr = par ? par_ph + 2 * it_ta : it_ta, cc = par ? par_pw + 2 * it_tb : it_tb;
+      sb = ((rr * g.kw + cc) * g.C * g.K + it_c) * 2;
     }
-  };
-  // operand load j -> slot j % SLOTS: A of tile wa.t (even j) or B of tile wb.t (odd j)
-  auto issue_a = [&](int slot) {
-    const bool live = wa.t < t_end;
-    const int a_pix = MODE == MODE_FWD ? wa.ta * g.W + wa.tb : -(wa.ta * g.Wo + wa.tb);
-    const int sa = live ? (a_pix * Acin + wa.c) * 2 : kRingOOB;
-    char* st = smem + slot * OP_B;
+    char* st = smem + stage * (STAGE_A_BYTES + BN * 128);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bool ok = (a_mask[i] >> (wa.tl & 31)) & 1u;   // (tail tiles: sa is out of range)
-      const int off = ok ? a_off[i] + sa : kRingOOB;
+      const bool ok = (a_mask[i] >> it_tl) & 1u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_a, (lds_void*)(st + (wave * 4 + i) * 1024), 16, off, 0, 0, 0);
+          rs_a, (lds_void*)(st + (wave * 4 + i) * 1024), 16, ok ? a_off[i] + sa : kRingOOB, 0, 0,
+          0);
     }
-    advance(wa);
-  };
-  auto issue_b = [&](int slot) {
-    const bool live = wb.t < t_end;
-    int b_bytes;
-    if constexpr (MODE == MODE_FWD) {
-      b_bytes = (wb.tl * Acin + wb.c) * 2;
-    } else {
-      const int rr = par ? par_ph + 2 * wb.ta : wb.ta, cc = par ? par_pw + 2 * wb.tb : wb.tb;
-      b_bytes = ((rr * g.kw + cc) * g.C * g.K + wb.c) * 2;
-    }
-    const int sb = live ? b_bytes : kRingOOB;
-    char* st = smem + slot * OP_B;
+    char* const stb = st + STAGE_A_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < BN / 32; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_b, (lds_void*)(st + (wave * 4 + i) * 1024), 16, b_off[i] + sb, 0, 0, 0);
-    advance(wb);
-  };
-  int j_issue = 0, slot_issue = 0;
-  auto issue_next = [&]() {
-    if (j_issue & 1) issue_b(slot_issue);
-    else issue_a(slot_issue);
-    ++j_issue;
-    slot_issue = slot_issue + 1 == SLOTS ? 0 : slot_issue + 1;
+          rs_b, (lds_void*)(stb + (wave * (BN / 32) + i) * 1024), 16, b_off[i] + sb, 0, 0, 0);
+    ++it_t;
+    it_c += BK;
+    if (it_c == Acin) {
+      it_c = 0;
+      ++it_tl;
+      if (++it_tb == taw) {
+        it_tb = 0;
+        ++it_ta;
+      }
+    }
   };
 
   f32x4 acc[MR][NR];
@@ -248,9 +229,10 @@ conv_ring_kernel(GemmArgs args) {
     for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto mma_slots = [&](int sa, int sb) {
-    const bf16* A = reinterpret_cast<const bf16*>(smem + sa * OP_B);
-    const bf16* B = reinterpret_cast<const bf16*>(smem + sb * OP_B);
+  auto mma_stage = [&](int stage) {
+    const bf16* A = reinterpret_cast<const bf16*>(smem + stage * (STAGE_A_BYTES + BN * 128));
+    const bf16* B = reinterpret_cast<const bf16*>(smem + stage * (STAGE_A_BYTES + BN * 128) +
+                                                  STAGE_A_BYTES);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fq;
@@ -277,24 +259,19 @@ conv_ring_kernel(GemmArgs args) {
   EP epre;
   if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
 
-  // ---- prologue: SLOTS - 2 operand loads in flight ----
-#pragma unroll
-  for (int j = 0; j < SLOTS - 2; ++j) issue_next();
-  int rd = 0;   // slot of A_t (B_t in the next)
+  // ---- 2-stage ring: tile t+1 in flight during the MFMAs of tile t ----
+  issue(0);
+  int rd = 0;
   for (int t = t_beg; t < t_end; ++t) {
-    ring_wait_vm<4 * (SLOTS - 4)>();
+    ring_wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue_next();
-    issue_next();
-    const int rb = rd + 1 == SLOTS ? 0 : rd + 1;
-    mma_slots(rd, rb);
-    rd = rb + 1 == SLOTS ? 0 : rb + 1;
+    if (t + 1 < t_end) issue(rd ^ 1);
+    mma_stage(rd);
+    rd ^= 1;
   }
-  // drain the ring (the over-issued tail DMAs too) before the epilogue reuses the LDS
-  ring_wait_vm<0>();
-  __syncthreads();
+  __syncthreads();   // every wave's MFMA reads are done: the epilogue reuses the LDS
 
   if (sk_n > 1 && !splitk_combine<MR, NR>(args, acc, smem, tm, tn)) return;
   if constexpr (BNB && EP::ON)
@@ -311,30 +288,39 @@ bool conv_ring_covers(const GemmArgs& a, int mode) {
   const ConvGeom& g = a.g;
   const int Acin = mode == MODE_FWD ? g.C : g.K;
   if (a.pre_scale != nullptr || a.abwd.x != nullptr) return false;
-  if (Acin % 64 != 0 || a.Ncol % 128 != 0 || conv_gemm_bm(a.M, a.Ncol) != 128) return false;
+  if (Acin % 64 != 0 || a.Ncol % 64 != 0 || conv_gemm_bm(a.M, a.Ncol) != 128) return false;
+  const int bn = conv_gemm_bn(a.M, a.Ncol);
+  if (bn != 128 && bn != 64) return false;
   const long a_elems = mode == MODE_FWD ? (long)g.N * g.H * g.W * g.C
                                         : (long)g.N * g.Ho * g.Wo * g.K;
   const long b_elems = (long)g.kh * g.kw * g.C * g.K;
   if (a_elems >= (1L << 30) || b_elems >= (1L << 30) || g.kh * g.kw > 32) return false;
   if (mode == MODE_DGRAD && g.stride != 1 && !a.par) return false;   // non-linear taps
-  return (a.Kdim + 63) / 64 >= tune(T_RING_KT);
+  return (a.Kdim + 63) / 64 >= tune(mode == MODE_FWD ? T_RING_KT : T_RING_KT_DGRAD);
 }
 
-template <int MODE, int FLAGS, int SLOTS>
+template <int MODE, int FLAGS, int BN>
 static void ring_launch(GemmArgs a, dim3 grid, hipStream_t s) {
-  size_t lds = std::max((size_t)SLOTS * 16 * 1024, EpiLayout<128, 128, 2>::BYTES);
-  hipLaunchKernelGGL((conv_ring_kernel<MODE, FLAGS, SLOTS>), grid, dim3(256), lds, s, a);
+  constexpr int WM = BN == 128 ? 2 : 4;
+  const size_t lds = std::max((size_t)2 * (128 + BN) * 64 * 2, EpiLayout<128, BN, WM>::BYTES);
+  hipLaunchKernelGGL((conv_ring_kernel<MODE, FLAGS, BN>), grid, dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
 }
 
-void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s) {
+template <int BN>
+static void ring_flags(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s) {
   if (mode == MODE_FWD) {
-    if (flags & F_STATS) ring_launch<MODE_FWD, F_STATS, 4>(a, grid, s);
-    else ring_launch<MODE_FWD, 0, 4>(a, grid, s);
+    if (flags & F_STATS) ring_launch<MODE_FWD, F_STATS, BN>(a, grid, s);
+    else ring_launch<MODE_FWD, 0, BN>(a, grid, s);
   } else {
-    if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, 4>(a, grid, s);
-    else ring_launch<MODE_DGRAD, 0, 4>(a, grid, s);
+    if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, BN>(a, grid, s);
+    else ring_launch<MODE_DGRAD, 0, BN>(a, grid, s);
   }
+}
+
+void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s) {
+  if (conv_gemm_bn(a.M, a.Ncol) == 128) ring_flags<128>(a, mode, flags, grid, s);
+  else ring_flags<64>(a, mode, flags, grid, s);
 }
 
 }  // namespace dtr

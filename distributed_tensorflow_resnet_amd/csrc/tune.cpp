@@ -68,11 +68,14 @@ const TuneEntry kTable[T_COUNT] = {
      "grid cap of the finalize-fused BN backward apply (each workgroup re-reads 16 fp64 per "
      "channel)"},
     {"ring", 1,
-     "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128x128 non-PRE convs (RN50 bs128 "
+     "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128-row non-PRE convs (RN50 bs128 "
      "conv dgrads 4.51 -> 4.05 ms/step, forwards 3.94 -> 3.85)"},
     {"ring_kt", 5,
-     "ring only for K loops of at least this many 64-deep tiles (the 4-tile 14x14 256->1024 "
+     "ring forwards from this many 64-deep K tiles (the 4-tile 14x14 256->1024 "
      "forward: 56 -> 61 us on the ring)"},
+    {"ring_kt_dgrad", 4,
+     "ring dgrads from this many 64-deep K tiles (the 4-tile 14x14 1024->256 dgrad: 75.8 -> "
+     "68.8 us on the ring)"},
 };
 
 std::atomic<long> g_val[T_COUNT];

@@ -39,7 +39,8 @@ enum TuneId : int {
   T_WT_STORE,          // conv epilogue write-through stores (-1 auto, 0 off, 1 on)
   T_BWD_FIN_BLOCKS,    // grid cap of the finalize-fused BN backward apply
   T_RING,              // LDS-DMA ring implicit GEMM (conv_ring.hip) for eligible convs
-  T_RING_KT,           // ... for K loops of at least this many 64-deep tiles
+  T_RING_KT,           // ... forward convs with K loops of at least this many 64-deep tiles
+  T_RING_KT_DGRAD,     // ... dgrads with K loops of at least this many tiles
   T_COUNT
 };
 

@@ -693,6 +693,10 @@ RING_CASES = [
     ("dgrad", 32, 14, 256, 256, 3, 1),
     ("dgrad", 128, 14, 256, 256, 3, 2),   # stride 2: output-parity classes
     ("dgrad", 128, 7, 512, 2048, 1, 1),   # split-K, 1x1
+    ("fwd", 48, 28, 64, 64, 3, 1),        # 128 x 64 tiles (64 output channels)
+    ("fwd", 48, 28, 512, 64, 1, 1),
+    ("dgrad", 48, 28, 64, 64, 3, 1),
+    ("dgrad", 48, 28, 64, 256, 1, 1),
 ]
 
 
