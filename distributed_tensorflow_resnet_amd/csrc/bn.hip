@@ -659,11 +659,13 @@ void bn_relu_bwd_apply(const bf16* dy, const bf16* x, const float* mean, const f
 
 // Grid of the finalize-fused apply: every workgroup re-reads 16 fp64 per channel, so
 // the grid is capped (BWD_FIN_BLOCKS, 4 vectors in flight per thread instead of 2).
+// (256: the RN50 shapes stream at 4.9-5.9 TB/s; caps of 512-2048 measured no faster,
+// profiles/bn_bwd_apply_bandwidth.md)
 constexpr int BWD_FIN_U = 4;
+constexpr long BWD_FIN_BLOCKS = 256;
 static long bwd_fin_blocks(long nvec) {
   const long b = (nvec + 256L * BWD_FIN_U - 1) / (256L * BWD_FIN_U);
-  const long cap = tune(T_BWD_FIN_BLOCKS);
-  return b < cap ? b : cap;
+  return b < BWD_FIN_BLOCKS ? b : BWD_FIN_BLOCKS;
 }
 
 // round-1 rule (the CIFAR shapes): C <= 64 on the uncapped U = 2 grid of <= 1024 blocks

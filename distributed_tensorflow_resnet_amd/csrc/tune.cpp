@@ -64,9 +64,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"wt_store", -1,
      "conv epilogue write-through stores: -1 auto (direct convs writing >= 2 MB: bs128 step "
      "1.304 -> 1.282 ms), 0 off, 1 on"},
-    {"bwd_fin_blocks", 256,
-     "grid cap of the finalize-fused BN backward apply (each workgroup re-reads 16 fp64 per "
-     "channel)"},
     {"ring", 1,
      "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128-row non-PRE convs (RN50 bs128 "
      "conv dgrads 4.51 -> 4.05 ms/step, forwards 3.94 -> 3.85)"},

@@ -37,7 +37,6 @@ enum TuneId : int {
   T_FIN_V,             // BN finalize kernel variant (-1 auto)
   T_BWD_APPLY_FIN,     // BN backward apply finalizes in-kernel when the grid allows
   T_WT_STORE,          // conv epilogue write-through stores (-1 auto, 0 off, 1 on)
-  T_BWD_FIN_BLOCKS,    // grid cap of the finalize-fused BN backward apply
   T_RING,              // LDS-DMA ring implicit GEMM (conv_ring.hip) for eligible convs
   T_RING_KT,           // ... forward convs with K loops of at least this many 64-deep tiles
   T_RING_KT_DGRAD,     // ... dgrads with K loops of at least this many tiles

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """BN+ReLU backward apply with the finalize fused in (bn_bwd_apply_acc): device time and
-streamed bandwidth per grid cap (tune bwd_fin_blocks), in-process A/B over the ImageNet
-ResNet-50 bs128 BN shapes.   python3 scripts/bn_bwd_grid.py [caps...]"""
+streamed bandwidth over the ImageNet ResNet-50 bs128 BN shapes.  Round 3 swept the grid
+cap (256-2048 workgroups, then a tune key): 256 was never beaten, the key was removed
+(profiles/bn_bwd_apply_bandwidth.md).   python3 scripts/bn_bwd_grid.py"""
 import os
 import statistics
 import sys
@@ -18,9 +19,8 @@ SHAPES = [(401408, 64, False), (401408, 256, True), (100352, 128, False), (10035
 
 
 def main():
-    caps = [int(c) for c in sys.argv[1:]] or [256, 512, 1024, 2048]
+    caps = [256]
     nat = fn.native()
-    dflt = {t[0]: t[3] for t in nat.tune_table()}
     dev = torch.device("cuda")
     st = torch.cuda.current_stream().cuda_stream
     print("| M | C | add | " + " | ".join(f"cap {c} us (TB/s)" for c in caps) + " |")
@@ -40,7 +40,6 @@ def main():
         res = {c: [] for c in caps}
         for _ in range(3):
             for c in caps:
-                nat.tune_set("bwd_fin_blocks", c)
                 if not nat.bn_bwd_apply_acc_fits(M, C):
                     continue
                 f = lambda: nat.bn_bwd_apply_acc(  # noqa: E731
@@ -57,7 +56,6 @@ def main():
                 b.record()
                 b.synchronize()
                 res[c].append(a.elapsed_time(b) * 1e3 / 20)
-        nat.tune_set("bwd_fin_blocks", dflt["bwd_fin_blocks"])
         cells = []
         for c in caps:
             if res[c]:
