@@ -296,7 +296,8 @@ bool conv_ring_covers(const GemmArgs& a, int mode) {
   const long b_elems = (long)g.kh * g.kw * g.C * g.K;
   if (a_elems >= (1L << 30) || b_elems >= (1L << 30) || g.kh * g.kw > 32) return false;
   if (mode == MODE_DGRAD && g.stride != 1 && !a.par) return false;   // non-linear taps
-  return (a.Kdim + 63) / 64 >= tune(mode == MODE_FWD ? T_RING_KT : T_RING_KT_DGRAD);
+  const long kt_min = mode == MODE_FWD ? tune(T_RING_KT) : tune(T_RING_KT_DGRAD);
+  return (a.Kdim + 63) / 64 >= kt_min;
 }
 
 template <int MODE, int FLAGS, int BN>
