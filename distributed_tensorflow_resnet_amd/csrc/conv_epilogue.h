@@ -291,35 +291,21 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs& args, f32x4 (&acc
           (int)((((long)z * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16);
   int* flag = reinterpret_cast<int*>(smem);
   if (!last_arriver(args.sk_cnt + tile, (unsigned)S, flag)) return false;
-  f32x4 tot[MR][NR];
+  // sum every slice -- this one's too, read back from the slab it just wrote -- into acc,
+  // 0 + s0 + s1 + ... in slice order: the same fp32 sum as a separate total, without
+  // holding a second MR x NR register tile beside acc (that spilled the ring dgrad)
 #pragma unroll
   for (int a = 0; a < MR; ++a)
 #pragma unroll
-    for (int b = 0; b < NR; ++b) tot[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int zz = 0; zz < S; ++zz) {
-    if (zz == z) {
 #pragma unroll
-      for (int a = 0; a < MR; ++a)
+    for (int a = 0; a < MR; ++a)
 #pragma unroll
-        for (int b = 0; b < NR; ++b) tot[a][b] += acc[a][b];
-    } else {
-      f32x4 v[MR][NR];
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int b = 0; b < NR; ++b)
-          v[a][b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-              rs, (int)((((long)zz * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16));
-#pragma unroll
-      for (int a = 0; a < MR; ++a)
-#pragma unroll
-        for (int b = 0; b < NR; ++b) tot[a][b] += v[a][b];
-    }
+      for (int b = 0; b < NR; ++b)
+        acc[a][b] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+            rs, (int)((((long)zz * slab) + ((long)(a * NR + b) * 256 + tid) * 4) * 4), 0, 16));
   }
-#pragma unroll
-  for (int a = 0; a < MR; ++a)
-#pragma unroll
-    for (int b = 0; b < NR; ++b) acc[a][b] = tot[a][b];
   reset_counter(args.sk_cnt + tile);
   __syncthreads();   // the flag word's LDS is the epilogue's
   return true;
