@@ -1020,6 +1020,14 @@ PYBIND11_MODULE(_C, m) {
     g.Ncol = mode == MODE_FWD ? c.K : c.C;
     return conv_direct_covers(g, mode);
   }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
+  m.def("persist_stage_fwd", [](ptr_t x0, ptr_t bn0_scale, ptr_t bn0_shift, ptr_t w, ptr_t gamma,
+                                ptr_t beta, ptr_t y, ptr_t stats, ptr_t bar, ptr_t err, int N,
+                                int L, float eps, ptr_t stream) {
+    PersistArgs a{P<const bf16>(x0), P<const float>(bn0_scale), P<const float>(bn0_shift),
+                  P<const bf16>(w), P<const float>(gamma), P<const float>(beta), P<bf16>(y),
+                  P<float>(stats), P<unsigned>(bar), P<int>(err), N, L, eps};
+    persist_stage_fwd(a, S(stream));
+  }, "prototype: L chained CIFAR stage-3 convs (3x3 64->64, 8x8) in one persistent launch");
   m.def("conv_ring_covers", [](int mode, std::vector<int> geom) {
     GemmArgs g{};
     g.g = geom_from(geom);

@@ -163,6 +163,24 @@ void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s)
 bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 
+// Persistent multi-layer prototype (persist.hip): L chained 3x3 64 -> 64 convs on 8x8
+// maps (CIFAR stage 3) in one launch, grid barriers between layers.
+struct PersistArgs {
+  const bf16* x0;            // [N,8,8,64] stage input (pre-activation)
+  const float* bn0_scale;    // BN+ReLU of the first conv's input
+  const float* bn0_shift;
+  const bf16* w;             // [L][64 co][3][3][64 ci]
+  const float* gamma;        // [L][64]: BN of each conv's output (the next conv's input)
+  const float* beta;
+  bf16* y;                   // [L][N,8,8,64] conv outputs (odd layers: + block input)
+  float* stats;              // [L][2][64] batch sum / sum of squares, zeroed by the caller
+  unsigned* bar;             // grid-barrier counter, zeroed by the caller
+  int* err;                  // set on a timed-out barrier
+  int N, L;
+  float eps;
+};
+void persist_stage_fwd(const PersistArgs& a, hipStream_t s);
+
 struct WgradArgs {
   const bf16* dy;           // [N,Ho,Wo,K]
   const bf16* x;            // [N,H,W,C] (pre-BN tensor if pre_scale given)
