@@ -64,6 +64,10 @@ const TuneEntry kTable[T_COUNT] = {
     {"wt_store", -1,
      "conv epilogue write-through stores: -1 auto (direct convs writing >= 2 MB: bs128 step "
      "1.304 -> 1.282 ms), 0 off, 1 on"},
+    {"plan_event_scope", 2,
+     "plan fork/join events: 0 runtime default (system-scope release), 1 device-scope "
+     "release, 2 no marker fence (CIFAR RN50 bs128 1.305 -> 1.280 ms, bs16 0.951 -> 0.932; "
+     "1 = 0)"},
     {"ring", 1,
      "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128-row non-PRE convs (RN50 bs128 "
      "conv dgrads 4.51 -> 4.05 ms/step, forwards 3.94 -> 3.85)"},

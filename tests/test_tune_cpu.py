@@ -72,7 +72,8 @@ def test_every_tuning_entry_is_documented_with_its_default():
         assert rows[key] == str(dflt), f"{key}: README default {rows[key]!r} != {dflt!r}"
     # every tune key the native code uses is in the table (no orphan enum values)
     used = set()
-    for f in glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h")):
+    for f in (glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))
+              + glob.glob(os.path.join(PKG, "csrc", "*.cpp"))):
         used |= set(re.findall(r"\btune(?:_set)?\((T_[A-Z0-9_]+)", open(f).read()))
     hdr = open(os.path.join(PKG, "csrc", "tune.h")).read()
     declared = set(re.findall(r"^\s*(T_[A-Z0-9_]+)", hdr, re.M)) - {"T_COUNT"}
