@@ -477,6 +477,7 @@ void conv_wgrad(const WgradArgs& a, hipStream_t s) {
   else if (bm == 64 && bn == 64) wg_launch<64, 64, 2, 2>(a, s);
   else if (bm == 64) wg_launch<64, 128, 2, 2>(a, s);
   else if (bn == 64) wg_launch<128, 64, 2, 2>(a, s);
+  else if (conv_wgrad_ring_covers(a)) conv_wgrad_ring(a, s);
   else wg_launch<128, 128, 2, 2>(a, s);
 }
 

@@ -192,6 +192,10 @@ struct WgradArgs {
   int px_per_split;         // multiple of 64
   int wt = 0;               // partials stored write-through (direct kernel; set by the launcher)
 };
+// LDS-DMA ring weight gradient (conv_wgrad_ring.hip): 128 x 128 tiles, same splits / slabs
+bool conv_wgrad_ring_covers(const WgradArgs& a);
+void conv_wgrad_ring(const WgradArgs& a, hipStream_t s);
+
 void conv_wgrad(const WgradArgs& a, hipStream_t s);
 // Direct halo-tiled wgrad for 3x3/s1 small C (conv_wgrad_direct.hip).
 bool conv_wgrad_direct(const WgradArgs& a, hipStream_t s);

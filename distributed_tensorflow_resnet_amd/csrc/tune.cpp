@@ -68,6 +68,9 @@ const TuneEntry kTable[T_COUNT] = {
      "plan fork/join events: 0 runtime default (system-scope release), 1 device-scope "
      "release, 2 no marker fence (CIFAR RN50 bs128 1.305 -> 1.280 ms, bs16 0.951 -> 0.932; "
      "1 = 0)"},
+    {"ring_wgrad", 1,
+     "LDS-DMA ring weight gradient (conv_wgrad_ring.hip) for the 128x128 tiles (RN50 bs128 "
+     "wgrad kernels 4.68 -> 4.59 ms/step: no-PRE -5 %, PRE ties)"},
     {"ring", 1,
      "LDS-DMA ring implicit GEMM (conv_ring.hip) for the 128-row non-PRE convs (RN50 bs128 "
      "conv dgrads 4.51 -> 4.05 ms/step, forwards 3.94 -> 3.85)"},

@@ -754,3 +754,34 @@ def test_ring_conv_matches_register_loop_and_reference(gpu, mode, N, H, C, K, k,
     assert _rel(outs[1], outs[0]) < 2e-3
     assert _rel(outs[1], want) < 1e-2
     torch.testing.assert_close(sums[1], sums[0], rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("N,H,C,K,k,s", [(4, 28, 128, 128, 3, 1), (8, 14, 256, 256, 3, 2),
+                                         (4, 56, 256, 128, 1, 1), (16, 7, 512, 512, 3, 1),
+                                         (2, 14, 1024, 2048, 1, 2)])
+def test_ring_wgrad_matches_register_loop_and_reference(gpu, N, H, C, K, k, s):
+    """LDS-DMA ring weight gradient (conv_wgrad_ring.hip) with the BN+ReLU prologue
+    applied in LDS (padding taps stay zero) == the register-staged loop (tune
+    ring_wgrad=0) and the fp32 reference, over the split-K partial slabs + reduce."""
+    torch.manual_seed(22)
+    nat = fn.native()
+    dflt = {t[0]: t[1] for t in nat.tune_table()}
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    g = fn.ConvGeom(N, H, H, C, K, k, k, s)
+    dy = torch.randn(N, g.Ho, g.Wo, K, device=gpu).to(BF)
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
+    outs = []
+    for ring in (1, 0):
+        nat.tune_set("ring_wgrad", ring)
+        try:
+            gw = torch.empty(k, k, C, K, device=gpu)
+            fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc, pre_shift=sh)
+            torch.cuda.synchronize()
+        finally:
+            nat.tune_set("ring_wgrad", dflt["ring_wgrad"])
+        outs.append(gw.clone())
+    a = torch.relu(x.float() * sc + sh).to(BF).float()
+    wt = torch.zeros(k, k, C, K, device=gpu, requires_grad=True)
+    ref.conv2d(a, wt, s).backward(dy.float())
+    assert _rel(outs[0], outs[1]) < 1e-4
+    assert _rel(outs[0], wt.grad) < 1e-2
