@@ -32,6 +32,17 @@ __device__ __forceinline__ float bits2f(unsigned short u) {
 // D = A(16x32) * B(32x16) + C, bf16 inputs, fp32 accumulate.
 // Lane l holds A[l&15][8*(l>>4)+j] and B[8*(l>>4)+j][l&15], j=0..7;
 // C/D: col = l&15, row = 4*(l>>4)+i.
+// XCD-aware block order.  MI355X deals workgroups round-robin over its 8 XCDs (linear
+// block b to XCD b % 8, each XCD with its own L2): the logical block of physical block b
+// such that every XCD gets one contiguous range of logical blocks, so neighbouring
+// logical blocks that share operands share an L2.  Bijective for any grid size
+// (cdna_hip_programming.md, "XCD swizzle must be bijective"); placement is a speed
+// matter only, never correctness.
+__device__ __forceinline__ unsigned xcd_logical_block(unsigned b, unsigned nwg) {
+  const unsigned xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

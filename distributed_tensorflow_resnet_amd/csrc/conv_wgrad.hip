@@ -61,9 +61,13 @@ conv_wgrad_kernel(WgradArgs args) {
   const int P = g.N * g.Ho * g.Wo;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int n0 = blockIdx.x * BN;
-  const int m0 = blockIdx.y * BM;
-  const int split = blockIdx.z;
+  // (logical tile: args.xcd keeps a split's column tiles -- which read the same dy rows
+  // and x pixels -- on one XCD)
+  const unsigned pblk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned lblk = args.xcd ? xcd_logical_block(pblk, gridDim.x * gridDim.y * gridDim.z) : pblk;
+  const int n0 = (int)(lblk % gridDim.x) * BN;
+  const int m0 = (int)((lblk / gridDim.x) % gridDim.y) * BM;
+  const int split = (int)(lblk / (gridDim.x * gridDim.y));
   const int p_begin = split * args.px_per_split;
   const int p_end = min(P, p_begin + args.px_per_split);
 
@@ -467,8 +471,10 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   return (int)((P + pps - 1) / pps);
 }
 
-void conv_wgrad(const WgradArgs& a, hipStream_t s) {
-  if (conv_wgrad_direct(a, s)) return;
+void conv_wgrad(const WgradArgs& a0, hipStream_t s) {
+  if (conv_wgrad_direct(a0, s)) return;
+  WgradArgs a = a0;
+  a.xcd = tune(T_WGRAD_XCD) ? 1 : 0;
   int bm, bn;
   wg_tile(a.g, &bm, &bn);
   if (bm == 16) wg_launch<16, 64, 1, 4>(a, s);

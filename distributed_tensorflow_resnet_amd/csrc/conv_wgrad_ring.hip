@@ -54,8 +54,11 @@ conv_wgrad_ring_kernel(WgradArgs args) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int p_begin = blockIdx.z * args.px_per_split;
+  const unsigned pblk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned lblk = args.xcd ? xcd_logical_block(pblk, gridDim.x * gridDim.y * gridDim.z) : pblk;
+  const int n0 = (int)(lblk % gridDim.x) * BN, m0 = (int)((lblk / gridDim.x) % gridDim.y) * BM;
+  const int split = (int)(lblk / (gridDim.x * gridDim.y));
+  const int p_begin = split * args.px_per_split;
   const int p_end = min(P, p_begin + args.px_per_split);
   const int KT = (p_end - p_begin + BK - 1) / BK;
 
@@ -213,7 +216,7 @@ conv_wgrad_ring_kernel(WgradArgs args) {
     rd ^= 1;
   }
 
-  float* out = args.part + (long)blockIdx.z * Cout * NT;
+  float* out = args.part + (long)split * Cout * NT;
 #pragma unroll
   for (int b = 0; b < NR; ++b) {
     const int n = n0 + wn * WTN + b * 16 + li;

@@ -191,6 +191,7 @@ struct WgradArgs {
   int splits;
   int px_per_split;         // multiple of 64
   int wt = 0;               // partials stored write-through (direct kernel; set by the launcher)
+  int xcd = 0;               // 1: XCD-aware block order (the column tiles of one split share an L2)
 };
 // LDS-DMA ring weight gradient (conv_wgrad_ring.hip): 128 x 128 tiles, same splits / slabs
 bool conv_wgrad_ring_covers(const WgradArgs& a);

@@ -68,6 +68,9 @@ const TuneEntry kTable[T_COUNT] = {
      "plan fork/join events: 0 runtime default (system-scope release), 1 device-scope "
      "release, 2 no marker fence (CIFAR RN50 bs128 1.305 -> 1.280 ms, bs16 0.951 -> 0.932; "
      "1 = 0)"},
+    {"wgrad_xcd", 1,
+     "XCD-aware block order of the split-K weight gradients (RN50 bs128 wgrads 4.31 -> 4.11 "
+     "ms/step in-process, step 12.18 -> 12.09 ms)"},
     {"ring_wgrad", 1,
      "LDS-DMA ring weight gradient (conv_wgrad_ring.hip) for the 128x128 tiles (RN50 bs128 "
      "wgrad kernels 4.68 -> 4.59 ms/step: no-PRE -5 %, PRE ties)"},

@@ -38,6 +38,7 @@ enum TuneId : int {
   T_BWD_APPLY_FIN,     // BN backward apply finalizes in-kernel when the grid allows
   T_WT_STORE,          // conv epilogue write-through stores (-1 auto, 0 off, 1 on)
   T_PLAN_EVENT_SCOPE,  // release scope of the plan's fork/join events
+  T_WGRAD_XCD,         // XCD-aware block order of the split-K weight gradients
   T_RING_WGRAD,        // LDS-DMA ring weight gradient (conv_wgrad_ring.hip), 128x128 tiles
   T_RING,              // LDS-DMA ring implicit GEMM (conv_ring.hip) for eligible convs
   T_RING_KT,           // ... forward convs with K loops of at least this many 64-deep tiles
