@@ -71,16 +71,36 @@ conv_ring_kernel(GemmArgs args) {
   constexpr int WM = BN == 128 ? 2 : 4, WN = 4 / WM;
   constexpr int MR = BM / WM / 16, NR = BN / WN / 16;
   static_assert(BM * BK * 2 == STAGE_A_BYTES, "A tile bytes");   // stage: A, then B (BN x BK)
-  constexpr bool BNB = (FLAGS & F_BNB) != 0;
+  constexpr bool BNB = (FLAGS & (F_BNB | F_BAPPLY)) != 0;   // BN-input rows in the epilogue
   static_assert((FLAGS & (F_PRE | F_ABWD)) == 0, "no A-operand prologue on the ring");
   static_assert(BN == 128 || BN == 64, "128 x 128 or 128 x 64 tiles");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ConvGeom& g = args.g;
+  // logical (row tile, column tile, slice / parity class) of this workgroup: the
+  // hardware's, or (args.xcd) an XCD-aware order -- workgroups are dealt round-robin to
+  // the 8 XCDs (block b to XCD b % 8, each with its own L2); xcd_logical_block gives
+  // every XCD one contiguous range of logical tiles, ordered so that neighbours share
+  // operands: 1 = the column tiles of a row tile adjacent (same A rows), 2 = row tiles.
+  int tm = blockIdx.x, tn = blockIdx.y, lz = blockIdx.z;
+  if (args.xcd) {
+    const unsigned gx = gridDim.x, gy = gridDim.y, gxy = gx * gy;
+    const unsigned L = xcd_logical_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z),
+                                         gxy * gridDim.z);
+    lz = (int)(L / gxy);
+    const unsigned r = L - (unsigned)lz * gxy;
+    if (args.xcd == 1) {
+      tm = (int)(r / gy);
+      tn = (int)(r - (unsigned)tm * gy);
+    } else {
+      tn = (int)(r / gx);
+      tm = (int)(r - (unsigned)tn * gx);
+    }
+  }
   int par_ph = 0, par_pw = 0;
   if (MODE == MODE_DGRAD && args.par) {   // stride-2 dgrad parity class (see conv_gemm.hip)
-    par_ph = blockIdx.z >> 1;
-    par_pw = blockIdx.z & 1;
+    par_ph = lz >> 1;
+    par_pw = lz & 1;
     args.par_h0 = (par_ph + g.pad) & 1;
     args.par_w0 = (par_pw + g.pad) & 1;
     args.par_hc = (g.H - args.par_h0 + 1) >> 1;
@@ -89,7 +109,7 @@ conv_ring_kernel(GemmArgs args) {
     args.Kdim = ((g.kh - par_ph + 1) >> 1) * ((g.kw - par_pw + 1) >> 1) * g.K;
   }
   const int M = args.M, NC = args.Ncol, KD = args.Kdim;
-  if (MODE == MODE_DGRAD && args.par && (int)(blockIdx.x * BM) >= M) return;
+  if (MODE == MODE_DGRAD && args.par && tm * BM >= M) return;
   const bool par = MODE == MODE_DGRAD && args.par;
   // taps of this launch (class): rows ta < tah, columns tb < taw
   const int taw = par ? (g.kw - par_pw + 1) >> 1 : g.kw;
@@ -97,7 +117,6 @@ conv_ring_kernel(GemmArgs args) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int tm = blockIdx.x, tn = blockIdx.y;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- per-lane gather state: rows (wave * 4 + i) * 8 + lane / 8, chunk kg ----
@@ -179,7 +198,7 @@ conv_ring_kernel(GemmArgs args) {
 
   // ---- K range of this split-K slice; scalar tap walk of the issue pointer ----
   const int KT_all = (KD + BK - 1) / BK;
-  const int sk_n = args.ksplit > 1 ? args.ksplit : 1, sk_z = sk_n > 1 ? (int)blockIdx.z : 0;
+  const int sk_n = args.ksplit > 1 ? args.ksplit : 1, sk_z = sk_n > 1 ? lz : 0;
   const int t_beg = (int)(((long)sk_z * KT_all) / sk_n);
   const int t_end = (int)(((long)(sk_z + 1) * KT_all) / sk_n);
   const int cpt = Acin / BK;                       // K tiles per tap
@@ -273,7 +292,7 @@ conv_ring_kernel(GemmArgs args) {
   }
   __syncthreads();   // every wave's MFMA reads are done: the epilogue reuses the LDS
 
-  if (sk_n > 1 && !splitk_combine<MR, NR>(args, acc, smem, tm, tn)) return;
+  if (sk_n > 1 && !splitk_combine<MR, NR>(args, acc, smem, tm, tn, lz)) return;
   if constexpr (BNB && EP::ON)
     conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre, tm, tn);
   else
@@ -303,6 +322,7 @@ bool conv_ring_covers(const GemmArgs& a, int mode) {
 template <int MODE, int FLAGS, int BN>
 static void ring_launch(GemmArgs a, dim3 grid, hipStream_t s) {
   constexpr int WM = BN == 128 ? 2 : 4;
+  a.xcd = (int)tune(T_RING_XCD);
   const size_t lds = std::max((size_t)2 * (128 + BN) * 64 * 2, EpiLayout<128, BN, WM>::BYTES);
   hipLaunchKernelGGL((conv_ring_kernel<MODE, FLAGS, BN>), grid, dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();
@@ -314,7 +334,8 @@ static void ring_flags(const GemmArgs& a, int mode, int flags, dim3 grid, hipStr
     if (flags & F_STATS) ring_launch<MODE_FWD, F_STATS, BN>(a, grid, s);
     else ring_launch<MODE_FWD, 0, BN>(a, grid, s);
   } else {
-    if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, BN>(a, grid, s);
+    if (flags & F_BAPPLY) ring_launch<MODE_DGRAD, F_BAPPLY, BN>(a, grid, s);
+    else if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, BN>(a, grid, s);
     else ring_launch<MODE_DGRAD, 0, BN>(a, grid, s);
   }
 }

@@ -114,6 +114,9 @@ struct GemmArgs {
   const float* bnb_scale;
   const float* bnb_shift;
   float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
+  // optional [3][Ncol] BN-backward apply coefficients (a, b, c): with bnb_x the dgrad
+  // epilogue writes dx = a*g - b - c*xhat (+ residual) instead of g (F_BAPPLY)
+  const float* bap_coef;
   BnFwdFin fin;             // with stat_part: finalize in-kernel
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
   // Accumulator mode of STATS / BNB: instead of (or beside) the per-tile partials,
@@ -130,6 +133,7 @@ struct GemmArgs {
   int M, Ncol, Kdim;
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
   int wt = 0;                   // epilogue output stores write-through (sc1): tune wt_store
+  int xcd = 0;                  // ring convs: XCD-aware tile order (tune ring_xcd, conv_ring.hip)
   // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
   // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
   // (sk_cnt) sums the slices in slice order and runs the epilogue

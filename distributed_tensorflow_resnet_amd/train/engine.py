@@ -619,14 +619,39 @@ class Engine:
         for n in names:
             self.ready_index[n] = idx
 
+    def _bap_ok(self, c: _Conv, N) -> bool:
+        """Whether the first 1x1 dgrad of an identity bottleneck block emits its input
+        BatchNorm's backward output itself (_conv_bwd ``bap``): accumulator-mode sums,
+        an implicit-GEMM stride-1 dgrad, and the block's wide input channels within
+        the ``bap_maxc`` bound (0 = off)."""
+        s = c.spec
+        maxc = tune.get("bap_maxc")
+        if not (self.bn_bacc_on and maxc > 0 and c.cin <= maxc):
+            return False
+        if s.kh != 1 or s.kw != 1 or s.stride != 1 or c.cin < 64 or c.cin % 64:
+            return False
+        return not self.nat.conv_direct_covers(1, self._geom(c, N))
+
     def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False,
-                  bnb: tuple | None = None, side: bool = True):
+                  bnb: tuple | None = None, side: bool = True, bap: tuple | None = None):
         """dgrad into dx (optional), then wgrad (+ reduce into the flat gradient).
 
         ``bnb=(bn, bn_input)``: the dgrad epilogue also emits that BN's backward
         partial sums (sum g, sum g*xhat of dx).  If ``dy`` is the output of a
         pending BN backward (_bn_bwd), the direct dgrad applies that BN backward
-        while staging dy (BnBwdPre) and materializes dy for the wgrad."""
+        while staging dy (BnBwdPre) and materializes dy for the wgrad.
+
+        ``bap=(bn, add)`` (bn's input is ``x``, the 1x1 conv's own input): dx receives
+        the BN+ReLU backward OUTPUT, BNbwd(dgrad) + add, with no separate apply pass.
+        The dgrad runs twice: a first pass only sums (sum g, sum g*xhat into the fp64
+        accumulators, no store), a finalize turns the sums into the apply coefficients,
+        and the second pass recomputes the same GEMM tile (bitwise the same fp32
+        values: same kernel schedule) and applies BN backward + add in its epilogue.
+        For a bottleneck block's first conv the GEMM is narrow (K = 64..512 input
+        rows), while the BN'd tensor is wide (256..2048 channels): recomputing it
+        costs less than writing the wide gradient, re-reading it and x, and writing
+        dx in a separate apply (reference: FusedBatchNormGrad after
+        Conv2DBackpropInput, resnet_model_official.py:133-175)."""
         geom = self._geom(c, N)
         s = c.spec
         abw = []
@@ -658,7 +683,25 @@ class Engine:
                 a_src = pb["da"]        # the dgrad stages BNbwd(da) and writes dy itself
             else:
                 self._emit_bn_bwd(plan)
-        if dx is not None:
+        if dx is not None and bap is not None:
+            bn, add = bap
+            self.n_bap += 1
+            assert not abw, "bap: the dgrad's input is not a pending BN-backward output"
+            M, C = N * s.h * s.w, c.cin
+            bl = [x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
+                  bn.shift.data_ptr()]
+            # pass 1: sums only (out = 0)
+            plan.conv_gemm(1, a_src.data_ptr(), c.hwio, 0, 0, 0, 0, 0, 0, 0, 0, 0, geom,
+                           bl + [bn.bpart.data_ptr()], [], [bn.bacc.data_ptr()], [], [],
+                           BN_DECAY, BN_EPS, 1)
+            plan.bn_bwd_finalize(bn.bacc.data_ptr(), -1, M, C, bn.gamma, bn.rstd.data_ptr(),
+                                 bn.dgamma, bn.dbeta, self.coef.data_ptr())
+            self._produced.update(bn.names)
+            # pass 2: the same GEMM, BN backward + add applied in the epilogue
+            plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0,
+                           0 if add is None else add.data_ptr(), 0, 0, 0, 0, 0, 0, geom,
+                           bl + [0, self.coef.data_ptr()], [], [], [], [], BN_DECAY, BN_EPS, 1)
+        elif dx is not None:
             bl, bfl = [], []
             if bnb is not None:
                 bn, bx = bnb
@@ -1006,6 +1049,7 @@ class Engine:
         self._main_wgrad = self.fork_wgrad and not self._head_fused
         self._pending_bwd, self._bnb_src = None, None
         self._reduce_main = False
+        self.n_bap = 0   # identity blocks whose first dgrad applies its BN backward (bap)
         dg = self._dense_geom(N)
         off, spl, pps = self.wg_off["dense"]
         dpart = self.wg_part.data_ptr() + 4 * off
@@ -1065,15 +1109,19 @@ class Engine:
                 dh1 = self._g(o2, tuple(h1.shape))
                 self._bn_bwd(plan, bns[1], da, h1, dh1, reduced=True)
                 dcur = dh1
-            da1 = self._g(o1, tuple(X.shape))
             proj = b.proj is not None
-            self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=da1,
-                           bnb=None if proj else (bns[0], X))
-            if proj:
-                self._conv_bwd(plan, self.convs[b.proj.name], dout, X, N, bns[0], dx=da1,
-                               accumulate=True, bnb=(bns[0], X))
             dx = self._g(o2, tuple(X.shape))
-            self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
+            if not proj and b.kind != "building" and self._bap_ok(convs[0], N):
+                # identity bottleneck: conv1's dgrad emits BNbwd(.) + dout itself
+                self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=dx, bap=(bns[0], dout))
+            else:
+                da1 = self._g(o1, tuple(X.shape))
+                self._conv_bwd(plan, convs[0], dcur, X, N, bns[0], dx=da1,
+                               bnb=None if proj else (bns[0], X))
+                if proj:
+                    self._conv_bwd(plan, self.convs[b.proj.name], dout, X, N, bns[0], dx=da1,
+                                   accumulate=True, bnb=(bns[0], X))
+                self._bn_bwd(plan, bns[0], da1, X, dx, add=None if proj else dout, reduced=True)
             dout, d = dx, o2
             if i == 0 and self._split_tail_on():
                 main_tail = self._split_tail(plan)

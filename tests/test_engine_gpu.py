@@ -211,6 +211,29 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
     assert _rel(t1, t0) < 1e-5
 
 
+def test_bn_backward_apply_recompute_matches_separate_apply(gpu, monkeypatch):
+    """tune bap_maxc: the identity bottleneck blocks' first 1x1 dgrad runs twice (sums, then
+    BN+ReLU backward + the residual gradient applied in the epilogue) instead of dgrad +
+    a separate BN-backward apply.  Same arithmetic on the same fp32 GEMM values: the
+    step's loss, gradients and BN statistics are bitwise equal."""
+    spec = imagenet_spec(50, image_hw=64)
+    res = {}
+    for mode in ("0", "2048"):  # (default 0)
+        monkeypatch.setenv("DTR_TUNE", f"bap_maxc={mode}")
+        eng, _, _, _ = _make(spec, 8, gpu)
+        st = torch.cuda.current_stream().cuda_stream
+        eng._run("fwd", st)
+        eng._run("bwd", st)
+        torch.cuda.synchronize()
+        res[mode] = (eng.scalars[0].item(), eng.grad.clone(), eng.params.stats.clone(),
+                     eng.n_bap)
+    (l0, g0, s0, n0), (l1, g1, s1, n1) = res["0"], res["2048"]
+    assert (n0, n1) == (0, 12)   # RN50: 3 + 4 + 6 + 3 blocks, one projection block each
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    assert torch.equal(s1, s0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec_fn,N,fork_every", [
     (lambda: cifar_spec(50), 16, "2"),
