@@ -194,6 +194,19 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   return [g, mode](hipStream_t s) { conv_gemm(g, mode, s); };
 }
 
+// [dz, w, x, add, out, mean, rstd, scale, shift, coef, bacc]: bn_dgrad1x1.hip
+static Launch mk_bnd1x1(int mode, std::vector<ptr_t> p, int M, int C, int K) {
+  if (p.size() != 11) throw std::invalid_argument("bnd1x1 needs 11 pointers");
+  if (!bnd1x1_covers(M, C, K))
+    throw std::invalid_argument("bnd1x1: needs K in {64, 128, 256}, C % slice == 0, M % row tile == 0");
+  if (mode == 0 && p[10] == 0) throw std::invalid_argument("bnd1x1 sums need bacc");
+  if (mode == 1 && (p[4] == 0 || p[9] == 0)) throw std::invalid_argument("bnd1x1 apply needs out, coef");
+  BndArgs a{P<const bf16>(p[0]), P<const bf16>(p[1]), P<const bf16>(p[2]), P<const bf16>(p[3]),
+            P<bf16>(p[4]), P<const float>(p[5]), P<const float>(p[6]), P<const float>(p[7]),
+            P<const float>(p[8]), P<const float>(p[9]), P<double>(p[10]), M, C, K};
+  return [a, mode](hipStream_t s) { bnd1x1(a, mode, s); };
+}
+
 static Launch mk_conv_wgrad(ptr_t dy, ptr_t x, ptr_t pre_scale, ptr_t pre_shift, ptr_t part,
                             std::vector<int> geom, int splits, int px_per_split) {
   WgradArgs w{};
@@ -998,6 +1011,8 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "bn_stats", mk_bn_stats);
   def_op(m, plan, "bn_bwd_reduce", mk_bn_bwd_reduce);
   def_op(m, plan, "bn_bwd_finalize", mk_bn_bwd_finalize);
+  def_op(m, plan, "bnd1x1", mk_bnd1x1);
+  m.def("bnd1x1_covers", &bnd1x1_covers, "whether the streaming narrow-K 1x1 dgrad + BN backward covers (M, C, K)");
   def_op(m, plan, "bn_bwd_apply", mk_bn_bwd_apply);
   def_op(m, plan, "bn_relu_apply", mk_bn_relu_apply);
   def_op(m, plan, "bn_relu_apply_acc", mk_bn_relu_apply_acc);

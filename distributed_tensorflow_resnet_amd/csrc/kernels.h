@@ -148,6 +148,26 @@ struct GemmArgs {
   int par_h0 = 0, par_w0 = 0, par_hc = 0, par_wc = 0;
 };
 
+// Streaming 1x1 dgrad with a narrow reduction (K = 64..256) fused with the BN+ReLU
+// backward of its wide output (bn_dgrad1x1.hip): mode 0 sums (sum g, sum g*xhat) into
+// bacc, mode 1 writes dx = a*g - b - c*xhat (+ add) with coef = (a, b, c).
+struct BndArgs {
+  const bf16* dz;           // [M][K] the 1x1 conv's output gradient
+  const bf16* w;            // [C][K] dgrad weights (HWIO of the 1x1 conv)
+  const bf16* x;            // [M][C] BN input
+  const bf16* add;          // optional [M][C] added to dx (mode 1)
+  bf16* out;                // [M][C] dx (mode 1)
+  const float* mean;
+  const float* rstd;
+  const float* scale;
+  const float* shift;
+  const float* coef;        // [3][C] (mode 1)
+  double* bacc;             // [BN_ACC_REP][2][C] (mode 0)
+  int M, C, K;
+};
+bool bnd1x1_covers(int M, int C, int K);
+void bnd1x1(const BndArgs& a, int mode, hipStream_t s);
+
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 void set_conv_splitk(int max_slices);   // split-K of under-filled FAST grids (1 = off)
 void set_conv_parity(int enabled);      // stride-2 dgrads by output parity class

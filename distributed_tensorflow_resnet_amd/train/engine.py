@@ -690,17 +690,28 @@ class Engine:
             M, C = N * s.h * s.w, c.cin
             bl = [x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
                   bn.shift.data_ptr()]
-            # pass 1: sums only (out = 0)
-            plan.conv_gemm(1, a_src.data_ptr(), c.hwio, 0, 0, 0, 0, 0, 0, 0, 0, 0, geom,
-                           bl + [bn.bpart.data_ptr()], [], [bn.bacc.data_ptr()], [], [],
-                           BN_DECAY, BN_EPS, 1)
+            if self.nat.bnd1x1_covers(M, C, s.cout):
+                # narrow K (64 / 128): the streaming kernel (bn_dgrad1x1.hip) runs both passes
+                base = [a_src.data_ptr(), c.hwio, x.data_ptr()]
+                bnp = bl[1:]
+                plan.bnd1x1(0, base + [0, 0] + bnp + [0, bn.bacc.data_ptr()], M, C, s.cout)
+            else:
+                # pass 1: the implicit-GEMM dgrad, sums only (out = 0)
+                plan.conv_gemm(1, a_src.data_ptr(), c.hwio, 0, 0, 0, 0, 0, 0, 0, 0, 0, geom,
+                               bl + [bn.bpart.data_ptr()], [], [bn.bacc.data_ptr()], [], [],
+                               BN_DECAY, BN_EPS, 1)
             plan.bn_bwd_finalize(bn.bacc.data_ptr(), -1, M, C, bn.gamma, bn.rstd.data_ptr(),
                                  bn.dgamma, bn.dbeta, self.coef.data_ptr())
             self._produced.update(bn.names)
-            # pass 2: the same GEMM, BN backward + add applied in the epilogue
-            plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0,
-                           0 if add is None else add.data_ptr(), 0, 0, 0, 0, 0, 0, geom,
-                           bl + [0, self.coef.data_ptr()], [], [], [], [], BN_DECAY, BN_EPS, 1)
+            addp = 0 if add is None else add.data_ptr()
+            if self.nat.bnd1x1_covers(M, C, s.cout):
+                plan.bnd1x1(1, base + [addp, dx.data_ptr()] + bnp + [self.coef.data_ptr(), 0], M,
+                            C, s.cout)
+            else:
+                # pass 2: the same GEMM, BN backward + add applied in the epilogue
+                plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0, addp, 0, 0, 0, 0,
+                               0, 0, geom, bl + [0, self.coef.data_ptr()], [], [], [], [],
+                               BN_DECAY, BN_EPS, 1)
         elif dx is not None:
             bl, bfl = [], []
             if bnb is not None:

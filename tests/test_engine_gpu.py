@@ -213,9 +213,10 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
 
 def test_bn_backward_apply_recompute_matches_separate_apply(gpu, monkeypatch):
     """tune bap_maxc: the identity bottleneck blocks' first 1x1 dgrad runs twice (sums, then
-    BN+ReLU backward + the residual gradient applied in the epilogue) instead of dgrad +
-    a separate BN-backward apply.  Same arithmetic on the same fp32 GEMM values: the
-    step's loss, gradients and BN statistics are bitwise equal."""
+    BN+ReLU backward + the residual gradient applied in the second pass) instead of dgrad +
+    a separate BN-backward apply -- by the streaming kernel where K <= 128 (stages 1-2),
+    by the implicit-GEMM dgrad's apply epilogue elsewhere.  Same forward (loss, BN
+    statistics bitwise); gradients equal up to the BN-backward sums' summation order."""
     spec = imagenet_spec(50, image_hw=64)
     res = {}
     for mode in ("0", "2048"):  # (default 0)
@@ -230,8 +231,20 @@ def test_bn_backward_apply_recompute_matches_separate_apply(gpu, monkeypatch):
     (l0, g0, s0, n0), (l1, g1, s1, n1) = res["0"], res["2048"]
     assert (n0, n1) == (0, 12)   # RN50: 3 + 4 + 6 + 3 blocks, one projection block each
     assert l1 == l0
-    assert torch.equal(g1, g0)
     assert torch.equal(s1, s0)
+    # stage 4 (K = 512: the implicit-GEMM apply epilogue, bitwise the separate apply), the
+    # final BN and the dense layer: bitwise.  Stages 1-3 (the streaming kernel's BN-backward
+    # sums in another order): up to rounding, amplified through the stem-ward layers like
+    # any sum-order change (cf. test_bn_accumulator_mode_matches_partials).
+    late = set()
+    for b in spec.blocks[13:]:
+        late.update(x.name for x in list(b.bns) + list(b.convs) + ([b.proj] if b.proj else []))
+    store = ParamStore(spec)
+    first = min(sl.offset for sl in store.train_slots
+                if sl.name.split("/")[0] in late)
+    assert torch.equal(g1[first:], g0[first:])
+    assert not torch.equal(g1[:first], g0[:first])
+    assert _rel(g1, g0) < 2e-2
 
 
 @pytest.mark.gpu

@@ -854,3 +854,63 @@ def test_dgrad_bn_backward_apply_epilogue(gpu, N, H, C, K, with_add):
     if add is not None:
         dx_ref = dx_ref + add.float().reshape(-1, C)
     assert _rel(got.reshape(-1, C), dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,K", [(8, 56, 256, 64), (8, 28, 512, 128), (2, 4, 256, 64),
+                                     (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 128, 256)])
+def test_streaming_narrow_dgrad_bn_backward(gpu, N, H, C, K):
+    """bnd1x1 (bn_dgrad1x1.hip): the sums pass == the implicit-GEMM dgrad's BN-backward
+    sums (fp64 accumulators) to fp32 rounding, and the apply pass == bn_bwd_apply of the
+    dgrad's stored gradient bitwise for the same coefficients (same MFMA order, same
+    bf16 rounding of g, same apply arithmetic); dx == the fp32 reference."""
+    torch.manual_seed(23)
+    nat = fn.native()
+    st = torch.cuda.current_stream().cuda_stream
+    M = N * H * H
+    assert nat.bnd1x1_covers(M, C, K)
+    g = fn.ConvGeom(N, H, H, C, K, 1, 1, 1)
+    dz = torch.randn(N, H, H, K, device=gpu).to(BF)
+    w = (torch.randn(1, 1, C, K, device=gpu) / math.sqrt(K)).to(BF)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    add = torch.randn(N, H, H, C, device=gpu).to(BF)
+    mean = torch.randn(C, device=gpu) * 0.1
+    rstd = torch.rand(C, device=gpu) + 0.5
+    gamma = torch.rand(C, device=gpu) + 0.5
+    sc, sh = gamma * rstd, torch.randn(C, device=gpu) * 0.2 - mean * gamma * rstd
+    rep = nat.bn_acc_rep()
+    # reference path: implicit-GEMM dgrad with BNB sums, finalize, separate apply
+    bacc1 = torch.zeros(rep * 2 * C, device=gpu, dtype=torch.float64)
+    part = torch.zeros((M // 16 + 1) * 2 * C, device=gpu)
+    da = torch.empty(N, H, H, C, device=gpu, dtype=BF)
+    nat.conv_gemm(1, dz.data_ptr(), w.data_ptr(), da.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
+                  g.as_list(), [x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(),
+                                sh.data_ptr(), part.data_ptr()], [], [bacc1.data_ptr()], [], [],
+                  0.997, ref.BN_EPS, 1, st)
+    coef1 = torch.empty(3 * C, device=gpu)
+    dgb1 = torch.empty(2 * C, device=gpu)
+    nat.bn_bwd_finalize(bacc1.data_ptr(), -1, M, C, gamma.data_ptr(), rstd.data_ptr(),
+                        dgb1.data_ptr(), dgb1.data_ptr() + 4 * C, coef1.data_ptr(), st)
+    want = torch.empty_like(da)
+    nat.bn_bwd_apply(da.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(),
+                     sh.data_ptr(), coef1.data_ptr(), add.data_ptr(), want.data_ptr(), M, C, st)
+    # streaming kernel: sums, then apply with the reference coefficients
+    bacc2 = torch.zeros_like(bacc1)
+    base = [dz.data_ptr(), w.data_ptr(), x.data_ptr()]
+    bnp = [mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(), sh.data_ptr()]
+    nat.bnd1x1(0, base + [0, 0] + bnp + [0, bacc2.data_ptr()], M, C, K, st)
+    got = torch.full_like(da, float("nan"))
+    nat.bnd1x1(1, base + [add.data_ptr(), got.data_ptr()] + bnp + [coef1.data_ptr(), 0], M, C, K,
+               st)
+    torch.cuda.synchronize()
+    s1 = bacc1.view(rep, 2, C).sum(0)
+    s2 = bacc2.view(rep, 2, C).sum(0)
+    scale_ = s1.abs().max().item() + 1.0
+    assert (s2 - s1).abs().max().item() <= 1e-5 * scale_
+    torch.testing.assert_close(got.float(), want.float(), rtol=0, atol=0)
+    dxt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
+    ref.conv2d(dxt, w.float(), 1).backward(dz.float())
+    xf, gf = x.float().reshape(-1, C), dxt.grad.reshape(-1, C)
+    gg = gf * ((xf * sc + sh) > 0).float()
+    xh = (xf - mean) * rstd
+    dx_ref = gamma * rstd * (gg - gg.mean(0) - xh * (gg * xh).mean(0)) + add.float().reshape(-1, C)
+    assert _rel(got.reshape(-1, C), dx_ref) < 1e-2
