@@ -77,26 +77,7 @@ conv_ring_kernel(GemmArgs args) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ConvGeom& g = args.g;
-  // logical (row tile, column tile, slice / parity class) of this workgroup: the
-  // hardware's, or (args.xcd) an XCD-aware order -- workgroups are dealt round-robin to
-  // the 8 XCDs (block b to XCD b % 8, each with its own L2); xcd_logical_block gives
-  // every XCD one contiguous range of logical tiles, ordered so that neighbours share
-  // operands: 1 = the column tiles of a row tile adjacent (same A rows), 2 = row tiles.
-  int tm = blockIdx.x, tn = blockIdx.y, lz = blockIdx.z;
-  if (args.xcd) {
-    const unsigned gx = gridDim.x, gy = gridDim.y, gxy = gx * gy;
-    const unsigned L = xcd_logical_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z),
-                                         gxy * gridDim.z);
-    lz = (int)(L / gxy);
-    const unsigned r = L - (unsigned)lz * gxy;
-    if (args.xcd == 1) {
-      tm = (int)(r / gy);
-      tn = (int)(r - (unsigned)tm * gy);
-    } else {
-      tn = (int)(r / gx);
-      tm = (int)(r - (unsigned)tn * gx);
-    }
-  }
+  const int tm = blockIdx.x, tn = blockIdx.y, lz = blockIdx.z;
   int par_ph = 0, par_pw = 0;
   if (MODE == MODE_DGRAD && args.par) {   // stride-2 dgrad parity class (see conv_gemm.hip)
     par_ph = lz >> 1;
@@ -322,7 +303,6 @@ bool conv_ring_covers(const GemmArgs& a, int mode) {
 template <int MODE, int FLAGS, int BN>
 static void ring_launch(GemmArgs a, dim3 grid, hipStream_t s) {
   constexpr int WM = BN == 128 ? 2 : 4;
-  a.xcd = (int)tune(T_RING_XCD);
   const size_t lds = std::max((size_t)2 * (128 + BN) * 64 * 2, EpiLayout<128, BN, WM>::BYTES);
   hipLaunchKernelGGL((conv_ring_kernel<MODE, FLAGS, BN>), grid, dim3(256), lds, s, a);
   DTR_CHECK_LAUNCH();

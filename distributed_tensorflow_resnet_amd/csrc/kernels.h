@@ -133,7 +133,6 @@ struct GemmArgs {
   int M, Ncol, Kdim;
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
   int wt = 0;                   // epilogue output stores write-through (sc1): tune wt_store
-  int xcd = 0;                  // ring convs: XCD-aware tile order (tune ring_xcd, conv_ring.hip)
   // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
   // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
   // (sk_cnt) sums the slices in slice order and runs the epilogue

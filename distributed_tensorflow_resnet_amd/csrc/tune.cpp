@@ -83,10 +83,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"ring_kt_dgrad", 4,
      "ring dgrads from this many 64-deep K tiles (the 4-tile 14x14 1024->256 dgrad: 75.8 -> "
      "68.8 us on the ring)"},
-    {"ring_xcd", 0,
-     "XCD-aware tile order of the ring convs: each XCD (own 4 MB L2) walks one contiguous "
-     "range of tiles, 1 = column tiles of a row tile adjacent (they share the A rows), 2 = "
-     "row tiles adjacent; 0 = hardware round-robin"},
 };
 
 std::atomic<long> g_val[T_COUNT];

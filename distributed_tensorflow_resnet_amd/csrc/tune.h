@@ -43,7 +43,6 @@ enum TuneId : int {
   T_RING,              // LDS-DMA ring implicit GEMM (conv_ring.hip) for eligible convs
   T_RING_KT,           // ... forward convs with K loops of at least this many 64-deep tiles
   T_RING_KT_DGRAD,     // ... dgrads with K loops of at least this many tiles
-  T_RING_XCD,          // XCD-aware tile order of the ring convs (0 off, 1 column-fastest, 2 row)
   T_COUNT
 };
 

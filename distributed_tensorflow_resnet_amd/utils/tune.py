@@ -34,11 +34,12 @@ ENGINE = {
                       "sums) instead of eight"),
     "mat_bn_elems": (7000000, "inner bottleneck BN-ReLU materialized once (instead of applied in "
                               "the consumer's staging) up to this many elements ..."),
-    "bap_maxc": (1024, "identity bottleneck blocks whose input has <= this many channels run "
-                          "their first 1x1 dgrad twice (sums, then BN backward + add in the "
-                          "second pass; the streaming bn_dgrad1x1 kernel for K <= 256) instead "
-                          "of dgrad + a separate BN-backward apply (RN50 bs128 stages 1-2: "
-                          "12.14 -> 11.91 ms); 0 off"),
+    "bap_maxc": (512, "identity bottleneck blocks whose input has <= this many channels run "
+                         "their first 1x1 dgrad twice (sums, then BN backward + add in the "
+                         "second pass; the streaming bn_dgrad1x1 kernel for K <= 256) instead "
+                         "of dgrad + a separate BN-backward apply (RN50 bs128: 12.15 -> 11.67 "
+                         "ms at 512 = stages 1-2; 11.87 at 1024: the K = 256 stage-3 pass "
+                         "pair 110 vs 97 us unfused); 0 off"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 
