@@ -207,6 +207,38 @@ static Launch mk_bnd1x1(int mode, std::vector<ptr_t> p, int M, int C, int K) {
   return [a, mode](hipStream_t s) { bnd1x1(a, mode, s); };
 }
 
+// [x, w, res, out, pre_scale, pre_shift, stat_acc]; pfin = conv_gemm's 12-entry list in
+// accumulator mode (cnt == -1) or empty: bn_fwd1x1.hip
+static Launch mk_bnf1x1(std::vector<ptr_t> p, std::vector<ptr_t> pfin, int M, int C, int K,
+                        float momentum, float eps, int update_moving) {
+  if (p.size() != 7) throw std::invalid_argument("bnf1x1 needs 7 pointers");
+  if (!bnf1x1_covers(M, C, K))
+    throw std::invalid_argument("bnf1x1: needs K in {64, 128, 256}, C % 256 == 0, M % row tile == 0");
+  if (p[3] == 0 || p[1] == 0 || p[0] == 0) throw std::invalid_argument("bnf1x1: x, w, out needed");
+  BnfArgs a{};
+  a.x = P<const bf16>(p[0]);
+  a.w = P<const bf16>(p[1]);
+  a.res = P<const bf16>(p[2]);
+  a.out = P<bf16>(p[3]);
+  a.pre_scale = P<const float>(p[4]);
+  a.pre_shift = P<const float>(p[5]);
+  a.stat_acc = P<double>(p[6]);
+  a.M = M;
+  a.C = C;
+  a.K = K;
+  if (!pfin.empty()) {
+    if (pfin.size() != 12 || (int)pfin[1] != -1)
+      throw std::invalid_argument("bnf1x1: pfin must be the 12-entry accumulator-mode list");
+    a.pfin = BnPreFin{nullptr, 1, P<const double>(pfin[0]), (int)pfin[2], (int)pfin[3],
+                      P<const float>(pfin[4]), P<const float>(pfin[5]), P<float>(pfin[6]),
+                      P<float>(pfin[7]), P<float>(pfin[8]), P<float>(pfin[9]),
+                      P<float>(pfin[10]), P<float>(pfin[11]), momentum, eps, update_moving};
+  }
+  if ((a.pre_scale == nullptr) != (a.pre_shift == nullptr))
+    throw std::invalid_argument("bnf1x1: pre_scale and pre_shift together");
+  return [a](hipStream_t s) { bnf1x1(a, s); };
+}
+
 static Launch mk_conv_wgrad(ptr_t dy, ptr_t x, ptr_t pre_scale, ptr_t pre_shift, ptr_t part,
                             std::vector<int> geom, int splits, int px_per_split) {
   WgradArgs w{};
@@ -1012,6 +1044,8 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "bn_bwd_reduce", mk_bn_bwd_reduce);
   def_op(m, plan, "bn_bwd_finalize", mk_bn_bwd_finalize);
   def_op(m, plan, "bnd1x1", mk_bnd1x1);
+  def_op(m, plan, "bnf1x1", mk_bnf1x1);
+  m.def("bnf1x1_covers", &bnf1x1_covers, "whether the streaming narrow-K 1x1 forward (+ BN prologue, residual, BN statistics) covers (M, C, K)");
   m.def("bnd1x1_covers", &bnd1x1_covers, "whether the streaming narrow-K 1x1 dgrad + BN backward covers (M, C, K)");
   def_op(m, plan, "bn_bwd_apply", mk_bn_bwd_apply);
   def_op(m, plan, "bn_relu_apply", mk_bn_relu_apply);

@@ -36,10 +36,12 @@ namespace dtr {
 namespace {
 constexpr int BND_WG_PER_CU = 2;
 
-// rows per tile and columns per workgroup: the resident B fragments (K x CW/4 per wave)
-// and the double-buffered A fragments (RT x K) stay within 2 waves per SIMD
+// rows per tile and columns per workgroup (256): the resident B fragments (K x 64 per
+// wave) and the A operand stay within 2 waves per SIMD -- A as double-buffered MFMA
+// fragments in VGPRs up to K = 128 (each wave loads its own copy, L1-served), as one
+// shared LDS tile at K = 256 (its B fragments take 128 VGPRs)
 constexpr int bnd_rt(int K) { return K <= 64 ? 32 : 16; }
-constexpr int bnd_cw(int K) { return K <= 128 ? 256 : 128; }
+constexpr int bnd_cw(int) { return 256; }
 }  // namespace
 
 template <int MODE, int K>
@@ -47,6 +49,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 bnd1x1_kernel(BndArgs a) {
   constexpr int CW = bnd_cw(K), RT = bnd_rt(K);
   constexpr int MR = RT / 16, WC = CW / 4, NR = WC / 16, KS = K / 32;
+  constexpr bool ALDS = K >= 256;            // A through a shared LDS tile
+  constexpr int LDA = K + 8;                 // its padded row (conflict-free b128 reads)
+  constexpr int ACH = ALDS ? RT * K / 8 / 256 : 1;   // 16-B A chunks per thread and tile
   constexpr int CG = CW / 8;           // 8-channel groups per tile row
   constexpr int RPI = 256 / CG;        // tile rows one pass of the 256 threads covers
   constexpr int VPT = RT / RPI;        // row vectors per thread per tile
@@ -56,6 +61,7 @@ bnd1x1_kernel(BndArgs a) {
   constexpr int SO = RT * LDO > 4 * RPI * CW ? RT * LDO : 4 * RPI * CW;
   __shared__ __attribute__((aligned(16))) bf16 so[SO];
   __shared__ __attribute__((aligned(16))) float prm[7][CW];
+  __shared__ __attribute__((aligned(16))) bf16 sa[ALDS ? RT * LDA : 8];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -88,14 +94,24 @@ bnd1x1_kernel(BndArgs a) {
 
   const int cg = tid % CG, r0 = tid / CG;
   const bf16x8 zero8 = {};
-  bf16x8 af[MR][KS], xv[VPT], av[VPT];
-  auto load_tile = [&](int t, bf16x8 (&A)[MR][KS], bf16x8 (&X)[VPT], bf16x8 (&D)[VPT]) {
+  bf16x8 af[ALDS ? 1 : MR][ALDS ? 1 : KS], an[ACH], xv[VPT], av[VPT];
+  auto load_tile = [&](int t, bf16x8 (&A)[ALDS ? 1 : MR][ALDS ? 1 : KS], bf16x8 (&AN)[ACH],
+                       bf16x8 (&X)[VPT], bf16x8 (&D)[VPT]) {
+    if constexpr (ALDS) {
 #pragma unroll
-    for (int r = 0; r < MR; ++r)
+      for (int q = 0; q < ACH; ++q) {
+        const int ch = tid + 256 * q;   // chunk: row ch / (K/8), 8 k's at (ch % (K/8)) * 8
+        AN[q] = *reinterpret_cast<const bf16x8*>(a.dz + (long)(t * RT + ch / (K / 8)) * K +
+                                                 (ch % (K / 8)) * 8);
+      }
+    } else {
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk)
-        A[r][kk] = *reinterpret_cast<const bf16x8*>(
-            a.dz + (long)(t * RT + r * 16 + (lane & 15)) * K + kk * 32 + 8 * (lane >> 4));
+      for (int r = 0; r < MR; ++r)
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+          A[r][kk] = *reinterpret_cast<const bf16x8*>(
+              a.dz + (long)(t * RT + r * 16 + (lane & 15)) * K + kk * 32 + 8 * (lane >> 4));
+    }
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
       const long o = (long)(t * RT + r0 + v * RPI) * C + c0 + cg * 8;
@@ -103,7 +119,7 @@ bnd1x1_kernel(BndArgs a) {
       if constexpr (MODE == 1) D[v] = a.add ? *reinterpret_cast<const bf16x8*>(a.add + o) : zero8;
     }
   };
-  load_tile(rt, af, xv, av);
+  load_tile(rt, af, an, xv, av);
   __syncthreads();   // parameter table
 
   float s1[8], s2[8];
@@ -116,12 +132,30 @@ bnd1x1_kernel(BndArgs a) {
     for (int r = 0; r < MR; ++r)
 #pragma unroll
       for (int b = 0; b < NR; ++b) acc[r][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (ALDS) {
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
+      for (int q = 0; q < ACH; ++q) {
+        const int ch = tid + 256 * q;
+        *reinterpret_cast<bf16x8*>(sa + (ch / (K / 8)) * LDA + (ch % (K / 8)) * 8) = an[q];
+      }
+      lds_barrier();
 #pragma unroll
-      for (int r = 0; r < MR; ++r)
+      for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-        for (int b = 0; b < NR; ++b) acc[r][b] = mfma16(af[r][kk], bfr[kk][b], acc[r][b]);
+        for (int r = 0; r < MR; ++r) {
+          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(
+              sa + (r * 16 + (lane & 15)) * LDA + kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+          for (int b = 0; b < NR; ++b) acc[r][b] = mfma16(fa, bfr[kk][b], acc[r][b]);
+        }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+#pragma unroll
+          for (int b = 0; b < NR; ++b) acc[r][b] = mfma16(af[r][kk], bfr[kk][b], acc[r][b]);
+    }
     // C fragment (r, b): rows r*16 + 4*(lane/16) + i, column wave*WC + b*16 + lane%16
 #pragma unroll
     for (int r = 0; r < MR; ++r)
@@ -139,7 +173,7 @@ bnd1x1_kernel(BndArgs a) {
       xc[v] = xv[v];
       ac[v] = av[v];
     }
-    if (rt + rstep < nrt) load_tile(rt + rstep, af, xv, av);
+    if (rt + rstep < nrt) load_tile(rt + rstep, af, an, xv, av);
 
     float sc[8], sh[8], mu[8], rs[8];
 #pragma unroll

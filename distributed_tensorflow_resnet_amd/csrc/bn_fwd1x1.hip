@@ -1,0 +1,222 @@
+// Streaming 1x1 forward conv with a narrow reduction (K = 64..256 input channels) and a
+// wide output (C % 256 == 0), fused with the BN+ReLU prologue of its input, the residual
+// add and the BatchNorm statistics of its output: the third (expanding) conv of the
+// ImageNet bottleneck blocks (reference: batch_norm -> relu -> conv2d_fixed_padding ->
+// + shortcut, resnet_model_official.py:133-175; the sums feed the next block's first BN).
+//
+//   a[m][k]  = bf16(relu(x[m][k] * scale[k] + shift[k]))        (or x itself: no PRE)
+//   y[m][c]  = bf16( sum_k a[m][k] * W[c][k] + res[m][c] )
+//   stats   += (sum_m y, sum_m y^2) per channel                  (fp64 replicas)
+//
+// The backward counterpart (bn_dgrad1x1.hip) explains the shape: as a 128x128 implicit-
+// GEMM tile with this epilogue the stage-1 conv moved its 461 MB at ~2.8 TB/s (162 us).
+// Here: persistent workgroups, one 256-column slice each, the slice's weights resident
+// as MFMA B fragments; per row tile of RT rows the A tile (RT x K) goes through LDS with
+// the BN+ReLU applied on the way in (each thread owns fixed channels there: its 8 scale /
+// shift pairs stay in registers), the residual rows of tile t+1 are in flight during tile
+// t's epilogue, the fp32 tile is staged through LDS and swept as 16-B row vectors: one
+// bf16 rounding of acc + res, 16-B stores, per-channel fp64 sums per thread, one fp64
+// atomic pair per channel and workgroup at the end.
+// The MFMA order per output (k-steps 0..K/32-1) and the prologue arithmetic are the
+// implicit-GEMM forward's, so y equals conv_gemm's output bitwise.
+#include <stdexcept>
+
+#include "bn_fused.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+namespace {
+constexpr int BNF_CW = 256;
+constexpr int BNF_WG_PER_CU = 2;
+constexpr int bnf_rt(int K) { return K <= 64 ? 32 : 16; }
+}  // namespace
+
+template <int K, bool PRE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+bnf1x1_kernel(BnfArgs a) {
+  constexpr int CW = BNF_CW, RT = bnf_rt(K);
+  constexpr int MR = RT / 16, WC = CW / 4, NR = WC / 16, KS = K / 32;
+  constexpr int CG = CW / 8, RPI = 256 / CG, VPT = RT / RPI;
+  constexpr int LDC = CW + 4;                  // fp32 staging row stride
+  constexpr int LDA = K + 8;                   // bf16 A tile row stride (conflict-free reads)
+  constexpr int ACH = RT * K / 8 / 256;        // 16-B A chunks per thread and tile
+  static_assert(ACH >= 1 && VPT >= 1, "tile shape");
+  // fp32 staging tile; at the end the two [RPI][CW] fp64 reduction planes
+  constexpr int STF = RT * LDC > 4 * RPI * CW ? RT * LDC : 4 * RPI * CW;
+  __shared__ __attribute__((aligned(16))) float st[STF];
+  __shared__ __attribute__((aligned(16))) bf16 sa[RT * LDA];
+  __shared__ __attribute__((aligned(16))) float pre_s[PRE ? 2 * K : 4];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int C = a.C;
+  const int CT = C / CW;
+  const int c0 = (int)(blockIdx.x % CT) * CW;
+  const int nrt = a.M / RT, rstep = (int)gridDim.x / CT;   // host: gridDim.x % CT == 0
+  int rt = (int)blockIdx.x / CT;
+  if (rt >= nrt) return;
+
+  // BN+ReLU table of the input (finalized here from the fp64 accumulators if pending)
+  if constexpr (PRE) {
+    if (a.pfin.acc != nullptr) {
+      bn_prefin_table(a.pfin, K, pre_s, pre_s + K, nullptr);   // ends with a barrier
+    } else {
+      for (int i = tid; i < K; i += 256) {
+        pre_s[i] = a.pre_scale[i];
+        pre_s[K + i] = a.pre_shift[i];
+      }
+      __syncthreads();
+    }
+  }
+  // this thread's A chunks: chunk ch = tid + 256 q -> row ch / (K/8), channels (ch % (K/8)) * 8
+  f32x4 ps0[ACH], ps1[ACH], pb0[ACH], pb1[ACH];
+#pragma unroll
+  for (int q = 0; q < ACH; ++q) {
+    const int kc = ((tid + 256 * q) % (K / 8)) * 8;
+    if constexpr (PRE) {
+      ps0[q] = *reinterpret_cast<const f32x4*>(pre_s + kc);
+      ps1[q] = *reinterpret_cast<const f32x4*>(pre_s + kc + 4);
+      pb0[q] = *reinterpret_cast<const f32x4*>(pre_s + K + kc);
+      pb1[q] = *reinterpret_cast<const f32x4*>(pre_s + K + kc + 4);
+    }
+  }
+  // resident B fragments: W[c0 + wave*WC + b*16 + lane%16][kk*32 + 8*(lane/16) ..+8]
+  bf16x8 bfr[KS][NR];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+    for (int b = 0; b < NR; ++b)
+      bfr[kk][b] = *reinterpret_cast<const bf16x8*>(
+          a.w + (long)(c0 + wave * WC + b * 16 + (lane & 15)) * K + kk * 32 + 8 * (lane >> 4));
+
+  const int cg = tid % CG, r0 = tid / CG;
+  const bf16x8 zero8 = {};
+  bf16x8 an[ACH], rv[VPT];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < ACH; ++q) {
+      const int ch = tid + 256 * q;
+      an[q] = *reinterpret_cast<const bf16x8*>(a.x + (long)(t * RT + ch / (K / 8)) * K +
+                                               (ch % (K / 8)) * 8);
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v)
+      rv[v] = a.res ? *reinterpret_cast<const bf16x8*>(
+                          a.res + (long)(t * RT + r0 + v * RPI) * C + c0 + cg * 8)
+                    : zero8;
+  };
+  load_tile(rt);
+
+  double s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0;
+
+  for (; rt < nrt; rt += rstep) {
+    // A tile -> LDS, BN+ReLU applied on the way in
+#pragma unroll
+    for (int q = 0; q < ACH; ++q) {
+      const int ch = tid + 256 * q;
+      bf16x8 v = an[q];
+      if constexpr (PRE) v = affine_relu8_sel(v, ps0[q], ps1[q], pb0[q], pb1[q], ~0u);
+      *reinterpret_cast<bf16x8*>(sa + (ch / (K / 8)) * LDA + (ch % (K / 8)) * 8) = v;
+    }
+    lds_barrier();
+    f32x4 acc[MR][NR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+#pragma unroll
+      for (int b = 0; b < NR; ++b) acc[r][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int r = 0; r < MR; ++r) {
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(
+            sa + (r * 16 + (lane & 15)) * LDA + kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int b = 0; b < NR; ++b) acc[r][b] = mfma16(fa, bfr[kk][b], acc[r][b]);
+      }
+    // C fragment (r, b): rows r*16 + 4*(lane/16) + i, column wave*WC + b*16 + lane%16
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+#pragma unroll
+      for (int b = 0; b < NR; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          st[(r * 16 + 4 * (lane >> 4) + i) * LDC + wave * WC + b * 16 + (lane & 15)] =
+              acc[r][b][i];
+    lds_barrier();
+    bf16x8 rc[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) rc[v] = rv[v];
+    if (rt + rstep < nrt) load_tile(rt + rstep);   // next tile's A chunks + residual rows
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const int rl = r0 + v * RPI;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(st + rl * LDC + cg * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(st + rl * LDC + cg * 8 + 4);
+      const float y[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (bf16)(y[j] + (float)rc[v][j]);
+        const double d = (double)(float)o[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+      *reinterpret_cast<bf16x8*>(a.out + (long)(rt * RT + rl) * C + c0 + cg * 8) = o;
+    }
+    lds_barrier();   // staging and A tiles are rewritten by the next tile
+  }
+
+  if (a.stat_acc != nullptr) {
+    double* red = reinterpret_cast<double*>(st);   // [2][RPI][CW]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[r0 * CW + cg * 8 + j] = s1[j];
+      red[RPI * CW + r0 * CW + cg * 8 + j] = s2[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < CW; c += 256) {
+      double t1 = 0.0, t2 = 0.0;
+      for (int q = 0; q < RPI; ++q) {
+        t1 += red[q * CW + c];
+        t2 += red[RPI * CW + q * CW + c];
+      }
+      bn_acc_add(a.stat_acc, C, c0 + c, t1, t2);
+    }
+  }
+}
+
+bool bnf1x1_covers(int M, int C, int K) {
+  return (K == 64 || K == 128 || K == 256) && C % BNF_CW == 0 && M % bnf_rt(K) == 0 && M > 0;
+}
+
+template <int K>
+static void bnf_launch(const BnfArgs& a, dim3 g, hipStream_t s) {
+  const bool pre = a.pre_scale != nullptr || a.pfin.acc != nullptr;
+  if (pre) hipLaunchKernelGGL((bnf1x1_kernel<K, true>), g, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((bnf1x1_kernel<K, false>), g, dim3(256), 0, s, a);
+}
+
+void bnf1x1(const BnfArgs& a, hipStream_t s) {
+  if (!bnf1x1_covers(a.M, a.C, a.K))
+    throw std::runtime_error("bnf1x1: needs K in {64, 128, 256}, C % 256 == 0, M % row tile == 0");
+  const int CT = a.C / BNF_CW;
+  const long tiles = (long)(a.M / bnf_rt(a.K)) * CT;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  long grid = (long)cus * BNF_WG_PER_CU;
+  grid -= grid % CT;
+  if (grid > tiles) grid = tiles;
+  if (grid < CT) grid = CT;
+  const dim3 g((unsigned)grid);
+  if (a.K == 64) bnf_launch<64>(a, g, s);
+  else if (a.K == 128) bnf_launch<128>(a, g, s);
+  else bnf_launch<256>(a, g, s);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

@@ -167,6 +167,22 @@ struct BndArgs {
 bool bnd1x1_covers(int M, int C, int K);
 void bnd1x1(const BndArgs& a, int mode, hipStream_t s);
 
+// Streaming 1x1 forward conv with a narrow reduction (K = 64..256) and a wide output
+// (bn_fwd1x1.hip): y = bf16(relu(bn(x)) W^T + res), BN statistics of y into stat_acc.
+struct BnfArgs {
+  const bf16* x;            // [M][K] input (pre-BN when PRE)
+  const bf16* w;            // [C][K] OHWI weights of the 1x1 conv
+  const bf16* res;          // optional [M][C] residual
+  bf16* out;                // [M][C]
+  const float* pre_scale;   // optional BN+ReLU of x (finalized) ...
+  const float* pre_shift;
+  BnPreFin pfin;            // ... or finalized here from fp64 accumulators (pfin.acc)
+  double* stat_acc;         // optional [BN_ACC_REP][2][C] (sum y, sum y^2)
+  int M, C, K;
+};
+bool bnf1x1_covers(int M, int C, int K);
+void bnf1x1(const BnfArgs& a, hipStream_t s);
+
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
 void set_conv_splitk(int max_slices);   // split-K of under-filled FAST grids (1 = off)
 void set_conv_parity(int enabled);      // stride-2 dgrads by output parity class

@@ -527,6 +527,9 @@ class Engine:
         reads; or, as per-tile partials, are finalized by the first consumer's prologue
         (few tiles) or else by a separate bn_finalize launch."""
         geom = self._geom(c, N)
+        if self._fwd_stream(c, N, pre, stats_for):
+            self._conv_fwd_stream(plan, c, x, out, N, pre, residual, stats_for)
+            return
         stat_ptr = 0
         fin, pfin = [], []
         if pre is not None and pre.pending is not None:
@@ -558,6 +561,40 @@ class Engine:
                        0 if pre is None else pre.scale.data_ptr(),
                        0 if pre is None else pre.shift.data_ptr(), 0, 0, stat_ptr, 0, geom, [],
                        fin, [], pfin, [], BN_DECAY, BN_EPS, 1)
+
+    def _fwd_stream(self, c: _Conv, N, pre: _BN | None, stats_for: _BN | None) -> bool:
+        """Whether a forward conv takes the streaming narrow-K 1x1 kernel (bn_fwd1x1.hip):
+        1x1 stride 1, K = 64..256 input channels, >= 256-wide output, statistics (if any) in
+        fp64 accumulators, its BN prologue (if any) finalized or pending in accumulators."""
+        s = c.spec
+        if not tune.get("fwd1x1_stream") or self.stem_s2d and s.name == self.spec.stem.name:
+            return False
+        if s.kh != 1 or s.kw != 1 or s.stride != 1:
+            return False
+        if not self.nat.bnf1x1_covers(N * s.ho * s.wo, s.cout, c.cin):
+            return False
+        if stats_for is not None and not self.bn_acc_on:
+            return False
+        return pre is None or pre.pending is None or pre.pending[0] == "acc"
+
+    def _conv_fwd_stream(self, plan, c: _Conv, x, out, N, pre, residual, stats_for):
+        s = c.spec
+        M = N * s.ho * s.wo
+        pfin, ps, psh = [], 0, 0
+        if pre is not None and pre.pending is not None:
+            _, part, M0 = pre.pending
+            pfin = [part, _ACC_CNT, 0, M0, pre.gamma, pre.beta, pre.mean.data_ptr(),
+                    pre.rstd.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
+                    pre.mmean, pre.mvar]
+            pre.pending = None
+        elif pre is not None:
+            ps, psh = pre.scale.data_ptr(), pre.shift.data_ptr()
+        acc = 0
+        if stats_for is not None:
+            acc = stats_for.acc.data_ptr()
+            stats_for.pending = ("acc", acc, M)
+        plan.bnf1x1([x.data_ptr(), c.ohwi, 0 if residual is None else residual.data_ptr(),
+                     out.data_ptr(), ps, psh, acc], pfin, M, s.cout, c.cin, BN_DECAY, BN_EPS, 1)
 
     def _bn_input(self, plan, bn: _BN, x, y):
         """Operand of the conv consuming BN(x): (y, None) after materializing

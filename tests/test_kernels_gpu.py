@@ -857,7 +857,7 @@ def test_dgrad_bn_backward_apply_epilogue(gpu, N, H, C, K, with_add):
 
 
 @pytest.mark.parametrize("N,H,C,K", [(8, 56, 256, 64), (8, 28, 512, 128), (2, 4, 256, 64),
-                                     (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 128, 256)])
+                                     (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 256, 256)])
 def test_streaming_narrow_dgrad_bn_backward(gpu, N, H, C, K):
     """bnd1x1 (bn_dgrad1x1.hip): the sums pass == the implicit-GEMM dgrad's BN-backward
     sums (fp64 accumulators) to fp32 rounding, and the apply pass == bn_bwd_apply of the
@@ -914,3 +914,67 @@ def test_streaming_narrow_dgrad_bn_backward(gpu, N, H, C, K):
     xh = (xf - mean) * rstd
     dx_ref = gamma * rstd * (gg - gg.mean(0) - xh * (gg * xh).mean(0)) + add.float().reshape(-1, C)
     assert _rel(got.reshape(-1, C), dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["pre", "pfin", "nopre"])
+@pytest.mark.parametrize("N,H,K,C", [(8, 56, 64, 256), (8, 28, 128, 512), (8, 14, 256, 1024),
+                                     (2, 4, 64, 256)])
+def test_streaming_narrow_fwd_bn_residual_stats(gpu, N, H, K, C, mode):
+    """bnf1x1 (bn_fwd1x1.hip) == the implicit-GEMM forward with the same fusions (BN+ReLU
+    prologue given or finalized from fp64 accumulators in the prologue, residual add, BN
+    statistics into fp64 accumulators): output bitwise, statistics to fp64/fp32 rounding,
+    the prologue's finalize outputs equal; and == the fp32 reference."""
+    torch.manual_seed(24)
+    nat = fn.native()
+    st = torch.cuda.current_stream().cuda_stream
+    M = N * H * H
+    assert nat.bnf1x1_covers(M, C, K)
+    rep = nat.bn_acc_rep()
+    g = fn.ConvGeom(N, H, H, K, C, 1, 1, 1)
+    x = torch.randn(N, H, H, K, device=gpu).to(BF)
+    w = (torch.randn(C, 1, 1, K, device=gpu) / math.sqrt(K)).to(BF)   # OHWI
+    res = torch.randn(N, H, H, C, device=gpu).to(BF)
+    gamma, beta = torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.1
+    sc, sh = torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.2
+    # accumulator sums of a made-up producer of x: exactly x's own batch sums
+    xf = x.float().reshape(-1, K).double()
+    pacc = torch.zeros(rep, 2, K, device=gpu, dtype=torch.float64)
+    pacc[0, 0], pacc[0, 1] = xf.sum(0), (xf * xf).sum(0)
+    outs = []
+    for kern in ("gemm", "stream"):
+        out = torch.full((N, H, H, C), float("nan"), device=gpu, dtype=BF)
+        sacc = torch.zeros(rep * 2 * C, device=gpu, dtype=torch.float64)
+        bnout = [torch.zeros(K, device=gpu) for _ in range(4)] + [torch.zeros(K, device=gpu),
+                                                                  torch.ones(K, device=gpu)]
+        pf, ps, psh = [], 0, 0
+        if mode == "pfin":
+            pf = [pacc.data_ptr(), 0xFFFFFFFF, 0, M, gamma.data_ptr(), beta.data_ptr()] + \
+                 [t.data_ptr() for t in bnout]
+            ps, psh = bnout[2].data_ptr(), bnout[3].data_ptr()
+        elif mode == "pre":
+            ps, psh = sc.data_ptr(), sh.data_ptr()
+        if kern == "gemm":
+            nat.conv_gemm(0, x.data_ptr(), w.data_ptr(), out.data_ptr(), 0, res.data_ptr(), ps, psh,
+                          0, 0, torch.zeros(1, device=gpu).data_ptr(), 0, g.as_list(), [],
+                          [sacc.data_ptr()], [], pf, [], 0.997, ref.BN_EPS, 1, st)
+        else:
+            nat.bnf1x1([x.data_ptr(), w.data_ptr(), res.data_ptr(), out.data_ptr(),
+                        0 if mode == "pfin" else ps, 0 if mode == "pfin" else psh,
+                        sacc.data_ptr()], pf, M, C, K, 0.997, ref.BN_EPS, 1, st)
+        torch.cuda.synchronize()
+        outs.append((out, sacc.view(rep, 2, C).sum(0), [t.clone() for t in bnout]))
+    (o0, s0, b0), (o1, s1, b1) = outs
+    torch.testing.assert_close(o1.float(), o0.float(), rtol=0, atol=0)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-2)
+    if mode == "pfin":
+        for t0, t1 in zip(b0, b1):
+            torch.testing.assert_close(t1, t0, rtol=1e-6, atol=1e-7)
+        scale, shift = b1[2], b1[3]
+    else:
+        scale, shift = (sc, sh) if mode == "pre" else (None, None)
+    a_in = x.float() if scale is None else torch.relu(x.float() * scale + shift).to(BF).float()
+    want = ref.conv2d(a_in, w.float().permute(1, 2, 3, 0), 1) + res.float()
+    assert _rel(o1, want) < 1e-2
+    yf = o1.float().reshape(-1, C).double()
+    torch.testing.assert_close(s1[0], yf.sum(0), rtol=1e-9, atol=1e-6)
+    torch.testing.assert_close(s1[1], (yf * yf).sum(0), rtol=1e-9, atol=1e-6)
