@@ -17,6 +17,6 @@ for m in imagenet_resnet50 imagenet_resnet50 imagenet_resnet101; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_in50 -o run -- python3 bench.py --model imagenet_resnet50 --steps 10 --warmup 5 > gpurun_out/prof_in50.log 2>&1 || { tail -20 gpurun_out/prof_in50.log; exit 1; }
 db=$(find gpurun_out/prof_in50 -name '*.db' | head -1)
-python3 scripts/rocpd_summary.py "$db" 10 "ImageNet ResNet-50 v2, bs128/GPU, 1x MI355X (round 3 late: streaming narrow-K dgrad + BN backward, bap_maxc=512)" gpurun_out/in50_kernels.md > /dev/null || exit 1
+python3 scripts/rocpd_summary.py "$db" 10 "ImageNet ResNet-50 v2, bs128/GPU, 1x MI355X (round 3 late: streaming narrow-K 1x1 forward and dgrad + BN backward)" gpurun_out/in50_kernels.md > /dev/null || exit 1
 rm -rf gpurun_out/prof_in50
 head -12 gpurun_out/in50_kernels.md
