@@ -1,8 +1,10 @@
-// Streaming 1x1 forward conv with a narrow reduction (K = 64..256 input channels) and a
-// wide output (C % 256 == 0), fused with the BN+ReLU prologue of its input, the residual
-// add and the BatchNorm statistics of its output: the third (expanding) conv of the
-// ImageNet bottleneck blocks (reference: batch_norm -> relu -> conv2d_fixed_padding ->
-// + shortcut, resnet_model_official.py:133-175; the sums feed the next block's first BN).
+// Streaming 1x1 forward conv fused with the BN+ReLU prologue of its input, the residual
+// add and the BatchNorm statistics of its output, for the ImageNet bottleneck blocks'
+// 1x1 convs whose weights fit in VGPRs: the expanding third conv (K = 64..256 input
+// channels, 256-column slices of a wide output) and the narrowing first conv of stages
+// 1-2 (256 -> 64, 512 -> 128: the whole output per workgroup) (reference: batch_norm ->
+// relu -> conv2d_fixed_padding -> + shortcut, resnet_model_official.py:133-175; the
+// sums feed the next BN).
 //
 //   a[m][k]  = bf16(relu(x[m][k] * scale[k] + shift[k]))        (or x itself: no PRE)
 //   y[m][c]  = bf16( sum_k a[m][k] * W[c][k] + res[m][c] )
@@ -28,21 +30,29 @@
 namespace dtr {
 
 namespace {
-constexpr int BNF_CW = 256;
 constexpr int BNF_WG_PER_CU = 2;
-constexpr int bnf_rt(int K) { return K <= 64 ? 32 : 16; }
+// output columns per workgroup: 256-column slices of wide outputs, or the whole 64 / 128
+// output channels of the narrowing convs
+constexpr int bnf_cw(int C) { return C % 256 == 0 ? 256 : (C == 128 || C == 64) ? C : 0; }
+// rows per tile: the epilogue's 8-channel groups cover whole rows (RT >= 2048 / CW), every
+// thread stages at least one 16-B A chunk (RT >= 2048 / K), one MFMA row block at least
+constexpr int bnf_max(int a, int b) { return a > b ? a : b; }
+constexpr int bnf_rt(int K, int CW) { return bnf_max(bnf_max(2048 / CW, 2048 / K), 16); }
+// resident B fragments per wave ((K / 32) x (CW / 64)) within 32 (128 VGPRs)
+constexpr bool bnf_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
 }  // namespace
 
-template <int K, bool PRE>
+template <int K, bool PRE, int CW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 bnf1x1_kernel(BnfArgs a) {
-  constexpr int CW = BNF_CW, RT = bnf_rt(K);
+  constexpr int RT = bnf_rt(K, CW);
   constexpr int MR = RT / 16, WC = CW / 4, NR = WC / 16, KS = K / 32;
   constexpr int CG = CW / 8, RPI = 256 / CG, VPT = RT / RPI;
   constexpr int LDC = CW + 4;                  // fp32 staging row stride
   constexpr int LDA = K + 8;                   // bf16 A tile row stride (conflict-free reads)
   constexpr int ACH = RT * K / 8 / 256;        // 16-B A chunks per thread and tile
-  static_assert(ACH >= 1 && VPT >= 1, "tile shape");
+  constexpr bool PREG = ACH <= 2;              // PRE scale / shift in VGPRs (else LDS reads)
+  static_assert(ACH >= 1 && VPT >= 1 && NR >= 1, "tile shape");
   // fp32 staging tile; at the end the two [RPI][CW] fp64 reduction planes
   constexpr int STF = RT * LDC > 4 * RPI * CW ? RT * LDC : 4 * RPI * CW;
   __shared__ __attribute__((aligned(16))) float st[STF];
@@ -71,11 +81,12 @@ bnf1x1_kernel(BnfArgs a) {
     }
   }
   // this thread's A chunks: chunk ch = tid + 256 q -> row ch / (K/8), channels (ch % (K/8)) * 8
-  f32x4 ps0[ACH], ps1[ACH], pb0[ACH], pb1[ACH];
+  constexpr int PQ = PREG ? ACH : 1;
+  f32x4 ps0[PQ], ps1[PQ], pb0[PQ], pb1[PQ];
 #pragma unroll
-  for (int q = 0; q < ACH; ++q) {
+  for (int q = 0; q < PQ; ++q) {
     const int kc = ((tid + 256 * q) % (K / 8)) * 8;
-    if constexpr (PRE) {
+    if constexpr (PRE && PREG) {
       ps0[q] = *reinterpret_cast<const f32x4*>(pre_s + kc);
       ps1[q] = *reinterpret_cast<const f32x4*>(pre_s + kc + 4);
       pb0[q] = *reinterpret_cast<const f32x4*>(pre_s + K + kc);
@@ -119,7 +130,15 @@ bnf1x1_kernel(BnfArgs a) {
     for (int q = 0; q < ACH; ++q) {
       const int ch = tid + 256 * q;
       bf16x8 v = an[q];
-      if constexpr (PRE) v = affine_relu8_sel(v, ps0[q], ps1[q], pb0[q], pb1[q], ~0u);
+      if constexpr (PRE && PREG) {
+        v = affine_relu8_sel(v, ps0[q], ps1[q], pb0[q], pb1[q], ~0u);
+      } else if constexpr (PRE) {
+        const int kc = (ch % (K / 8)) * 8;
+        v = affine_relu8_sel(v, *reinterpret_cast<const f32x4*>(pre_s + kc),
+                             *reinterpret_cast<const f32x4*>(pre_s + kc + 4),
+                             *reinterpret_cast<const f32x4*>(pre_s + K + kc),
+                             *reinterpret_cast<const f32x4*>(pre_s + K + kc + 4), ~0u);
+      }
       *reinterpret_cast<bf16x8*>(sa + (ch / (K / 8)) * LDA + (ch % (K / 8)) * 8) = v;
     }
     lds_barrier();
@@ -190,21 +209,35 @@ bnf1x1_kernel(BnfArgs a) {
 }
 
 bool bnf1x1_covers(int M, int C, int K) {
-  return (K == 64 || K == 128 || K == 256) && C % BNF_CW == 0 && M % bnf_rt(K) == 0 && M > 0;
+  const int CW = bnf_cw(C);
+  return (K == 64 || K == 128 || K == 256 || K == 512) && bnf_fits(K, CW) && C % CW == 0 &&
+         M > 0 && M % bnf_rt(K, CW) == 0;
 }
 
-template <int K>
+template <int K, int CW>
 static void bnf_launch(const BnfArgs& a, dim3 g, hipStream_t s) {
-  const bool pre = a.pre_scale != nullptr || a.pfin.acc != nullptr;
-  if (pre) hipLaunchKernelGGL((bnf1x1_kernel<K, true>), g, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((bnf1x1_kernel<K, false>), g, dim3(256), 0, s, a);
+  if constexpr (bnf_fits(K, CW)) {
+    const bool pre = a.pre_scale != nullptr || a.pfin.acc != nullptr;
+    if (pre) hipLaunchKernelGGL((bnf1x1_kernel<K, true, CW>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((bnf1x1_kernel<K, false, CW>), g, dim3(256), 0, s, a);
+  }
+}
+
+template <int CW>
+static void bnf_launch_k(const BnfArgs& a, dim3 g, hipStream_t s) {
+  if (a.K == 64) bnf_launch<64, CW>(a, g, s);
+  else if (a.K == 128) bnf_launch<128, CW>(a, g, s);
+  else if (a.K == 256) bnf_launch<256, CW>(a, g, s);
+  else bnf_launch<512, CW>(a, g, s);
 }
 
 void bnf1x1(const BnfArgs& a, hipStream_t s) {
   if (!bnf1x1_covers(a.M, a.C, a.K))
-    throw std::runtime_error("bnf1x1: needs K in {64, 128, 256}, C % 256 == 0, M % row tile == 0");
-  const int CT = a.C / BNF_CW;
-  const long tiles = (long)(a.M / bnf_rt(a.K)) * CT;
+    throw std::runtime_error("bnf1x1: shape not covered (K in 64..512, C = 64 / 128 or a "
+                             "multiple of 256, resident weights <= 128 VGPRs, M % row tile)");
+  const int CW = bnf_cw(a.C);
+  const int CT = a.C / CW;
+  const long tiles = (long)(a.M / bnf_rt(a.K, CW)) * CT;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -213,9 +246,9 @@ void bnf1x1(const BnfArgs& a, hipStream_t s) {
   if (grid > tiles) grid = tiles;
   if (grid < CT) grid = CT;
   const dim3 g((unsigned)grid);
-  if (a.K == 64) bnf_launch<64>(a, g, s);
-  else if (a.K == 128) bnf_launch<128>(a, g, s);
-  else bnf_launch<256>(a, g, s);
+  if (CW == 256) bnf_launch_k<256>(a, g, s);
+  else if (CW == 128) bnf_launch_k<128>(a, g, s);
+  else bnf_launch_k<64>(a, g, s);
   DTR_CHECK_LAUNCH();
 }
 

@@ -40,10 +40,11 @@ ENGINE = {
                          "of dgrad + a separate BN-backward apply (RN50 bs128: 12.15 -> 11.67 "
                          "ms at 512 = stages 1-2; 11.87 at 1024: the K = 256 stage-3 pass "
                          "pair 110 vs 97 us unfused); 0 off"),
-    "fwd1x1_stream": (1, "1x1 stride-1 forward convs with 64-256 input and >= 256 output "
-                         "channels (the bottlenecks' expanding conv, stage-1 projections) on "
-                         "the streaming kernel bn_fwd1x1 (BN prologue, residual and BN "
-                         "statistics fused; 2x the implicit-GEMM tile's bytes/s)"),
+    "fwd1x1_stream": (1, "1x1 stride-1 forward convs whose weights fit in VGPRs (the "
+                         "bottlenecks' expanding conv, the stage 1-2 narrowing conv and "
+                         "projection) on the streaming kernel bn_fwd1x1 (BN prologue, "
+                         "residual and BN statistics fused; 2x the implicit-GEMM tile's "
+                         "bytes/s: RN50 11.69 -> 11.03 ms for the expanding convs)"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 

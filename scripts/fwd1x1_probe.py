@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""The expanding 1x1 forward convs of the ImageNet RN50 bottlenecks (K narrow -> C wide, BN+ReLU
-prologue, residual, BN statistics into fp64 accumulators): the implicit-GEMM kernel vs the
+"""The 1x1 forward convs of the ImageNet RN50 bottlenecks the streaming kernel covers (the
+expanding K narrow -> C wide, the narrowing 256 -> 64 / 512 -> 128; BN+ReLU prologue, residual,
+BN statistics into fp64 accumulators): the implicit-GEMM kernel vs the
 streaming kernel (bn_fwd1x1.hip), HIP events, median of reps, 128 images.
 
     python3 scripts/fwd1x1_probe.py [reps]
@@ -37,7 +38,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     print("| N,H,K->C | PRE | MB moved | implicit GEMM us | TB/s | streaming us | TB/s |")
     print("|---|---|---|---|---|---|---|")
-    for (H, K, C) in [(56, 64, 256), (28, 128, 512), (14, 256, 1024)]:
+    for (H, K, C) in [(56, 64, 256), (28, 128, 512), (14, 256, 1024), (56, 256, 64), (28, 512, 128),
+                      (56, 64, 64), (28, 256, 128)]:
         for pre in (True, False):
             N = 128
             M = N * H * H
@@ -57,7 +59,7 @@ def main():
             t1 = timed(lambda: nat.bnf1x1([x.data_ptr(), w.data_ptr(), res.data_ptr(),
                                            out.data_ptr(), ps, psh, sacc.data_ptr()], [], M, C, K,
                                           0.997, ref.BN_EPS, 1, st), reps)
-            mb = (M * K + 2 * M * C) * 2 / 1e6
+            mb = (M * K + 2 * M * C) * 2 / 1e6 if C > K else (M * K + M * C) * 2 / 1e6
             print(f"| {N},{H},{K}->{C} | {pre} | {mb:.0f} | {t0:.1f} | {mb / t0:.2f} | "
                   f"{t1:.1f} | {mb / t1:.2f} |", flush=True)
 
