@@ -198,9 +198,11 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
 static Launch mk_bnd1x1(int mode, std::vector<ptr_t> p, int M, int C, int K) {
   if (p.size() != 11) throw std::invalid_argument("bnd1x1 needs 11 pointers");
   if (!bnd1x1_covers(M, C, K))
-    throw std::invalid_argument("bnd1x1: needs K in {64, 128, 256}, C % slice == 0, M % row tile == 0");
-  if (mode == 0 && p[10] == 0) throw std::invalid_argument("bnd1x1 sums need bacc");
-  if (mode == 1 && (p[4] == 0 || p[9] == 0)) throw std::invalid_argument("bnd1x1 apply needs out, coef");
+    throw std::invalid_argument("bnd1x1: shape not covered (K in 64..512, C = 64 / 128 or a multiple of 256, resident weights <= 128 VGPRs, M % row tile)");
+  if (mode < 0 || mode > 2) throw std::invalid_argument("bnd1x1 mode: 0 sums, 1 apply, 2 store + sums");
+  if (mode != 1 && p[10] == 0) throw std::invalid_argument("bnd1x1 sums need bacc");
+  if (mode >= 1 && p[4] == 0) throw std::invalid_argument("bnd1x1 apply / store need out");
+  if (mode == 1 && p[9] == 0) throw std::invalid_argument("bnd1x1 apply needs coef");
   BndArgs a{P<const bf16>(p[0]), P<const bf16>(p[1]), P<const bf16>(p[2]), P<const bf16>(p[3]),
             P<bf16>(p[4]), P<const float>(p[5]), P<const float>(p[6]), P<const float>(p[7]),
             P<const float>(p[8]), P<const float>(p[9]), P<double>(p[10]), M, C, K};

@@ -6,6 +6,10 @@
 //   g[m][c]  = bf16( sum_k dz[m][k] * W[c][k] ) * [x[m][c]*scale[c] + shift[c] > 0]
 //   SUMS  : bacc += (sum_m g, sum_m g * (x - mean) * rstd)          (fp64 replicas)
 //   APPLY : dx[m][c] = bf16( a[c] g - b[c] - c[c] (x - mean) rstd + add[m][c] )
+//   STORE+SUMS (mode 2): the unfused BNB dgrad -- out = the bf16 dgrad, plus SUMS
+// Shapes: K = 64..512 narrow-or-wide reductions whose weights fit in VGPRs, over 256-column
+// slices of a wide output (the bottlenecks' first conv) or the whole 64 / 128-column output
+// (the expanding conv's dgrad at stages 1-2).
 //
 // Why a separate kernel: as an implicit-GEMM tile with a fat epilogue (conv_gemm.hip /
 // conv_ring.hip, F_BNB / F_BAPPLY) these passes moved their bytes at 2.1-2.9 TB/s -- each
@@ -36,22 +40,27 @@ namespace dtr {
 namespace {
 constexpr int BND_WG_PER_CU = 2;
 
-// rows per tile and columns per workgroup (256): the resident B fragments (K x 64 per
-// wave) and the A operand stay within 2 waves per SIMD -- A as double-buffered MFMA
-// fragments in VGPRs up to K = 128 (each wave loads its own copy, L1-served), as one
-// shared LDS tile at K = 256 (its B fragments take 128 VGPRs)
-constexpr int bnd_rt(int K) { return K <= 64 ? 32 : 16; }
-constexpr int bnd_cw(int) { return 256; }
+// Columns per workgroup: 256-column slices of wide outputs, or the whole 64 / 128-column
+// output of the narrowing dgrads.  The resident B fragments ((K / 32) x (CW / 64) per wave)
+// and the A operand stay within 2 waves per SIMD -- A as double-buffered MFMA fragments in
+// VGPRs up to K = 128 (each wave loads its own copy, L1-served), as one shared LDS tile
+// from K = 256.  Rows per tile: the epilogue's 8-channel groups cover whole rows.
+constexpr int bnd_cw(int C) { return C % 256 == 0 ? 256 : (C == 128 || C == 64) ? C : 0; }
+constexpr int bnd_rt(int K, int CW) {
+  return CW == 256 ? (K <= 64 ? 32 : 16) : (2048 / CW > 16 ? 2048 / CW : 16);
+}
+constexpr bool bnd_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
 }  // namespace
 
-template <int MODE, int K>
+template <int MODE, int K, int CW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 bnd1x1_kernel(BndArgs a) {
-  constexpr int CW = bnd_cw(K), RT = bnd_rt(K);
+  constexpr int RT = bnd_rt(K, CW);
   constexpr int MR = RT / 16, WC = CW / 4, NR = WC / 16, KS = K / 32;
   constexpr bool ALDS = K >= 256;            // A through a shared LDS tile
   constexpr int LDA = K + 8;                 // its padded row (conflict-free b128 reads)
   constexpr int ACH = ALDS ? RT * K / 8 / 256 : 1;   // 16-B A chunks per thread and tile
+  static_assert(!ALDS || RT * K >= 2048, "every thread stages an A chunk");
   constexpr int CG = CW / 8;           // 8-channel groups per tile row
   constexpr int RPI = 256 / CG;        // tile rows one pass of the 256 threads covers
   constexpr int VPT = RT / RPI;        // row vectors per thread per tile
@@ -194,7 +203,9 @@ bnd1x1_kernel(BndArgs a) {
     for (int v = 0; v < VPT; ++v) {
       const int rl = r0 + v * RPI;
       const bf16x8 gv = *reinterpret_cast<const bf16x8*>(so + rl * LDO + cg * 8);
-      if constexpr (MODE == 0) {
+      if constexpr (MODE != 1) {
+        if constexpr (MODE == 2)   // the dgrad itself, as the implicit-GEMM BNB dgrad stores it
+          *reinterpret_cast<bf16x8*>(a.out + (long)(rt * RT + rl) * C + c0 + cg * 8) = gv;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xc[v][j];
@@ -230,7 +241,7 @@ bnd1x1_kernel(BndArgs a) {
     lds_barrier();   // the staging tile is rewritten by the next tile
   }
 
-  if constexpr (MODE == 0) {
+  if constexpr (MODE != 1) {
     // fold the RPI threads of each channel group (fixed order), then one fp64 atomic pair
     // per channel and workgroup into the accumulator replica
     float* red = reinterpret_cast<float*>(so);   // [2][RPI][CW]
@@ -252,14 +263,35 @@ bnd1x1_kernel(BndArgs a) {
 }
 
 bool bnd1x1_covers(int M, int C, int K) {
-  return (K == 64 || K == 128 || K == 256) && C % bnd_cw(K) == 0 && M % bnd_rt(K) == 0 && M > 0;
+  const int CW = bnd_cw(C);
+  return (K == 64 || K == 128 || K == 256 || K == 512) && bnd_fits(K, CW) && C % CW == 0 &&
+         M > 0 && M % bnd_rt(K, CW) == 0 && (K < 256 || bnd_rt(K, CW) * K >= 2048);
+}
+
+template <int K, int CW>
+static void bnd_launch(const BndArgs& a, int mode, dim3 g, hipStream_t s) {
+  if constexpr (bnd_fits(K, CW)) {
+    if (mode == 0) hipLaunchKernelGGL((bnd1x1_kernel<0, K, CW>), g, dim3(256), 0, s, a);
+    else if (mode == 1) hipLaunchKernelGGL((bnd1x1_kernel<1, K, CW>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((bnd1x1_kernel<2, K, CW>), g, dim3(256), 0, s, a);
+  }
+}
+
+template <int CW>
+static void bnd_launch_k(const BndArgs& a, int mode, dim3 g, hipStream_t s) {
+  if (a.K == 64) bnd_launch<64, CW>(a, mode, g, s);
+  else if (a.K == 128) bnd_launch<128, CW>(a, mode, g, s);
+  else if (a.K == 256) bnd_launch<256, CW>(a, mode, g, s);
+  else bnd_launch<512, CW>(a, mode, g, s);
 }
 
 void bnd1x1(const BndArgs& a, int mode, hipStream_t s) {
   if (!bnd1x1_covers(a.M, a.C, a.K))
-    throw std::runtime_error("bnd1x1: needs K in {64, 128, 256}, C % slice == 0, M % row tile == 0");
-  const int CT = a.C / bnd_cw(a.K);
-  const long tiles = (long)(a.M / bnd_rt(a.K)) * CT;
+    throw std::runtime_error("bnd1x1: shape not covered (K in 64..512, C = 64 / 128 or a "
+                             "multiple of 256, resident weights <= 128 VGPRs, M % row tile)");
+  const int CW = bnd_cw(a.C);
+  const int CT = a.C / CW;
+  const long tiles = (long)(a.M / bnd_rt(a.K, CW)) * CT;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -267,16 +299,10 @@ void bnd1x1(const BndArgs& a, int mode, hipStream_t s) {
   grid -= grid % CT;
   if (grid > tiles) grid = tiles;
   if (grid < CT) grid = CT;
-  const dim3 g((unsigned)grid), b(256);
-  if (mode == 0) {
-    if (a.K == 64) hipLaunchKernelGGL((bnd1x1_kernel<0, 64>), g, b, 0, s, a);
-    else if (a.K == 128) hipLaunchKernelGGL((bnd1x1_kernel<0, 128>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((bnd1x1_kernel<0, 256>), g, b, 0, s, a);
-  } else {
-    if (a.K == 64) hipLaunchKernelGGL((bnd1x1_kernel<1, 64>), g, b, 0, s, a);
-    else if (a.K == 128) hipLaunchKernelGGL((bnd1x1_kernel<1, 128>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((bnd1x1_kernel<1, 256>), g, b, 0, s, a);
-  }
+  const dim3 g((unsigned)grid);
+  if (CW == 256) bnd_launch_k<256>(a, mode, g, s);
+  else if (CW == 128) bnd_launch_k<128>(a, mode, g, s);
+  else bnd_launch_k<64>(a, mode, g, s);
   DTR_CHECK_LAUNCH();
 }
 

@@ -669,6 +669,17 @@ class Engine:
             return False
         return not self.nat.conv_direct_covers(1, self._geom(c, N))
 
+    def _dgrad_stream_ok(self, c: _Conv, N) -> bool:
+        """1x1 stride-1 dgrads with BN-backward sums whose weights fit the streaming kernel
+        (bn_dgrad1x1.hip mode 2): the expanding conv's dgrad at stages 1-2, the first
+        conv's at stage 3 (tune dgrad1x1_stream)."""
+        s = c.spec
+        if not tune.get("dgrad1x1_stream") or s.kh != 1 or s.kw != 1 or s.stride != 1:
+            return False
+        M = N * s.h * s.w
+        return (self.nat.bnd1x1_covers(M, c.cin, s.cout)
+                and not self.nat.conv_direct_covers(1, self._geom(c, N)))
+
     def _conv_bwd(self, plan, c: _Conv, dy, x, N, pre: _BN | None, dx=None, accumulate=False,
                   bnb: tuple | None = None, side: bool = True, bap: tuple | None = None):
         """dgrad into dx (optional), then wgrad (+ reduce into the flat gradient).
@@ -762,7 +773,13 @@ class Engine:
                 if self.bn_bacc_on:
                     bfl = [bn.bacc.data_ptr()]
                     self._bnb_src = (bn.bacc.data_ptr(), -1)
-            if "dgrad" not in _DIAG_SKIP:
+            stream_bnb = (bnb is not None and self.bn_bacc_on and not accumulate and not abw
+                          and self._dgrad_stream_ok(c, N))
+            if stream_bnb and "dgrad" not in _DIAG_SKIP:
+                # 1x1 dgrad + BN-backward sums on the streaming kernel (bn_dgrad1x1.hip mode 2)
+                plan.bnd1x1(2, [a_src.data_ptr(), c.hwio, bx.data_ptr(), 0, dx.data_ptr()] +
+                            bl[1:5] + [0, bn.bacc.data_ptr()], Mx, C, s.cout)
+            elif "dgrad" not in _DIAG_SKIP:
                 plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0, 0, 0, 0, 0, 0,
                                0, int(accumulate), geom, bl, [], bfl, [], abw, BN_DECAY, BN_EPS,
                                1)

@@ -45,6 +45,9 @@ ENGINE = {
                          "projection) on the streaming kernel bn_fwd1x1 (BN prologue, "
                          "residual and BN statistics fused; 2x the implicit-GEMM tile's "
                          "bytes/s: RN50 11.69 -> 11.03 ms for the expanding convs)"),
+    "dgrad1x1_stream": (1, "1x1 stride-1 dgrads carrying BN-backward sums whose weights fit "
+                           "in VGPRs (the expanding conv at stages 1-2, the first conv at "
+                           "stage 3) on the streaming kernel bn_dgrad1x1 (store + sums)"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 

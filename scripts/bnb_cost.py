@@ -42,8 +42,9 @@ def main():
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream().cuda_stream
     N = 128
-    print("| H,Cin<-Cout,k,s | x/step | ring | dgrad us | +BNB us | BNB cost us | x MB | step ms |")
-    print("|---|---|---|---|---|---|---|---|")
+    print("| H,Cin<-Cout,k,s | x/step | ring | dgrad us | +BNB us | BNB cost us | x MB | step ms "
+          "| streaming +BNB us |")
+    print("|---|---|---|---|---|---|---|---|---|")
     tot = 0.0
     for (H, C, K, k, s, n) in SHAPES:
         g = fn.ConvGeom(N, H, H, C, K, k, k, s)
@@ -65,9 +66,14 @@ def main():
         t0 = timed(lambda: dg([], []), reps)
         t1 = timed(lambda: dg(bl, [bacc.data_ptr()]), reps)
         ring = nat.conv_ring_covers(1, g.as_list())
+        t2 = float("nan")
+        if k == 1 and s == 1 and nat.bnd1x1_covers(M, C, K):
+            t2 = timed(lambda: nat.bnd1x1(2, [dy.data_ptr(), w.data_ptr(), x.data_ptr(), 0,
+                                              out.data_ptr()] + bl[1:5] + [0, bacc.data_ptr()],
+                                          M, C, K, st), reps)
         tot += n * (t1 - t0)
         print(f"| {H},{C}<-{K},{k},{s} | {n} | {ring} | {t0:.1f} | {t1:.1f} | {t1 - t0:.1f} | "
-              f"{M * C * 2 / 1e6:.0f} | {n * (t1 - t0) / 1e3:.3f} |", flush=True)
+              f"{M * C * 2 / 1e6:.0f} | {n * (t1 - t0) / 1e3:.3f} | {t2:.1f} |", flush=True)
     print(f"\nBNB epilogue cost over the step's dgrads: {tot / 1e3:.3f} ms")
 
 

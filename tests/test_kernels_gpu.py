@@ -979,3 +979,49 @@ def test_streaming_narrow_fwd_bn_residual_stats(gpu, N, H, K, C, mode):
     yf = o1.float().reshape(-1, C).double()
     torch.testing.assert_close(s1[0], yf.sum(0), rtol=1e-9, atol=1e-6)
     torch.testing.assert_close(s1[1], (yf * yf).sum(0), rtol=1e-9, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,H,C,K", [(8, 56, 64, 256), (8, 28, 128, 512), (8, 14, 1024, 256),
+                                     (8, 14, 64, 64), (4, 14, 128, 256), (8, 28, 256, 64)])
+def test_streaming_dgrad_store_and_bn_backward_sums(gpu, N, H, C, K):
+    """bnd1x1 mode 2 == the implicit-GEMM dgrad with the BNB epilogue: the stored dgrad
+    bitwise (same MFMA order), the BN-backward sums to fp32 rounding, both vs the fp32
+    reference."""
+    torch.manual_seed(25)
+    nat = fn.native()
+    st = torch.cuda.current_stream().cuda_stream
+    M = N * H * H
+    assert nat.bnd1x1_covers(M, C, K)
+    rep = nat.bn_acc_rep()
+    g = fn.ConvGeom(N, H, H, C, K, 1, 1, 1)
+    dz = torch.randn(N, H, H, K, device=gpu).to(BF)
+    w = (torch.randn(1, 1, C, K, device=gpu) / math.sqrt(K)).to(BF)
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    mean, rstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.2
+    bnp = [mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(), sh.data_ptr()]
+    part = torch.zeros((M // 16 + 1) * 2 * C, device=gpu)
+    outs = []
+    for kern in ("gemm", "stream"):
+        out = torch.full((N, H, H, C), float("nan"), device=gpu, dtype=BF)
+        bacc = torch.zeros(rep * 2 * C, device=gpu, dtype=torch.float64)
+        if kern == "gemm":
+            nat.conv_gemm(1, dz.data_ptr(), w.data_ptr(), out.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0,
+                          g.as_list(), [x.data_ptr()] + bnp + [part.data_ptr()], [],
+                          [bacc.data_ptr()], [], [], 0.997, ref.BN_EPS, 1, st)
+        else:
+            nat.bnd1x1(2, [dz.data_ptr(), w.data_ptr(), x.data_ptr(), 0, out.data_ptr()] + bnp +
+                       [0, bacc.data_ptr()], M, C, K, st)
+        torch.cuda.synchronize()
+        outs.append((out, bacc.view(rep, 2, C).sum(0)))
+    (o0, s0), (o1, s1) = outs
+    torch.testing.assert_close(o1.float(), o0.float(), rtol=0, atol=0)
+    scale_ = s0.abs().max().item() + 1.0
+    assert (s1 - s0).abs().max().item() <= 1e-5 * scale_
+    dxt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
+    ref.conv2d(dxt, w.float(), 1).backward(dz.float())
+    assert _rel(o1, dxt.grad) < 1e-2
+    xf, gf = x.float().reshape(-1, C), o1.float().reshape(-1, C)
+    gg = gf * ((xf * sc + sh) > 0).float()
+    torch.testing.assert_close(s1[0].float(), gg.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s1[1].float(), (gg * (xf - mean) * rstd).sum(0), rtol=1e-4, atol=1e-2)
