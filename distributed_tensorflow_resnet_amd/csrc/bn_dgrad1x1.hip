@@ -45,11 +45,15 @@ constexpr int BND_WG_PER_CU = 2;
 // and the A operand stay within 2 waves per SIMD -- A as double-buffered MFMA fragments in
 // VGPRs up to K = 128 (each wave loads its own copy, L1-served), as one shared LDS tile
 // from K = 256.  Rows per tile: the epilogue's 8-channel groups cover whole rows.
-constexpr int bnd_cw(int C) { return C % 256 == 0 ? 256 : (C == 128 || C == 64) ? C : 0; }
+constexpr bool bnd_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
+constexpr int bnd_cw(int C, int K) {
+  return (C % 256 == 0 && bnd_fits(K, 256)) ? 256
+         : (C % 128 == 0 && bnd_fits(K, 128)) ? 128
+         : (C % 64 == 0 && bnd_fits(K, 64)) ? 64 : 0;
+}
 constexpr int bnd_rt(int K, int CW) {
   return CW == 256 ? (K <= 64 ? 32 : 16) : (2048 / CW > 16 ? 2048 / CW : 16);
 }
-constexpr bool bnd_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
 }  // namespace
 
 template <int MODE, int K, int CW>
@@ -263,8 +267,8 @@ bnd1x1_kernel(BndArgs a) {
 }
 
 bool bnd1x1_covers(int M, int C, int K) {
-  const int CW = bnd_cw(C);
-  return (K == 64 || K == 128 || K == 256 || K == 512) && bnd_fits(K, CW) && C % CW == 0 &&
+  const int CW = bnd_cw(C, K);
+  return (K == 64 || K == 128 || K == 256 || K == 512) && CW > 0 && C % CW == 0 &&
          M > 0 && M % bnd_rt(K, CW) == 0 && (K < 256 || bnd_rt(K, CW) * K >= 2048);
 }
 
@@ -289,12 +293,10 @@ void bnd1x1(const BndArgs& a, int mode, hipStream_t s) {
   if (!bnd1x1_covers(a.M, a.C, a.K))
     throw std::runtime_error("bnd1x1: shape not covered (K in 64..512, C = 64 / 128 or a "
                              "multiple of 256, resident weights <= 128 VGPRs, M % row tile)");
-  const int CW = bnd_cw(a.C);
+  const int CW = bnd_cw(a.C, a.K);
   const int CT = a.C / CW;
   const long tiles = (long)(a.M / bnd_rt(a.K, CW)) * CT;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = cu_count();
   long grid = (long)cus * BND_WG_PER_CU;
   grid -= grid % CT;
   if (grid > tiles) grid = tiles;

@@ -31,15 +31,19 @@ namespace dtr {
 
 namespace {
 constexpr int BNF_WG_PER_CU = 2;
-// output columns per workgroup: 256-column slices of wide outputs, or the whole 64 / 128
-// output channels of the narrowing convs
-constexpr int bnf_cw(int C) { return C % 256 == 0 ? 256 : (C == 128 || C == 64) ? C : 0; }
+// resident B fragments per wave ((K / 32) x (CW / 64)) within 32 (128 VGPRs)
+constexpr bool bnf_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
+// output columns per workgroup: the widest of 256 / 128 / 64 that divides C and whose
+// weights fit (narrower slices re-read the A rows once per slice, from L2 / MALL)
+constexpr int bnf_cw(int C, int K) {
+  return (C % 256 == 0 && bnf_fits(K, 256)) ? 256
+         : (C % 128 == 0 && bnf_fits(K, 128)) ? 128
+         : (C % 64 == 0 && bnf_fits(K, 64)) ? 64 : 0;
+}
 // rows per tile: the epilogue's 8-channel groups cover whole rows (RT >= 2048 / CW), every
 // thread stages at least one 16-B A chunk (RT >= 2048 / K), one MFMA row block at least
 constexpr int bnf_max(int a, int b) { return a > b ? a : b; }
 constexpr int bnf_rt(int K, int CW) { return bnf_max(bnf_max(2048 / CW, 2048 / K), 16); }
-// resident B fragments per wave ((K / 32) x (CW / 64)) within 32 (128 VGPRs)
-constexpr bool bnf_fits(int K, int CW) { return CW > 0 && (K / 32) * (CW / 64) <= 32; }
 }  // namespace
 
 template <int K, bool PRE, int CW>
@@ -209,8 +213,8 @@ bnf1x1_kernel(BnfArgs a) {
 }
 
 bool bnf1x1_covers(int M, int C, int K) {
-  const int CW = bnf_cw(C);
-  return (K == 64 || K == 128 || K == 256 || K == 512) && bnf_fits(K, CW) && C % CW == 0 &&
+  const int CW = bnf_cw(C, K);
+  return (K == 64 || K == 128 || K == 256 || K == 512) && CW > 0 && C % CW == 0 &&
          M > 0 && M % bnf_rt(K, CW) == 0;
 }
 
@@ -235,12 +239,10 @@ void bnf1x1(const BnfArgs& a, hipStream_t s) {
   if (!bnf1x1_covers(a.M, a.C, a.K))
     throw std::runtime_error("bnf1x1: shape not covered (K in 64..512, C = 64 / 128 or a "
                              "multiple of 256, resident weights <= 128 VGPRs, M % row tile)");
-  const int CW = bnf_cw(a.C);
+  const int CW = bnf_cw(a.C, a.K);
   const int CT = a.C / CW;
   const long tiles = (long)(a.M / bnf_rt(a.K, CW)) * CT;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = cu_count();
   long grid = (long)cus * BNF_WG_PER_CU;
   grid -= grid % CT;
   if (grid > tiles) grid = tiles;

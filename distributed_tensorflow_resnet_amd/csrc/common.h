@@ -146,6 +146,21 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
 // (wt_store_direct), the implicit-GEMM convs store normally.
 inline int wt_store_mode() { return (int)tune(T_WT_STORE); }
 inline bool wt_store_enabled() { return wt_store_mode() == 1; }
+
+// Compute units of the current device, queried once per device (persistent-grid sizing
+// on the launch path without a runtime attribute query per launch).
+inline int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
 // Direct convs: write-through once a launch writes >= 2 MB.  A kernel boundary pays
 // ~bytes / 6 TB/s to write back the dirty lines its predecessor left in L2
 // (MI355X_MICROARCH.md "boundary"); write-through stores leave none.  Measured, CIFAR

@@ -857,7 +857,8 @@ def test_dgrad_bn_backward_apply_epilogue(gpu, N, H, C, K, with_add):
 
 
 @pytest.mark.parametrize("N,H,C,K", [(8, 56, 256, 64), (8, 28, 512, 128), (2, 4, 256, 64),
-                                     (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 256, 256)])
+                                     (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 256, 256),
+                                     (16, 7, 2048, 512)])
 def test_streaming_narrow_dgrad_bn_backward(gpu, N, H, C, K):
     """bnd1x1 (bn_dgrad1x1.hip): the sums pass == the implicit-GEMM dgrad's BN-backward
     sums (fp64 accumulators) to fp32 rounding, and the apply pass == bn_bwd_apply of the
@@ -919,7 +920,7 @@ def test_streaming_narrow_dgrad_bn_backward(gpu, N, H, C, K):
 @pytest.mark.parametrize("mode", ["pre", "pfin", "nopre"])
 @pytest.mark.parametrize("N,H,K,C", [(8, 56, 64, 256), (8, 28, 128, 512), (8, 14, 256, 1024),
                                      (2, 4, 64, 256), (8, 56, 256, 64), (8, 28, 512, 128),
-                                     (8, 14, 64, 64), (4, 14, 256, 128)])
+                                     (8, 14, 64, 64), (4, 14, 256, 128), (16, 7, 512, 2048)])
 def test_streaming_narrow_fwd_bn_residual_stats(gpu, N, H, K, C, mode):
     """bnf1x1 (bn_fwd1x1.hip) == the implicit-GEMM forward with the same fusions (BN+ReLU
     prologue given or finalized from fp64 accumulators in the prologue, residual add, BN
@@ -982,7 +983,8 @@ def test_streaming_narrow_fwd_bn_residual_stats(gpu, N, H, K, C, mode):
 
 
 @pytest.mark.parametrize("N,H,C,K", [(8, 56, 64, 256), (8, 28, 128, 512), (8, 14, 1024, 256),
-                                     (8, 14, 64, 64), (4, 14, 128, 256), (8, 28, 256, 64)])
+                                     (8, 14, 64, 64), (4, 14, 128, 256), (8, 28, 256, 64),
+                                     (16, 7, 2048, 512)])
 def test_streaming_dgrad_store_and_bn_backward_sums(gpu, N, H, C, K):
     """bnd1x1 mode 2 == the implicit-GEMM dgrad with the BNB epilogue: the stored dgrad
     bitwise (same MFMA order), the BN-backward sums to fp32 rounding, both vs the fp32
