@@ -54,7 +54,9 @@ const TuneEntry kTable[T_COUNT] = {
     {"wgd_bmp64", 256, "... 64 channels"},
     {"wgrad_target_wg", 768,
      "split-K wgrad: target workgroups (3 per CU hide the per-tile load latency)"},
-    {"wgrad_slab_mb", 32, "split-K wgrad: cap of one layer's fp32 partial slabs, MB"},
+    {"wgrad_slab_mb", 16,
+     "split-K wgrad: cap of one layer's fp32 partial slabs, MB (RN50 bs128, back to back: "
+     "32 10.68 / 10.70 ms, 16 10.62 / 10.60, 12 10.79, 8 11.38)"},
     {"fin_v", 1,
      "BN finalize variant: 1 auto (per-channel one-round kernel for many partials), 0 LDS "
      "tree, 2 one-round"},
