@@ -78,8 +78,7 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
   g.stat_part = P<float>(stat_part);
   g.accumulate = accumulate;
   if (!bnb.empty()) {  // [x, mean, rstd, scale, shift, part]: fused BN-ReLU backward reduce
-                       // [x, mean, rstd, scale, shift, 0, coef]: fused BN-ReLU backward apply
-    if (bnb.size() != 6 && bnb.size() != 7) throw std::invalid_argument("bnb needs 6 or 7 pointers");
+    if (bnb.size() != 6) throw std::invalid_argument("bnb needs 6 pointers");
     if (mode != MODE_DGRAD) throw std::invalid_argument("bnb is dgrad-only");
     g.bnb_x = P<const bf16>(bnb[0]);
     g.bnb_mean = P<const float>(bnb[1]);
@@ -87,12 +86,6 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     g.bnb_scale = P<const float>(bnb[3]);
     g.bnb_shift = P<const float>(bnb[4]);
     g.bnb_part = P<float>(bnb[5]);
-    if (bnb.size() == 7) {
-      if (bnb[5] != 0 || bnb[6] == 0 || out == 0)
-        throw std::invalid_argument("bnb apply mode: part must be 0, coef and out set");
-      if (!bfin.empty()) throw std::invalid_argument("bnb apply mode takes no finalize");
-      g.bap_coef = P<const float>(bnb[6]);
-    }
   }
   if (fin.size() == 1) {  // [acc]: STATS into the fp64 accumulator replicas (kernels.h)
     if (stat_part == 0) throw std::invalid_argument("stat acc requires stat_part");
@@ -143,6 +136,7 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                       P<bf16>(abwd[9]), P<float>(abwd[10]), P<float>(abwd[11]),
                       P<float>(abwd[12])};
   }
+  if (out == 0 && out_f32 == 0) throw std::invalid_argument("conv_gemm: out or out_f32 needed");
   g.g = geom_from(geom);
   const ConvGeom& c = g.g;
   const int taps = c.kh * c.kw;
@@ -170,9 +164,6 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
                                   "dgrad (CIFAR shapes)");
     }
   }
-  if (g.bap_coef != nullptr && (conv_direct_covers(g, mode) || g.Ncol < 64 || c.stride != 1))
-    throw std::invalid_argument("bnb apply mode: implicit-GEMM stride-1 dgrads of >= 64 "
-                                "columns only");
   if (g.pfin.cnt > 0 && g.pfin.acc == nullptr) {
     const int C = c.C;   // PRE is forward-only: the A channels
     if (g.pfin.cnt > pfin_cap(C))

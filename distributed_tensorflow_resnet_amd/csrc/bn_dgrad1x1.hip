@@ -12,7 +12,7 @@
 // (the expanding conv's dgrad at stages 1-2).
 //
 // Why a separate kernel: as an implicit-GEMM tile with a fat epilogue (conv_gemm.hip /
-// conv_ring.hip, F_BNB / F_BAPPLY) these passes moved their bytes at 2.1-2.9 TB/s -- each
+// conv_ring.hip, F_BNB; an apply-epilogue variant was measured and removed) these passes moved their bytes at 2.1-2.9 TB/s -- each
 // 128x128 workgroup loads its operands once, then spends its life in the LDS-staged
 // epilogue with nothing in flight -- while the standalone BN-backward apply streams at
 // 4.7 TB/s (scripts/bap_probe.py).  Here the GEMM is a side show (K = 64..128: 2-4 MFMA

@@ -6,11 +6,7 @@
 
 namespace dtr {
 
-// F_BAPPLY (dgrad): the epilogue emits the BN+ReLU backward OUTPUT of the produced
-// gradient instead of the gradient itself: dx = a*g - b - c*xhat (+ residual),
-// g = bf16(acc) * [x*scale+shift > 0], with the coefficients (a, b, c) = bap_coef
-// finalized from an earlier BNB pass of the same GEMM (GemmArgs::bap_coef).
-enum { F_PRE = 1, F_STATS = 2, F_BNB = 4, F_ABWD = 8, F_BAPPLY = 16 };
+enum { F_PRE = 1, F_STATS = 2, F_BNB = 4, F_ABWD = 8 };
 
 // Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
 // it fits in 64 KiB (one phase), else one wave-row per phase (128x128 tiles).
@@ -254,10 +250,10 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
           P.acc[it] = (ok && args.accumulate && !args.out_f32)
                           ? *reinterpret_cast<const bf16x8*>(args.out + o) : zero8;
         }
-        if constexpr ((FLAGS & (F_BNB | F_BAPPLY)) != 0)
+        if constexpr ((FLAGS & F_BNB) != 0)
           P.x[ph * PP::RIT + it] = ok ? *reinterpret_cast<const bf16x8*>(args.bnb_x + o) : zero8;
       }
-    if constexpr (PP::COEF && (FLAGS & (F_BNB | F_BAPPLY)) != 0) {
+    if constexpr (PP::COEF && (FLAGS & F_BNB) != 0) {
       const bool colok = col0 < args.Ncol;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -332,9 +328,6 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   if (tile_n < 0) tile_n = blockIdx.y;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
-  constexpr bool BAP = (FLAGS & F_BAPPLY) != 0;
-  constexpr bool XLD = BNB || BAP;   // BN-input rows + BN coefficients are read
-  static_assert(!(BAP && (BNB || STATS)), "BAPPLY emits dx: no statistics in the same pass");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MR = WTM / 16, NR = WTN / 16;
   const int M = args.M, NC = args.Ncol;
@@ -363,16 +356,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   float bnb_t1 = 0.f, bnb_t2 = 0.f;   // BNB column totals (thread tid < BN)
   float bsc[8], bsh[8], bmu[8], brs[8];
-  float bca[BAP ? 8 : 1], bcb[BAP ? 8 : 1], bcc[BAP ? 8 : 1];   // BAPPLY: a, b, c per column
-  if constexpr (BAP) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bca[j] = colok ? args.bap_coef[col0 + j] : 0.f;
-      bcb[j] = colok ? args.bap_coef[NC + col0 + j] : 0.f;
-      bcc[j] = colok ? args.bap_coef[2 * NC + col0 + j] : 0.f;
-    }
-  }
-  if constexpr (XLD) {
+  if constexpr (BNB) {
     constexpr bool COEF = EpiPre<BM, BN, WM, XO>::COEF;
     if (COEF && EpiPre<BM, BN, WM, XO>::ON && pre) {
 #pragma unroll
@@ -408,7 +392,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     constexpr int RIT = (EL::PR + EL::RPP - 1) / EL::RPP;
     constexpr bool PREL = EpiPre<BM, BN, WM, XO>::ON;
     constexpr bool PRER = PREL && !XO;   // single-phase: residual / accumulate rows too
-    constexpr bool BATCH = XLD;
+    constexpr bool BATCH = BNB;
     constexpr bool BATCHR = EL::PHASES > 1 && !BNB;   // (BNB: no residual; the registers spill)
     bf16x8 lx[BATCH ? RIT : 1], lr[BATCHR ? RIT : 1];
     if (BATCH && PREL && pre) {   // this phase's prefetched BN-input rows (selects, no indexing)
@@ -426,7 +410,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         const int r = r0 + it * EL::RPP;
         if (!colok || r >= nph) continue;
         const long o = epi_row(args, prow0 + r) * NC + col0;
-        if constexpr (XLD) lx[BATCH ? it : 0] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
+        if constexpr (BNB) lx[BATCH ? it : 0] = *reinterpret_cast<const bf16x8*>(args.bnb_x + o);
       }
     }
     if (BATCHR && args.residual) {
@@ -491,7 +475,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cp + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const long o = epi_row(args, row) * NC + col0;
-      if (args.residual && !BAP) {
+      if (args.residual) {
         const bf16x8 rv = (PRER && pre) ? pre->res[PRER ? it : 0]
                           : BATCHR      ? lr[BATCHR ? it : 0]
                                         : *reinterpret_cast<const bf16x8*>(args.residual + o);
@@ -524,20 +508,6 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
         ob[it][j] = (bf16)v[j];
         v[j] = (float)ob[it][j];
       }
-      if constexpr (BAP) {   // the same arithmetic as bn_bwd_apply_kernel on the bf16 gradient
-        const bf16x8 xv = lx[BATCH ? it : 0];
-        const bf16x8 zero8 = {};
-        const bf16x8 rv = !args.residual ? zero8
-                          : BATCHR ? lr[BATCHR ? it : 0]
-                                   : *reinterpret_cast<const bf16x8*>(args.residual + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xf = (float)xv[j];
-          const float gg = (xf * bsc[j] + bsh[j] > 0.f) ? v[j] : 0.f;
-          const float xh = (xf - bmu[j]) * brs[j];
-          ob[it][j] = (bf16)(bca[j] * gg - bcb[j] - bcc[j] * xh + (float)rv[j]);
-        }
-      }
       if constexpr (STATS) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -562,7 +532,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     // lds_barrier()s, which wait for LDS only, so the stores drain while the column
     // sums run (args.wt: write-through sc1 buffer stores, so the tile does not
     // sit dirty in this XCD's L2 for the end-of-kernel release to write back)
-    if (!args.out_f32 && args.out) {   // (out == nullptr: a BNB pass that only sums)
+    if (!args.out_f32) {
       if (args.wt) {
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.out, 0, 0x7fffffff, 0x00020000);
 #pragma unroll

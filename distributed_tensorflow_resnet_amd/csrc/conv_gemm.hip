@@ -61,7 +61,6 @@ conv_gemm_kernel(GemmArgs args) {
   constexpr bool PRE = (FLAGS & F_PRE) != 0;
   constexpr bool STATS = (FLAGS & F_STATS) != 0;
   constexpr bool BNB = (FLAGS & F_BNB) != 0;
-  constexpr bool XLD = (FLAGS & (F_BNB | F_BAPPLY)) != 0;   // epilogue reads BN-input rows
   static_assert((FLAGS & F_ABWD) == 0, "the fused BN backward prologue is direct-conv only");
   constexpr int BK = 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -461,7 +460,7 @@ conv_gemm_kernel(GemmArgs args) {
     using I1 = std::integral_constant<int, 1>;
     issue(t_beg, I0{});
     issue(t_beg + 1, I1{});
-    if constexpr (XLD) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+    if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
     if constexpr (PRE) {
       if (args.pfin.cnt > 0) {
         bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
@@ -499,7 +498,7 @@ conv_gemm_kernel(GemmArgs args) {
     if (sk_n > 1 && !splitk_combine<MR, NR>(args, acc, smem, tm, tn, blockIdx.z)) return;
   } else {   // general gather (runtime `fast` only for the narrow-column tiles)
   load_tile(0);
-  if constexpr (XLD) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
+  if constexpr (BNB) epi_prefetch<BM, BN, WM, FLAGS, true>(args, m0, n0, epre);
   if constexpr (PRE) {   // BN scale/shift table (finalized here if this is the first consumer)
     if (args.pfin.cnt > 0) {
       bn_prefin_table(args.pfin, Acin, pre_s, pre_s + Acin, reinterpret_cast<float*>(As));
@@ -527,7 +526,7 @@ conv_gemm_kernel(GemmArgs args) {
   }
   }
 
-  if constexpr (XLD && EP::ON)
+  if constexpr (BNB && EP::ON)
     conv_epilogue<BM, BN, WM, WN, FLAGS, true>(args, acc, smem, m0, n0, &epre, tm, tn);
   else
     conv_epilogue<BM, BN, WM, WN, FLAGS, false>(args, acc, smem, m0, n0, nullptr, tm, tn);
@@ -691,16 +690,8 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
     else if (st) launch_cfg<BM, BN, WM, WN, MODE, F_STATS>(a, s);
     else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   } else {
-    if (a.bap_coef != nullptr) {
-      // BN-backward apply epilogue: instantiated for the wide-column tiles only (the
-      // bottleneck blocks' first 1x1 dgrad, engine _conv_bwd_bap)
-      if constexpr (BN >= 64) launch_cfg<BM, BN, WM, WN, MODE, F_BAPPLY>(a, s);
-      else throw std::runtime_error("conv_gemm: BN-backward apply epilogue needs >= 64 columns");
-    } else if (bnb) {
-      launch_cfg<BM, BN, WM, WN, MODE, F_BNB>(a, s);
-    } else {
-      launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
-    }
+    if (bnb) launch_cfg<BM, BN, WM, WN, MODE, F_BNB>(a, s);
+    else launch_cfg<BM, BN, WM, WN, MODE, 0>(a, s);
   }
 }
 

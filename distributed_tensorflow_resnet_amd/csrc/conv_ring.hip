@@ -71,7 +71,7 @@ conv_ring_kernel(GemmArgs args) {
   constexpr int WM = BN == 128 ? 2 : 4, WN = 4 / WM;
   constexpr int MR = BM / WM / 16, NR = BN / WN / 16;
   static_assert(BM * BK * 2 == STAGE_A_BYTES, "A tile bytes");   // stage: A, then B (BN x BK)
-  constexpr bool BNB = (FLAGS & (F_BNB | F_BAPPLY)) != 0;   // BN-input rows in the epilogue
+  constexpr bool BNB = (FLAGS & F_BNB) != 0;
   static_assert((FLAGS & (F_PRE | F_ABWD)) == 0, "no A-operand prologue on the ring");
   static_assert(BN == 128 || BN == 64, "128 x 128 or 128 x 64 tiles");
 
@@ -314,8 +314,7 @@ static void ring_flags(const GemmArgs& a, int mode, int flags, dim3 grid, hipStr
     if (flags & F_STATS) ring_launch<MODE_FWD, F_STATS, BN>(a, grid, s);
     else ring_launch<MODE_FWD, 0, BN>(a, grid, s);
   } else {
-    if (flags & F_BAPPLY) ring_launch<MODE_DGRAD, F_BAPPLY, BN>(a, grid, s);
-    else if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, BN>(a, grid, s);
+    if (flags & F_BNB) ring_launch<MODE_DGRAD, F_BNB, BN>(a, grid, s);
     else ring_launch<MODE_DGRAD, 0, BN>(a, grid, s);
   }
 }

@@ -114,9 +114,6 @@ struct GemmArgs {
   const float* bnb_scale;
   const float* bnb_shift;
   float* bnb_part;          // [tiles][2][Ncol]: sum g, sum g*xhat
-  // optional [3][Ncol] BN-backward apply coefficients (a, b, c): with bnb_x the dgrad
-  // epilogue writes dx = a*g - b - c*xhat (+ residual) instead of g (F_BAPPLY)
-  const float* bap_coef;
   BnFwdFin fin;             // with stat_part: finalize in-kernel
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
   // Accumulator mode of STATS / BNB: instead of (or beside) the per-tile partials,

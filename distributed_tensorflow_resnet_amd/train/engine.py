@@ -659,15 +659,16 @@ class Engine:
     def _bap_ok(self, c: _Conv, N) -> bool:
         """Whether the first 1x1 dgrad of an identity bottleneck block emits its input
         BatchNorm's backward output itself (_conv_bwd ``bap``): accumulator-mode sums,
-        an implicit-GEMM stride-1 dgrad, and the block's wide input channels within
+        a shape the streaming kernel covers, and the block's wide input channels within
         the ``bap_maxc`` bound (0 = off)."""
         s = c.spec
         maxc = tune.get("bap_maxc")
         if not (self.bn_bacc_on and maxc > 0 and c.cin <= maxc):
             return False
-        if s.kh != 1 or s.kw != 1 or s.stride != 1 or c.cin < 64 or c.cin % 64:
+        if s.kh != 1 or s.kw != 1 or s.stride != 1:
             return False
-        return not self.nat.conv_direct_covers(1, self._geom(c, N))
+        return (self.nat.bnd1x1_covers(N * s.h * s.w, c.cin, s.cout)
+                and not self.nat.conv_direct_covers(1, self._geom(c, N)))
 
     def _dgrad_stream_ok(self, c: _Conv, N) -> bool:
         """1x1 stride-1 dgrads with BN-backward sums whose weights fit the streaming kernel
@@ -691,10 +692,10 @@ class Engine:
 
         ``bap=(bn, add)`` (bn's input is ``x``, the 1x1 conv's own input): dx receives
         the BN+ReLU backward OUTPUT, BNbwd(dgrad) + add, with no separate apply pass.
-        The dgrad runs twice: a first pass only sums (sum g, sum g*xhat into the fp64
-        accumulators, no store), a finalize turns the sums into the apply coefficients,
-        and the second pass recomputes the same GEMM tile (bitwise the same fp32
-        values: same kernel schedule) and applies BN backward + add in its epilogue.
+        The dgrad runs twice on the streaming kernel (bn_dgrad1x1.hip): a first pass only
+        sums (sum g, sum g*xhat into the fp64 accumulators, no store), a finalize turns
+        the sums into the apply coefficients, and the second pass recomputes the same
+        GEMM tile (bitwise the same fp32 values) and applies BN backward + add.
         For a bottleneck block's first conv the GEMM is narrow (K = 64..512 input
         rows), while the BN'd tensor is wide (256..2048 channels): recomputing it
         costs less than writing the wide gradient, re-reading it and x, and writing
@@ -738,28 +739,16 @@ class Engine:
             M, C = N * s.h * s.w, c.cin
             bl = [x.data_ptr(), bn.mean.data_ptr(), bn.rstd.data_ptr(), bn.scale.data_ptr(),
                   bn.shift.data_ptr()]
-            if self.nat.bnd1x1_covers(M, C, s.cout):
-                # narrow K (64 / 128): the streaming kernel (bn_dgrad1x1.hip) runs both passes
-                base = [a_src.data_ptr(), c.hwio, x.data_ptr()]
-                bnp = bl[1:]
-                plan.bnd1x1(0, base + [0, 0] + bnp + [0, bn.bacc.data_ptr()], M, C, s.cout)
-            else:
-                # pass 1: the implicit-GEMM dgrad, sums only (out = 0)
-                plan.conv_gemm(1, a_src.data_ptr(), c.hwio, 0, 0, 0, 0, 0, 0, 0, 0, 0, geom,
-                               bl + [bn.bpart.data_ptr()], [], [bn.bacc.data_ptr()], [], [],
-                               BN_DECAY, BN_EPS, 1)
+            # the streaming kernel (bn_dgrad1x1.hip) runs both passes (_bap_ok checked coverage)
+            base = [a_src.data_ptr(), c.hwio, x.data_ptr()]
+            bnp = bl[1:]
+            plan.bnd1x1(0, base + [0, 0] + bnp + [0, bn.bacc.data_ptr()], M, C, s.cout)
             plan.bn_bwd_finalize(bn.bacc.data_ptr(), -1, M, C, bn.gamma, bn.rstd.data_ptr(),
                                  bn.dgamma, bn.dbeta, self.coef.data_ptr())
             self._produced.update(bn.names)
             addp = 0 if add is None else add.data_ptr()
-            if self.nat.bnd1x1_covers(M, C, s.cout):
-                plan.bnd1x1(1, base + [addp, dx.data_ptr()] + bnp + [self.coef.data_ptr(), 0], M,
-                            C, s.cout)
-            else:
-                # pass 2: the same GEMM, BN backward + add applied in the epilogue
-                plan.conv_gemm(1, a_src.data_ptr(), c.hwio, dx.data_ptr(), 0, addp, 0, 0, 0, 0,
-                               0, 0, geom, bl + [0, self.coef.data_ptr()], [], [], [], [],
-                               BN_DECAY, BN_EPS, 1)
+            plan.bnd1x1(1, base + [addp, dx.data_ptr()] + bnp + [self.coef.data_ptr(), 0], M, C,
+                        s.cout)
         elif dx is not None:
             bl, bfl = [], []
             if bnb is not None:

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Where the time of the narrow-K 1x1 dgrads goes (ImageNet RN50 bottleneck conv1 dgrads,
-128 images, 1x MI355X): the dgrad alone, + BN-backward sums (fp64 accumulators or per-tile
-partials), the sums-only pass (no store), the BN-backward-apply epilogue pass, and the
-separate streaming apply, each timed with HIP events (median of reps).
+128 images, 1x MI355X): the implicit-GEMM dgrad alone, + BN-backward sums (fp64 accumulators
+or per-tile partials), the separate streaming apply, and the streaming kernel's sums and
+apply passes, each timed with HIP events (median of reps).  (The implicit-GEMM sums-only
+and apply-epilogue passes of profiles/imagenet_bn_backward_fusion.md were removed.)
 
     python3 scripts/bap_probe.py [reps]
 """
@@ -36,10 +37,9 @@ def main():
     nat = fn.native()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream().cuda_stream
-    print("| N,H,C(wide),K | MB wide | dgrad | +BNB acc | +BNB part | sums only acc | sums only part "
-          "| apply epilogue | separate apply | dgrad+BNB+apply | 2-pass | stream sums | stream apply "
-          "| stream 2-pass |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    print("| N,H,C(wide),K | MB wide | dgrad | +BNB acc | +BNB part | separate apply "
+          "| dgrad+BNB+apply | stream sums | stream apply | stream 2-pass |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for (N, H, C, K) in [(128, 56, 256, 64), (128, 28, 512, 128), (128, 14, 1024, 256),
                          (128, 7, 2048, 512)]:
         M = N * H * H
@@ -69,10 +69,6 @@ def main():
         t["dgrad"] = timed(lambda: dg(out.data_ptr(), [], []), reps)
         t["acc"] = timed(lambda: dg(out.data_ptr(), bl + [part.data_ptr()], [bacc.data_ptr()]), reps)
         t["part"] = timed(lambda: dg(out.data_ptr(), bl + [part.data_ptr()], []), reps)
-        t["s_acc"] = timed(lambda: dg(0, bl + [part.data_ptr()], [bacc.data_ptr()]), reps)
-        t["s_part"] = timed(lambda: dg(0, bl + [part.data_ptr()], []), reps)
-        t["bap"] = timed(lambda: dg(dx.data_ptr(), bl + [0, coef.data_ptr()], [], add.data_ptr()),
-                         reps)
         t["apply"] = timed(lambda: nat.bn_bwd_apply(
             out.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(),
             sh.data_ptr(), coef.data_ptr(), add.data_ptr(), dx.data_ptr(), M, C, st), reps)
@@ -86,8 +82,7 @@ def main():
                                                [coef.data_ptr(), 0], M, C, K, st), reps)
         mb = M * C * 2 / 1e6
         print(f"| {N},{H},{C},{K} | {mb:.0f} | {t['dgrad']:.1f} | {t['acc']:.1f} | {t['part']:.1f} | "
-              f"{t['s_acc']:.1f} | {t['s_part']:.1f} | {t['bap']:.1f} | {t['apply']:.1f} | "
-              f"{t['acc'] + t['apply']:.1f} | {t['s_acc'] + t['bap']:.1f} | {t['ss']:.1f} | "
+              f"{t['apply']:.1f} | {t['acc'] + t['apply']:.1f} | {t['ss']:.1f} | "
               f"{t['sa']:.1f} | {t['ss'] + t['sa']:.1f} |", flush=True)
 
 

@@ -787,75 +787,6 @@ def test_ring_wgrad_matches_register_loop_and_reference(gpu, N, H, C, K, k, s):
     assert _rel(outs[0], wt.grad) < 1e-2
 
 
-# (N, H, C = the wide BN'd channels = dgrad output columns, K = the narrow dgrad input):
-# the first 1x1 conv of each ImageNet bottleneck stage (general loop, 1-2 K tiles; ring
-# from 4 K tiles) and an odd partial-tile case
-BAP_CASES = [(8, 56, 256, 64), (8, 28, 512, 128), (16, 14, 1024, 256), (32, 7, 2048, 512),
-             (6, 9, 128, 64)]
-
-
-@pytest.mark.parametrize("with_add", [True, False])
-@pytest.mark.parametrize("N,H,C,K", BAP_CASES)
-def test_dgrad_bn_backward_apply_epilogue(gpu, N, H, C, K, with_add):
-    """F_BAPPLY: a sums-only dgrad pass (no store) + bn_bwd_finalize + the same dgrad with
-    the BN+ReLU backward and the residual add applied in its epilogue == dgrad (BNB sums)
-    + finalize + the separate bn_bwd_apply, bitwise; and == the fp32 reference of
-    dx = BNbwd(conv2d_transpose(dy, W)) + add."""
-    torch.manual_seed(22)
-    nat = fn.native()
-    st = torch.cuda.current_stream().cuda_stream
-    M = N * H * H
-    g = fn.ConvGeom(N, H, H, C, K, 1, 1, 1)
-    dy = torch.randn(N, H, H, K, device=gpu).to(BF)
-    w = (torch.randn(1, 1, C, K, device=gpu) / math.sqrt(K)).to(BF)
-    x = torch.randn(N, H, H, C, device=gpu).to(BF)
-    add = torch.randn(N, H, H, C, device=gpu).to(BF) if with_add else None
-    mean = torch.randn(C, device=gpu) * 0.1
-    rstd = torch.rand(C, device=gpu) + 0.5
-    gamma = torch.rand(C, device=gpu) + 0.5
-    sc, sh = gamma * rstd, torch.randn(C, device=gpu) * 0.2 - mean * gamma * rstd
-    bl = [x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), sc.data_ptr(), sh.data_ptr()]
-    part = torch.zeros((M // 64 + 1) * 2 * C, device=gpu)
-    addp = 0 if add is None else add.data_ptr()
-
-    def sums_and_coef(out_ptr):
-        bacc = torch.zeros(nat.bn_acc_rep() * 2 * C, device=gpu, dtype=torch.float64)
-        nat.conv_gemm(1, dy.data_ptr(), w.data_ptr(), out_ptr, 0, 0, 0, 0, 0, 0, 0, 0,
-                      g.as_list(), bl + [part.data_ptr()], [], [bacc.data_ptr()], [], [],
-                      0.997, ref.BN_EPS, 1, st)
-        dgb, coef = torch.empty(2 * C, device=gpu), torch.empty(3 * C, device=gpu)
-        nat.bn_bwd_finalize(bacc.data_ptr(), -1, M, C, gamma.data_ptr(), rstd.data_ptr(),
-                            dgb.data_ptr(), dgb.data_ptr() + 4 * C, coef.data_ptr(), st)
-        return dgb, coef
-
-    # unfused: dgrad writes g, finalize, separate apply
-    da = torch.empty(N, H, H, C, device=gpu, dtype=BF)
-    dgb1, coef1 = sums_and_coef(da.data_ptr())
-    want = torch.empty_like(da)
-    nat.bn_bwd_apply(da.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                     sc.data_ptr(), sh.data_ptr(), coef1.data_ptr(), addp, want.data_ptr(), M,
-                     C, st)
-    # fused: sums-only pass, finalize, apply epilogue
-    dgb2, coef2 = sums_and_coef(0)
-    got = torch.full_like(da, float("nan"))
-    nat.conv_gemm(1, dy.data_ptr(), w.data_ptr(), got.data_ptr(), 0, addp, 0, 0, 0, 0, 0, 0,
-                  g.as_list(), bl + [0, coef2.data_ptr()], [], [], [], [], 0.997, ref.BN_EPS, 1,
-                  st)
-    torch.cuda.synchronize()
-    torch.testing.assert_close(dgb2, dgb1, rtol=0, atol=0)
-    torch.testing.assert_close(got.float(), want.float(), rtol=0, atol=0)
-    # fp32 reference
-    dxt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
-    ref.conv2d(dxt, w.float(), 1).backward(dy.float())
-    xf, gf = x.float().reshape(-1, C), dxt.grad.reshape(-1, C)
-    gg = gf * ((xf * sc + sh) > 0).float()
-    xh = (xf - mean) * rstd
-    dx_ref = gamma * rstd * (gg - gg.mean(0) - xh * (gg * xh).mean(0))
-    if add is not None:
-        dx_ref = dx_ref + add.float().reshape(-1, C)
-    assert _rel(got.reshape(-1, C), dx_ref) < 1e-2
-
-
 @pytest.mark.parametrize("N,H,C,K", [(8, 56, 256, 64), (8, 28, 512, 128), (2, 4, 256, 64),
                                      (4, 14, 1024, 128), (8, 14, 1024, 256), (4, 4, 256, 256),
                                      (16, 7, 2048, 512)])
