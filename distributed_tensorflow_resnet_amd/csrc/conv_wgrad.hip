@@ -461,10 +461,6 @@ int wgrad_pick_splits(const ConvGeom& g, int* px_per_split) {
   const long slab = (long)g.K * NT * 4;
   const long cap_bytes = (cap_mb << 20) / (slab > 0 ? slab : 1);
   if (splits > cap_bytes) splits = cap_bytes;
-  // ... but never below ~2 workgroups per CU: the cap alone left the big-output layers
-  // (7x7 3x3 512: one 9.4 MB slab -> 144 workgroups of 98 K-tiles) on a fraction of the chip
-  const long min_wg = tune(T_WGRAD_MIN_WG);
-  if (splits * tiles < min_wg) splits = (min_wg + tiles - 1) / tiles;
   long maxs = P / 256;
   if (maxs < 1) maxs = 1;
   if (splits > maxs) splits = maxs;

@@ -57,9 +57,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"wgrad_slab_mb", 16,
      "split-K wgrad: cap of one layer's fp32 partial slabs, MB (RN50 bs128, back to back: "
      "32 10.68 / 10.70 ms, 16 10.62 / 10.60, 12 10.79, 8 11.38)"},
-    {"wgrad_min_wg", 0,
-     "split-K wgrad: workgroups the split count never goes below (the slab cap would leave "
-     "big-output layers on a fraction of the chip); 0 off"},
     {"fin_v", 1,
      "BN finalize variant: 1 auto (per-channel one-round kernel for many partials), 0 LDS "
      "tree, 2 one-round"},

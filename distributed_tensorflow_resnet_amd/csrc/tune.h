@@ -34,7 +34,6 @@ enum TuneId : int {
   T_WGD_BMP64,
   T_WGRAD_TARGET_WG,   // split-K wgrad: target workgroups
   T_WGRAD_SLAB_MB,     // split-K wgrad: cap of one layer's fp32 partial slabs (MB)
-  T_WGRAD_MIN_WG,      // split-K wgrad: workgroups the split count never goes below
   T_FIN_V,             // BN finalize kernel variant (-1 auto)
   T_BWD_APPLY_FIN,     // BN backward apply finalizes in-kernel when the grid allows
   T_WT_STORE,          // conv epilogue write-through stores (-1 auto, 0 off, 1 on)
