@@ -488,22 +488,6 @@ static Launch mk_sgd_update_pack(ptr_t master, ptr_t grad, ptr_t mom, long n, fl
   };
 }
 
-static Launch mk_sgd_ohwi(ptr_t master, ptr_t grad, ptr_t mom, float init, long long warm_steps,
-                          float warm_from, float warm_to, std::vector<long long> bounds,
-                          std::vector<float> vals, ptr_t gstep, float momentum, float wd,
-                          float grad_scale, int use_momentum, ptr_t segs, ptr_t tile0, int nseg,
-                          long long tiles, ptr_t flat, int nflat, long long flat_n, ptr_t bf,
-                          ptr_t lr_out, ptr_t arrive) {
-  if (gstep == 0 || arrive == 0) throw std::invalid_argument("sgd_ohwi: gstep and arrive needed");
-  const LrSchedule sc = make_sched(init, warm_steps, warm_from, warm_to, bounds, vals);
-  return [=](hipStream_t s) {
-    sgd_ohwi(P<float>(master), P<const float>(grad), P<float>(mom), sc, P<long long>(gstep),
-             momentum, wd, grad_scale, use_momentum, P<const ParamSeg>(segs),
-             P<const long long>(tile0), nseg, tiles, P<const long long>(flat), nflat, flat_n,
-             P<bf16>(bf), P<float>(lr_out), P<unsigned>(arrive), s);
-  };
-}
-
 static Launch mk_step_increment(ptr_t gstep) {
   return [=](hipStream_t s) { step_increment(P<long long>(gstep), s); };
 }
@@ -1073,7 +1057,6 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "maxpool_bwd", mk_maxpool_bwd);
   def_op(m, plan, "sgd_update_pack", mk_sgd_update_pack);
   def_op(m, plan, "ohwi_pack", mk_ohwi_pack);
-  def_op(m, plan, "sgd_ohwi", mk_sgd_ohwi);
   def_op(m, plan, "step_increment", mk_step_increment);
   def_op(m, plan, "l2_half_sum", mk_l2_half_sum);
   def_op(m, plan, "fill", mk_fill);

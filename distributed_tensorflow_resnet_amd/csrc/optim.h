@@ -22,13 +22,6 @@ void sgd_update_pack(float* master, const float* grad, float* mom, long n, const
 // gstep_inc (optional): global_step += 1 in the same launch.
 void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0, int nseg,
                long long total_tiles, bf16* bf, long long* gstep_inc, hipStream_t s);
-// Both in one launch (sgd_update_pack + ohwi_pack + global_step += 1), tile by tile; flat =
-// [offset, numel] pairs of the tensors without an OHWI copy; arrive: a zeroed counter.
-void sgd_ohwi(float* master, const float* grad, float* mom, const LrSchedule& s,
-              long long* gstep, float momentum, float wd, float grad_scale, int use_momentum,
-              const ParamSeg* segs, const long long* tile0, int nseg, long long tiles,
-              const long long* flat, int nflat, long long flat_n, bf16* bf, float* lr_out,
-              unsigned* arrive, hipStream_t st);
 void step_increment(long long* gstep, hipStream_t s);
 int l2_workspace_floats();
 void l2_half_sum(const float* v, long n, float* ws, float* out, hipStream_t s);

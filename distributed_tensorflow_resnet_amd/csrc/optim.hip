@@ -212,130 +212,6 @@ void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0
   DTR_CHECK_LAUNCH();
 }
 
-// The training step's optimizer as ONE launch: sgd_pack's update + ohwi_pack's OHWI
-// transpose, tile by tile.  Block b < tiles owns one 64 x 64 tile of a weight's HWIO
-// matrix ([tap*C + ci][co]): it updates its elements (reads along co, coalesced), writes
-// the fp32 master, momentum and HWIO bf16 copy, stages the bf16 values in LDS and writes
-// them transposed into the OHWI copy (along tap*C + ci, coalesced) -- so the OHWI copy
-// never re-reads the fp32 master and the second launch is gone.  (The earlier fused form,
-// scattered 2-byte OHWI stores from the flat update, was slower than the two launches:
-// profiles/rejected_experiments_r2.md.)  Blocks b >= tiles update the tensors without an
-// OHWI copy (BatchNorm gammas / betas, biases), listed as flat ranges.  global_step += 1
-// by the last block to arrive (every block read global_step before arriving).
-__global__ void __launch_bounds__(256)
-sgd_ohwi_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
-                LrSchedule sched, long long* __restrict__ gstep, float momentum, float wd,
-                float grad_scale, int use_momentum, const ParamSeg* __restrict__ segs,
-                const long long* __restrict__ tile0, int nseg, long long tiles,
-                const long long* __restrict__ flat, int nflat, long long flat_n,
-                bf16* __restrict__ bf, float* __restrict__ lr_out, unsigned* __restrict__ arrive) {
-  __shared__ bf16 tile[64][66];
-  __shared__ long long st0[SEG_LDS_MAX];
-  __shared__ int seg_of_block;
-  const long long b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const float lr = lr_at(sched, (long)*gstep);
-  if (lr_out && b == 0 && tid == 0) *lr_out = lr;
-  auto upd = [&](long e) -> float {   // sgd_pack's scalar arithmetic
-    float wj = w[e];
-    const float gj = g[e] * grad_scale + wd * wj;
-    if (use_momentum) {
-      const float acc = momentum * mom[e] + gj;
-      mom[e] = acc;
-      wj -= lr * acc;
-    } else {
-      wj -= lr * gj;
-    }
-    w[e] = wj;
-    return wj;
-  };
-  if (b < tiles) {
-    int lo = 0;
-    if (nseg <= SEG_LDS_MAX) {
-      for (int i = tid; i < nseg; i += blockDim.x) st0[i] = tile0[i];
-      __syncthreads();
-      if (tid == 0) {
-        int l = 0, h = nseg - 1;
-        while (l < h) {
-          const int mid = (l + h + 1) >> 1;
-          if (st0[mid] <= b) l = mid;
-          else h = mid - 1;
-        }
-        seg_of_block = l;
-      }
-      __syncthreads();
-      lo = seg_of_block;
-    } else {
-      int hi = nseg - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (tile0[mid] <= b) lo = mid;
-        else hi = mid - 1;
-      }
-    }
-    const ParamSeg& sg = segs[lo];
-    const int taps = sg.kh * sg.kw;
-    const int R = taps * sg.C;
-    const int tc_n = (sg.K + 63) / 64;
-    const int t = (int)(b - tile0[lo]);
-    const int tr = t / tc_n, tcol = t - tr * tc_n;
-    const int r0 = tr * 64, c0 = tcol * 64;
-    const int tx = tid & 63, ty = tid >> 6;
-    for (int i = ty; i < 64; i += 4) {       // rows r0+i, columns c0+tx: update + HWIO copy
-      const int r = r0 + i, co = c0 + tx;
-      bf16 h = (bf16)0.f;
-      if (r < R && co < sg.K) {
-        const float wj = upd(sg.offset + (long)r * sg.K + co);
-        h = (bf16)wj;
-        if (sg.bf_hwio >= 0) bf[sg.bf_hwio + (long)r * sg.kpad + co] = h;
-      }
-      tile[i][tx] = h;
-    }
-    __syncthreads();
-    for (int i = ty; i < 64; i += 4) {       // OHWI rows co = c0+i, columns r0+tx
-      const int co = c0 + i, r = r0 + tx;
-      if (co < sg.K && r < R) {
-        const int tap = r / sg.C, ci = r - tap * sg.C;
-        bf[sg.bf_ohwi + ((long)co * taps + tap) * sg.cpad + ci] = tile[tx][i];
-      }
-    }
-  } else {
-    // flat ranges [flat[2i], flat[2i] + flat[2i+1]) of the tensors without an OHWI copy
-    const long long base = (b - tiles) * 256 + tid;
-    for (long long k = base; k < flat_n; k += (gridDim.x - tiles) * 256LL) {
-      long long rem = k;
-      int i = 0;
-      while (i + 1 < nflat && rem >= flat[2 * i + 1]) rem -= flat[2 * i + 1], ++i;
-      upd(flat[2 * i] + rem);
-    }
-  }
-  // global_step += 1 once every block has read it (and is done)
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      *gstep += 1;
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-void sgd_ohwi(float* master, const float* grad, float* mom, const LrSchedule& s,
-              long long* gstep, float momentum, float wd, float grad_scale, int use_momentum,
-              const ParamSeg* segs, const long long* tile0, int nseg, long long tiles,
-              const long long* flat, int nflat, long long flat_n, bf16* bf, float* lr_out,
-              unsigned* arrive, hipStream_t st) {
-  long long fb = (flat_n + 255) / 256;
-  if (fb > 256) fb = 256;
-  const long long grid = tiles + fb;
-  if (grid <= 0) return;
-  hipLaunchKernelGGL(sgd_ohwi_kernel, dim3((unsigned)grid), dim3(256), 0, st, master, grad, mom,
-                     s, gstep, momentum, wd, grad_scale, use_momentum, segs, tile0, nseg, tiles,
-                     flat, nflat, flat_n, bf, lr_out, arrive);
-  DTR_CHECK_LAUNCH();
-}
-
 __global__ void step_incr_kernel(long long* gstep) {
   if (threadIdx.x == 0) *gstep += 1;
 }

@@ -343,14 +343,6 @@ class Engine:
         self.ohwi_tiles = int(sum(tiles))
         self.ohwi_tile0 = torch.tensor(np.concatenate([[0], np.cumsum(tiles)[:-1]]).astype(np.int64),
                                        device=self.device)
-        # sgd_ohwi (one optimizer launch): the tensors without an OHWI copy as flat ranges,
-        # and its arrival counter for global_step += 1
-        flat = [(int(r["offset"]), int(r["numel"])) for r in seg_arr if r["bf_ohwi"] < 0]
-        self.opt_flat_n = sum(n for _, n in flat)
-        self.opt_nflat = len(flat)
-        self.opt_flat = torch.tensor(np.array(flat or [(0, 0)], dtype=np.int64).reshape(-1),
-                                     device=self.device)
-        self.opt_arrive = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.wbf = torch.zeros(max(bf_total, 1), dtype=BF16, device=self.device)
         bptr = self.wbf.data_ptr()
         for rec, s in zip(seg_arr, ps.train_slots):
@@ -1231,25 +1223,15 @@ class Engine:
         # ---- optimizer
         b2 = plan.size()
         s = self.sched
-        if tune.get("fused_opt"):
-            # one launch: update + HWIO / OHWI bf16 copies tile by tile + global_step += 1
-            plan.sgd_ohwi(self.params.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(),
-                          s.init, s.warm_steps, s.warm_from, s.warm_to, list(s.bounds),
-                          list(s.values), self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
-                          int(self.use_momentum), self.segs.data_ptr(),
-                          self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
-                          self.opt_flat.data_ptr(), self.opt_nflat, self.opt_flat_n,
-                          self.wbf.data_ptr(), sp + 8, self.opt_arrive.data_ptr())
-        else:
-            plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
-                                 self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
-                                 s.warm_from, s.warm_to, list(s.bounds), list(s.values),
-                                 self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
-                                 int(self.use_momentum), self.segs.data_ptr(), self.nseg,
-                                 self.wbf.data_ptr(), sp + 8, 1)
-            plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
-                           self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
-                           self.wbf.data_ptr(), self.gstep.data_ptr())   # + global_step += 1
+        plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
+                             self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
+                             s.warm_from, s.warm_to, list(s.bounds), list(s.values),
+                             self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
+                             int(self.use_momentum), self.segs.data_ptr(), self.nseg,
+                             self.wbf.data_ptr(), sp + 8, 1)
+        plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
+                       self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr(),
+                       self.gstep.data_ptr())   # + global_step += 1
         if self.stem_s2d:
             plan.stem_s2d_pack(self.stem_master, self.stem_w4.data_ptr(), spec.stem.cout)
         self._t_opt_end = plan.timing_point("opt_end")

@@ -48,8 +48,6 @@ ENGINE = {
     "dgrad1x1_stream": (1, "1x1 stride-1 dgrads carrying BN-backward sums whose weights fit "
                            "in VGPRs (the expanding conv at stages 1-2, the first conv at "
                            "stage 3) on the streaming kernel bn_dgrad1x1 (store + sums)"),
-    "fused_opt": (0, "the optimizer as one launch (sgd_ohwi: update, HWIO / OHWI bf16 copies "
-                     "tile by tile, global_step += 1) instead of sgd_update_pack + ohwi_pack"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 
