@@ -192,8 +192,13 @@ class Engine:
         # after the stem (_split_tail).  0 = all on the side stream.  Measured (CIFAR RN50,
         # ms/step, 0 / 0.5 / 0.75 / 1): bs16 0.978 / 0.972 / 0.972 / 0.970, bs32 1.002 /
         # 0.994 / 1.017 / 1.011, bs64 1.128 / 1.131 / 1.131 / 1.130, bs128 1.326 / 1.316 /
-        # 1.314 / 1.303 (scripts/ab_tail.sh)
-        self.tail_main = min(1.0, max(0.0, tune.get("tail_main")))
+        # 1.314 / 1.303 (scripts/ab_tail.sh).  ImageNet, after the streaming 1x1 kernels
+        # shortened the main stream's chain: RN50 bs128 1 / 0.5 / 0.25 = 10.56 / 10.49 /
+        # 10.49 ms, RN101 bs256 1 / 0.5 = 32.78 / 32.66 ms (scripts/gpu_r3_final.sh).
+        tm = tune.get("tail_main")
+        if tm < 0:
+            tm = 1.0 if spec.dataset.startswith("cifar") else 0.5
+        self.tail_main = min(1.0, max(0.0, tm))
         # ...and the last reduces then run on the main stream behind one join
         # (reduce_main_tail=0: forked to the side stream like the earlier buckets)
         self.reduce_main_tail = bool(tune.get("reduce_main_tail"))

@@ -22,8 +22,10 @@ ENGINE = {
                        "cross-stream event edges poorly)"),
     "fork_every": (-1, "residual blocks per side-stream fork, -1 auto: 4 CIFAR (bs16 0.948 vs "
                        "0.959 / 1.012 ms at 2 / 8), 2 ImageNet (12.81 vs 12.91 ms at 4)"),
-    "tail_main": (1.0, "fraction of the backward tail's queued weight gradients run on the idle "
-                       "main stream after the stem (CIFAR bs128 1.326 -> 1.303 ms at 0 -> 1)"),
+    "tail_main": (-1.0, "fraction of the backward tail's queued weight gradients run on the "
+                        "idle main stream after the stem, -1 auto: 1 CIFAR (bs128 1.326 -> 1.303 "
+                        "ms at 0 -> 1), 0.5 ImageNet (RN50 10.56 -> 10.49 ms, RN101 32.78 -> "
+                        "32.66 ms at 1 -> 0.5)"),
     "reduce_main_tail": (1, "the last split-K reduces run on the main stream behind one join"),
     "reduce_mb": (-1.0, "split-K reduce group size in MB, -1 auto (~6 groups, <= 4 MB: CIFAR "
                         "RN50 -2.3 % step vs one group)"),
