@@ -230,8 +230,12 @@ int wgrad_direct_bmp(const ConvGeom& g) {
   int bmp = 0;
   if (g.C == 16 && g.W == 32) bmp = (int)tune(T_WGD_BMP16);
   else if (g.C == 32 && g.W == 16) bmp = (int)tune(T_WGD_BMP32);
-  else if (g.C == 64 && g.W == 8) bmp = (int)tune(T_WGD_BMP64);
   const long P = (long)g.N * g.H * g.W;
+  if (g.C == 64 && g.W == 8) {
+    bmp = (int)tune(T_WGD_BMP64);
+    // -1 auto: at 16 images (1024 pixels) the split-K implicit-GEMM wgrad wins
+    if (bmp < 0) bmp = P <= 1024 ? 0 : 256;
+  }
   const int lo = wgd_min_bmp(g.C);               // smallest instantiated tile
   const int hi = g.C == 16 ? 1024 : g.C == 32 ? 512 : 256;
   if (bmp < lo || bmp > hi || (bmp & (bmp - 1))) return 0;

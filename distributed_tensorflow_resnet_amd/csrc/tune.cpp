@@ -51,7 +51,9 @@ const TuneEntry kTable[T_COUNT] = {
      "workgroups the direct wgrad launches at least (small per-rank batches shrink its tiles)"},
     {"wgd_bmp16", 512, "direct wgrad pixels per split, 16 channels (256 -> 512: 1.396 -> 1.320 ms)"},
     {"wgd_bmp32", 512, "... 32 channels"},
-    {"wgd_bmp64", 256, "... 64 channels"},
+    {"wgd_bmp64", -1,
+     "... 64 channels, -1 auto: 256, or the implicit-GEMM wgrad at <= 1024 pixels (bs16 "
+     "step 0.928 -> 0.919 ms; bs128 1.277 vs 1.282 kept)"},
     {"wgrad_target_wg", 768,
      "split-K wgrad: target workgroups (3 per CU hide the per-tile load latency)"},
     {"wgrad_slab_mb", 16,
