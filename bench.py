@@ -37,12 +37,31 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 MODELS = {
-    # name: (dataset, size, batch, batch_is_global, baseline stp/s, baseline source)
+    # name: (dataset, size, batch, batch_is_global, headline baseline stp/s, its source)
     "cifar_resnet50": ("cifar10", 50, 128, True, 21.82, "README.md:16-22 (4x Titan Xp, Horovod)"),
     "cifar_resnet20": ("cifar10", 20, 128, True, None, None),
     "imagenet_resnet50": ("imagenet", 50, 128, False, 0.93, "README.md:39-44 (8 P100, 8ps-8wk)"),
     "imagenet_resnet101": ("imagenet", 101, 256, False, None, None),
 }
+# vs_baseline compares like with like: the reference row run on the same number of
+# GPUs when it published one (BASELINE.md rows 3 / 1 / 7 for CIFAR, 12 / 8 for
+# ImageNet), else the model's headline row above; the JSON names the row used.
+BASELINE_BY_GPUS = {
+    "cifar_resnet50": {1: (13.94, "BASELINE.md row 3: README.md:24-28 (1x P100, local)"),
+                       4: (21.82, "BASELINE.md row 1: README.md:16-22 (4x Titan Xp, Horovod)"),
+                       8: (28.66, "BASELINE.md row 7: README.md:31 (8x P100, Horovod)")},
+    "imagenet_resnet50": {1: (0.96, "BASELINE.md row 12: README.md:48 (1x P100, batch 128)"),
+                          8: (0.93, "BASELINE.md row 8: README.md:39-44 (8x P100, 8ps-8wk)")},
+}
+
+
+def baseline_for(model: str, n_gpus: int):
+    """(stp/s, source) of the reference number this run is compared with."""
+    row = BASELINE_BY_GPUS.get(model, {}).get(n_gpus)
+    if row is not None:
+        return row
+    b, src = MODELS[model][4], MODELS[model][5]
+    return (b, f"headline row (no {n_gpus}-GPU row published): {src}") if b else (None, None)
 DATA = {
     True: "synthetic: random uint8 32x32 CIFAR records, on-device pad-4/crop/flip/standardize "
           "every step; random-init weights",
@@ -263,7 +282,7 @@ def main(argv=None) -> int:
     if args.roctx:
         os.environ["DTR_ROCTX"] = "1"
 
-    dataset, size, batch, is_global, baseline, _src = MODELS[args.model]
+    dataset, size, batch, is_global, _b, _src = MODELS[args.model]
     if args.batch:
         batch = args.batch
     if is_global:
@@ -280,6 +299,7 @@ def main(argv=None) -> int:
     pg_world = dist.get_world_size() if dist.is_initialized() else 1
     backend = dist.get_backend() if dist.is_initialized() else None
     sps = args.steps / elapsed
+    baseline, baseline_src = baseline_for(args.model, world)
     if ctx.is_chief:
         out = {
             "metric": METRIC,
@@ -292,6 +312,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "strong" if is_global else "weak",
             "vs_baseline": round(sps / baseline, 3) if baseline else None,
+            "baseline": {"value": baseline, "source": baseline_src},
             "dtype": extra["dtype"],
             "data": DATA[dataset.startswith("cifar")] if args.device == "cuda" else
                     "synthetic uint8 batch (CPU fp32 trainer), random-init weights",

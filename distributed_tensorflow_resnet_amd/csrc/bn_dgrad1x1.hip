@@ -70,8 +70,8 @@ bnd1x1_kernel(BndArgs a) {
   constexpr int VPT = RT / RPI;        // row vectors per thread per tile
   constexpr int LDO = CW + 8;          // bf16 row stride of the staging tile
   static_assert(VPT >= 1 && RT % RPI == 0, "tile rows");
-  // staging tile; at the end (SUMS) the two [RPI][CW] fp32 reduction planes
-  constexpr int SO = RT * LDO > 4 * RPI * CW ? RT * LDO : 4 * RPI * CW;
+  // staging tile; at the end (SUMS) the two [RPI][CW] fp64 reduction planes
+  constexpr int SO = RT * LDO > 8 * RPI * CW ? RT * LDO : 8 * RPI * CW;
   __shared__ __attribute__((aligned(16))) bf16 so[SO];
   __shared__ __attribute__((aligned(16))) float prm[7][CW];
   __shared__ __attribute__((aligned(16))) bf16 sa[ALDS ? RT * LDA : 8];
@@ -135,9 +135,11 @@ bnd1x1_kernel(BndArgs a) {
   load_tile(rt, af, an, xv, av);
   __syncthreads();   // parameter table
 
-  float s1[8], s2[8];
+  // per-thread sums: each tile's VPT rows in fp32, the running sum over tiles in fp64
+  // (like bn_fwd1x1; RN101 bs256 folds ~200 rows per thread) -- ADVICE r3
+  double s1[8], s2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.0;
 
   for (; rt < nrt; rt += rstep) {
     f32x4 acc[MR][NR];
@@ -188,7 +190,9 @@ bnd1x1_kernel(BndArgs a) {
     }
     if (rt + rstep < nrt) load_tile(rt + rstep, af, an, xv, av);
 
-    float sc[8], sh[8], mu[8], rs[8];
+    float sc[8], sh[8], mu[8], rs[8], t1[8], t2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t1[j] = t2[j] = 0.f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const f32x4 p0 = *reinterpret_cast<const f32x4*>(&prm[0][cg * 8 + 4 * h]);
@@ -214,8 +218,8 @@ bnd1x1_kernel(BndArgs a) {
         for (int j = 0; j < 8; ++j) {
           const float xf = (float)xc[v][j];
           const float gg = (xf * sc[j] + sh[j] > 0.f) ? (float)gv[j] : 0.f;
-          s1[j] += gg;
-          s2[j] += gg * (xf - mu[j]) * rs[j];
+          t1[j] += gg;
+          t2[j] += gg * (xf - mu[j]) * rs[j];
         }
       } else {
         float ca[8], cb[8], cc[8];
@@ -242,13 +246,20 @@ bnd1x1_kernel(BndArgs a) {
         *reinterpret_cast<bf16x8*>(a.out + (long)(rt * RT + rl) * C + c0 + cg * 8) = o;
       }
     }
+    if constexpr (MODE != 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += (double)t1[j];
+        s2[j] += (double)t2[j];
+      }
+    }
     lds_barrier();   // the staging tile is rewritten by the next tile
   }
 
   if constexpr (MODE != 1) {
     // fold the RPI threads of each channel group (fixed order), then one fp64 atomic pair
     // per channel and workgroup into the accumulator replica
-    float* red = reinterpret_cast<float*>(so);   // [2][RPI][CW]
+    double* red = reinterpret_cast<double*>(so);   // [2][RPI][CW]
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[r0 * CW + cg * 8 + j] = s1[j];
@@ -256,12 +267,12 @@ bnd1x1_kernel(BndArgs a) {
     }
     __syncthreads();
     for (int c = tid; c < CW; c += 256) {
-      float t1 = 0.f, t2 = 0.f;
+      double t1 = 0.0, t2 = 0.0;
       for (int q = 0; q < RPI; ++q) {
         t1 += red[q * CW + c];
         t2 += red[RPI * CW + q * CW + c];
       }
-      bn_acc_add(a.bacc, C, c0 + c, (double)t1, (double)t2);
+      bn_acc_add(a.bacc, C, c0 + c, t1, t2);
     }
   }
 }

@@ -3,6 +3,7 @@
 #include "tune.h"
 
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -92,6 +93,13 @@ const TuneEntry kTable[T_COUNT] = {
 std::atomic<long> g_val[T_COUNT];
 std::once_flag g_once;
 
+std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) --b;
+  return s.substr(a, b - a);
+}
+
 void load() {
   for (int i = 0; i < T_COUNT; ++i) g_val[i].store(kTable[i].dflt);
   const char* env = std::getenv("DTR_TUNE");
@@ -104,9 +112,21 @@ void load() {
     const std::string item = s.substr(p, q - p);
     const size_t eq = item.find('=');
     if (eq != std::string::npos) {
-      const std::string k = item.substr(0, eq);
-      for (int i = 0; i < T_COUNT; ++i)
-        if (k == kTable[i].key) g_val[i].store(std::strtol(item.c_str() + eq + 1, nullptr, 10));
+      // keys and values trimmed like utils/tune.py; a value that is not a whole
+      // integer is rejected loudly instead of being truncated by strtol
+      const std::string k = trim(item.substr(0, eq));
+      const std::string v = trim(item.substr(eq + 1));
+      for (int i = 0; i < T_COUNT; ++i) {
+        if (k != kTable[i].key) continue;
+        char* end = nullptr;
+        const long val = std::strtol(v.c_str(), &end, 10);
+        if (v.empty() || end == nullptr || *end != '\0') {
+          std::fprintf(stderr, "DTR_TUNE: %s=%s is not an integer; keeping the default %ld\n",
+                       k.c_str(), v.c_str(), kTable[i].dflt);
+          break;
+        }
+        g_val[i].store(val);
+      }
       // keys of the Python engine (utils/tune.py) are validated there
     }
     p = q + 1;

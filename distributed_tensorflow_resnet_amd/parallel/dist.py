@@ -189,8 +189,12 @@ class DistContext:
                 if kind == "rccl":
                     comm = nat.Comm(ident, world, rank, device_index)
                 else:
+                    # the transport's own attach timeout fires well inside the
+                    # deadline, so a missing peer reaches the agreed c10d fallback
+                    # below instead of the deadline's exit
                     comm = nat.Comm.shm(ident.decode(), world, rank, device_index,
-                                        timeout_s=self.timeout_s)
+                                        timeout_s=self.timeout_s,
+                                        init_timeout_s=max(1.0, 0.8 * self.timeout_s))
             except Exception as e:   # noqa: BLE001 - reported as the fallback reason
                 err = f"{kind} init failed on rank {rank}: {e}"
         if not self._agree(comm is not None):

@@ -200,28 +200,84 @@ def read_frozen(path: str):
     return meta, tensors
 
 
+def _initializer_nodes(p, dims: list) -> tuple[list, str]:
+    """The initializer subgraph TF 1.12 builds in front of a variable (op names as in
+    the reference's resnet50_cifar_eval_graph.meta): conv kernels variance-scaling
+    truncated normal (resnet_model_official.py:90), the dense kernel glorot uniform,
+    gamma / moving_variance ones, the rest zeros.  Returns (nodes, output name)."""
+    f32, i32 = ("type", 1), ("type", 3)
+    base = f"{p.name}/Initializer"
+    shape = np.asarray(dims, dtype=np.int32)
+    if p.kind == "conv":
+        r = f"{base}/truncated_normal"
+        fan_in = int(np.prod(dims[:-1]))
+        std = np.asarray(np.sqrt(1.0 / fan_in) / 0.87962566103423978, np.float32)
+        return [gd.Node(f"{r}/shape", "Const", [], "", {"dtype": i32, "value": shape}),
+                gd.Node(f"{r}/mean", "Const", [], "", {"dtype": f32, "value": np.asarray(0.0, np.float32)}),
+                gd.Node(f"{r}/stddev", "Const", [], "", {"dtype": f32, "value": std}),
+                gd.Node(f"{r}/TruncatedNormal", "TruncatedNormal", [f"{r}/shape"], "",
+                        {"T": i32, "dtype": f32, "seed": 0, "seed2": 0}),
+                gd.Node(f"{r}/mul", "Mul", [f"{r}/TruncatedNormal", f"{r}/stddev"], "", {"T": f32}),
+                gd.Node(r, "Add", [f"{r}/mul", f"{r}/mean"], "", {"T": f32})], r
+    if p.kind == "dense_kernel":
+        r = f"{base}/random_uniform"
+        lim = np.asarray(np.sqrt(6.0 / (dims[0] + dims[1])), np.float32)
+        return [gd.Node(f"{r}/shape", "Const", [], "", {"dtype": i32, "value": shape}),
+                gd.Node(f"{r}/min", "Const", [], "", {"dtype": f32, "value": np.asarray(-lim, np.float32)}),
+                gd.Node(f"{r}/max", "Const", [], "", {"dtype": f32, "value": lim}),
+                gd.Node(f"{r}/RandomUniform", "RandomUniform", [f"{r}/shape"], "",
+                        {"T": i32, "dtype": f32, "seed": 0, "seed2": 0}),
+                gd.Node(f"{r}/sub", "Sub", [f"{r}/max", f"{r}/min"], "", {"T": f32}),
+                gd.Node(f"{r}/mul", "Mul", [f"{r}/RandomUniform", f"{r}/sub"], "", {"T": f32}),
+                gd.Node(r, "Add", [f"{r}/mul", f"{r}/min"], "", {"T": f32})], r
+    ones = p.kind in ("gamma", "moving_variance")
+    r = f"{base}/{'ones' if ones else 'zeros'}"
+    return [gd.Node(r, "Const", [], "", {"dtype": f32,
+                                         "value": np.full(dims, 1.0 if ones else 0.0,
+                                                          dtype=np.float32)})], r
+
+
 def export_eval_meta_graph(spec: ModelSpec, tensors: dict) -> bytes:
     """The eval graph BEFORE freezing, as a MetaGraphDef (reference
     resnet_cifar_frozen_model.py:91-96, export_meta_graph ->
     resnet50_cifar_eval_graph.meta): the frozen GraphDef's weight Consts are
     VariableV2 nodes again (same names, dtypes and shapes, no values -- those
-    live in the checkpoint), plus `global_step`, and the variables /
-    trainable_variables collections.  Node names are exactly the `.pb`'s."""
+    live in the checkpoint), each behind its initializer subgraph and followed by
+    its `<v>/Assign`, plus `global_step`, and the variables / trainable_variables
+    collections whose VariableDefs name the initializer op and initial value
+    (so tf.train.import_meta_graph / freeze_graph can rebuild the Variables).
+    The other node names are exactly the `.pb`'s."""
     graph = export_graphdef(spec, tensors)
     params = {p.name: p for p in spec.params}
     nodes = []
+    inits = {}
     for n in graph.nodes:
         if n.op == "Const" and n.name in params:
             dims = list(np.asarray(n.attr["value"]).shape)
+            init_nodes, init = _initializer_nodes(params[n.name], dims)
+            nodes += init_nodes
             n = gd.Node(n.name, "VariableV2", [], n.device,
                         {"container": b"", "dtype": ("type", 1), "shape": gd.Shape(dims),
                          "shared_name": b"", "_output_shapes": [gd.Shape(dims)]})
+            nodes.append(n)
+            nodes.append(gd.Node(f"{n.name}/Assign", "Assign", [n.name, init], "",
+                                 {"T": ("type", 1), "use_locking": True,
+                                  "validate_shape": True}))
+            inits[n.name] = (f"{n.name}/Assign", f"{init}:0")
+            continue
         nodes.append(n)
-    nodes.insert(0, gd.Node("global_step", "VariableV2", [], "",
-                            {"container": b"", "dtype": ("type", 9), "shape": gd.Shape([]),
-                             "shared_name": b"", "_output_shapes": [gd.Shape([])]}))
+    gs = [gd.Node("global_step/Initializer/zeros", "Const", [], "",
+                  {"dtype": ("type", 9), "value": np.asarray(0, np.int64)}),
+          gd.Node("global_step", "VariableV2", [], "",
+                  {"container": b"", "dtype": ("type", 9), "shape": gd.Shape([]),
+                   "shared_name": b"", "_output_shapes": [gd.Shape([])]}),
+          gd.Node("global_step/Assign", "Assign", ["global_step", "global_step/Initializer/zeros"],
+                  "", {"T": ("type", 9), "use_locking": True, "validate_shape": True})]
+    nodes = gs + nodes
+    inits["global_step"] = ("global_step/Assign", "global_step/Initializer/zeros:0")
     trainable = {p.name for p in spec.trainables}
-    variables = [("global_step", False)] + [(p.name, p.name in trainable) for p in spec.params]
+    variables = [("global_step", False) + inits["global_step"]] + \
+        [(p.name, p.name in trainable) + inits[p.name] for p in spec.params]
     return gd.encode_meta_graph(gd.Graph(nodes, graph.producer, graph.min_consumer), variables)
 
 
@@ -242,7 +298,11 @@ def freeze(prefix: str, out_path: str, dataset: str, resnet_size: int,
         kind = "cifar" if spec.dataset.startswith("cifar") else "imagenet"
         meta_path = os.path.join(os.path.dirname(os.path.abspath(out_path)),
                                  f"resnet{resnet_size}_{kind}_eval_graph.meta")
-    if meta_path:
+    if meta_path and os.path.exists(meta_path):
+        # like the reference (resnet_cifar_frozen_model.py:92): an existing eval meta
+        # graph -- possibly TF's own -- is kept, never overwritten
+        pass
+    elif meta_path:
         tmp = meta_path + ".tmp"
         with open(tmp, "wb") as fh:
             fh.write(export_eval_meta_graph(spec, tensors))

@@ -379,8 +379,10 @@ def encode_meta_graph(g: Graph, variables, tf_version: str = "1.12.0") -> bytes:
     """MetaGraphDef (the `.meta` of tf.train.export_meta_graph): field 1
     MetaInfoDef {meta_graph_version, tensorflow_version}, field 2 the GraphDef,
     field 4 the collections "variables" / "trainable_variables" as serialized
-    VariableDef {variable_name "<v>:0", snapshot_name "<v>/read:0"} (bytes_list).
-    ``variables``: [(name, trainable)] in creation order."""
+    VariableDef {variable_name "<v>:0", initializer_name "<v>/Assign", snapshot_name
+    "<v>/read:0", initial_value_name "<init>:0", trainable} (bytes_list).
+    ``variables``: [(name, trainable[, initializer_name, initial_value_name])] in
+    creation order."""
     out = bytearray()
     info = bytearray()
     _bytes_field(info, 1, f"v{tf_version}".encode())
@@ -389,12 +391,17 @@ def encode_meta_graph(g: Graph, variables, tf_version: str = "1.12.0") -> bytes:
     _bytes_field(out, 2, encode_graph(g))
     for key, keep in (("trainable_variables", lambda t: t), ("variables", lambda t: True)):
         blist = bytearray()
-        for name, trainable in variables:
+        for v in variables:
+            name, trainable = v[0], v[1]
             if not keep(trainable):
                 continue
             vdef = bytearray()
             _bytes_field(vdef, 1, f"{name}:0".encode())
+            if len(v) > 2:
+                _bytes_field(vdef, 2, v[2].encode())
             _bytes_field(vdef, 3, f"{name}/read:0".encode())
+            if len(v) > 3:
+                _bytes_field(vdef, 6, v[3].encode())
             if trainable:
                 _varint_field(vdef, 7, 1)
             _bytes_field(blist, 1, bytes(vdef))
@@ -432,6 +439,29 @@ def read_meta_info(path: str) -> dict:
                                             names.append(v5.decode().rsplit(":", 1)[0])
             info["collections"][key] = names
     return info
+
+
+def read_variable_defs(path: str) -> dict:
+    """{collection: [{field number: value}]} of the VariableDefs in a `.meta`."""
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    out = {}
+    for f, _, v in _proto_fields(buf):
+        if f != 4:
+            continue
+        key, defs = None, []
+        for f2, _, v2 in _proto_fields(v):
+            if f2 == 1:
+                key = v2.decode()
+            elif f2 == 2:
+                for f3, _, v3 in _proto_fields(v2):
+                    if f3 == 2:
+                        for f4, _, v4 in _proto_fields(v3):
+                            if f4 == 1:
+                                defs.append({f5: (v5 if isinstance(v5, int) else v5.decode())
+                                             for f5, _, v5 in _proto_fields(v4)})
+        out[key] = defs
+    return out
 
 
 def write_graph(g: Graph, path: str) -> None:

@@ -67,10 +67,24 @@ def overrides() -> dict:
 
 def validate(native_keys=()) -> None:
     """Every DTR_TUNE key must be an engine or a native tuning key."""
-    known = set(ENGINE) | set(native_keys)
-    bad = sorted(set(overrides()) - known)
+    native_keys = set(native_keys)
+    known = set(ENGINE) | native_keys
+    ov = overrides()
+    bad = sorted(set(ov) - known)
     if bad:
         raise ValueError(f"unknown DTR_TUNE key(s) {bad}; known: {sorted(known)}")
+    # native values are integers (csrc/tune.cpp rejects anything else); so are the
+    # engine's integer keys -- a fractional value is an error, never truncated
+    for k, v in ov.items():
+        if k in native_keys or isinstance(ENGINE.get(k, (0.0,))[0], int):
+            _int(k, v)
+
+
+def _int(key: str, v: str) -> int:
+    try:
+        return int(v)
+    except ValueError:
+        raise ValueError(f"DTR_TUNE {key}={v!r}: an integer is required") from None
 
 
 def get(key: str):
@@ -79,4 +93,4 @@ def get(key: str):
     v = overrides().get(key)
     if v is None:
         return default
-    return type(default)(float(v)) if isinstance(default, int) else type(default)(v)
+    return _int(key, v) if isinstance(default, int) else type(default)(v)

@@ -22,6 +22,7 @@ from distributed_tensorflow_resnet_amd.utils.checkpoint import tf_to_state
 from distributed_tensorflow_resnet_amd.utils.tf_interp import Interpreter
 
 REF_DIR = "/root/reference/test/resnet50-cifar-ckpt-20190218"
+REF_EVAL_META = os.path.join(REF_DIR, "resnet50_cifar_eval_graph.meta")
 REF_PB = os.path.join(REF_DIR, "resnet50_cifar_frozen_model_eval.pb")
 if not os.path.exists(REF_PB):   # copy kept with the tests (tests/fixtures/README.md)
     REF_PB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures",
@@ -186,14 +187,17 @@ def test_freeze_writes_graphdef_and_predict_reads_reference(tmp_path, ref_tensor
     assert os.path.basename(meta_path) == "resnet50_cifar_eval_graph.meta"
     mg = gd.read_meta_graph(meta_path)
     pbg = gd.read_graph(out)
-    assert [n.name for n in mg.nodes if n.name != "global_step"] == [n.name for n in pbg.nodes]
+    def _init(name):   # the variables' initializer subgraphs and Assigns (meta graph only)
+        return "/Initializer" in name or name.endswith("/Assign") or name == "global_step"
+
+    assert [n.name for n in mg.nodes if not _init(n.name)] == [n.name for n in pbg.nodes]
     pb_ops = pbg.by_name()
     params = set(ref_tensors)
     for n in mg.nodes:
         if n.name in params:
             assert n.op == "VariableV2" and pb_ops[n.name].op == "Const"
             assert list(n.attr["shape"].dims) == list(np.asarray(ref_tensors[n.name]).shape)
-        elif n.name != "global_step":
+        elif not _init(n.name):
             assert n.op == pb_ops[n.name].op and n.inputs == pb_ops[n.name].inputs, n.name
     info = gd.read_meta_info(meta_path)
     assert info["tensorflow_version"] == "1.12.0"
@@ -210,6 +214,21 @@ def test_freeze_writes_graphdef_and_predict_reads_reference(tmp_path, ref_tensor
             if n.op == "VariableV2":
                 assert n.attr["shape"].dims == ref_vars[n.name].attr["shape"].dims, n.name
                 assert n.attr["dtype"] == ref_vars[n.name].attr["dtype"], n.name
+        # every variable carries its initializer + Assign like TF's own export,
+        # and the VariableDefs name them (import_meta_graph resolves initializer_name)
+        ref_ops = {n.name: n.op for n in ref_mg.nodes}
+        our_ops = {n.name: n.op for n in mg.nodes}
+        census = lambda ops, pat: sorted(o for k, o in ops.items() if pat in k)  # noqa: E731
+        assert census(our_ops, "/Initializer") == census(ref_ops, "/Initializer")
+        assert census(our_ops, "/Assign") == census(ref_ops, "/Assign")
+        ours_v, ref_v = gd.read_variable_defs(meta_path), gd.read_variable_defs(REF_EVAL_META)
+        for key in ("variables", "trainable_variables"):
+            assert ours_v[key] == ref_v[key], key
+    # freezing again into the same directory keeps the existing eval meta graph
+    before = open(meta_path, "rb").read()
+    open(meta_path, "ab").write(b"x")
+    frozen.freeze(prefix, out, "cifar10", 50)
+    assert open(meta_path, "rb").read() == before + b"x"
     meta2, t2 = frozen.read_frozen(out)
     assert meta2["resnet_size"] == 50
     for k, v in ref_tensors.items():

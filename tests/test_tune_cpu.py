@@ -97,3 +97,10 @@ def test_dtr_tune_parsing_and_validation(monkeypatch):
     monkeypatch.setenv("DTR_TUNE", "fork_every")
     with pytest.raises(ValueError, match="not key=value"):
         tune.overrides()
+    # integer keys never truncate a fractional value (strtol("12.5") == 12)
+    monkeypatch.setenv("DTR_TUNE", "wgrad_slab_mb=12.5")
+    with pytest.raises(ValueError, match="integer is required"):
+        tune.validate(["wgrad_slab_mb"])
+    monkeypatch.setenv("DTR_TUNE", "fork_every=2.5")
+    with pytest.raises(ValueError, match="integer is required"):
+        tune.get("fork_every")
