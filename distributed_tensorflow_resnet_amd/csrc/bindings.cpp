@@ -417,6 +417,48 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
   return [a](hipStream_t s) { head_fused(a, s); };
 }
 
+// Persistent small-batch CIFAR step (cifar_persist.hip).  mode 0: forward launch, 1:
+// backward launch.  ptrs = [blocks, bns, x_in, stem_w, fslot, bslot, bar, err, dense_w,
+// dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N,
+// classes, kpad, update_moving, wgrad_wgs]; floats = [grad_scale, momentum, eps].
+static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::vector<float> f) {
+  if (p.size() != 17 || n.size() != 7 || f.size() != 3)
+    throw std::invalid_argument("prn: 17 pointers, 7 ints, 3 floats");
+  PrnArgs a{};
+  a.blocks = P<const PrnBlock>(p[0]);
+  a.bns = P<const PrnBn>(p[1]);
+  a.x_in = P<const bf16>(p[2]);
+  a.stem_w = P<const bf16>(p[3]);
+  a.fslot = P<float>(p[4]);
+  a.bslot = P<float>(p[5]);
+  a.bar = P<unsigned>(p[6]);
+  a.err = P<int>(p[7]);
+  a.dense_w = P<const bf16>(p[8]);
+  a.dense_b = P<const float>(p[9]);
+  a.labels = P<const int>(p[10]);
+  a.pooled = P<bf16>(p[11]);
+  a.dlogits = P<bf16>(p[12]);
+  a.ws = P<float>(p[13]);
+  a.dpool = P<float>(p[14]);
+  a.dx0 = P<bf16>(p[15]);
+  a.items = P<const PrnItem>(p[16]);
+  a.nblocks = n[0];
+  a.nitems = n[1];
+  a.N = n[2];
+  a.classes = n[3];
+  a.kpad = n[4];
+  a.update_moving = n[5];
+  const int wgs = n[6];
+  a.grad_scale = f[0];
+  a.momentum = f[1];
+  a.eps = f[2];
+  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad))
+    throw std::invalid_argument("prn: unsupported shape");
+  if (mode == 0) return [a](hipStream_t s) { prn_forward(a, s); };
+  if (mode == 1) return [a, wgs](hipStream_t s) { prn_backward(a, wgs, s); };
+  throw std::invalid_argument("prn: mode 0 (forward) or 1 (backward)");
+}
+
 // bn_bwd_apply with the finalize fused in: fin = [acc, gamma, dgamma, dbeta, coef]
 static Launch mk_bn_bwd_apply_acc(ptr_t dy, ptr_t x, ptr_t mean, ptr_t rstd, ptr_t scale,
                                   ptr_t shift, std::vector<ptr_t> fin, ptr_t add, ptr_t dx, int M,
@@ -1051,6 +1093,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_apply_acc_fits", &bn_bwd_apply_acc_fits,
         "whether bn_bwd_apply_acc (finalize fused into the apply) covers (M, C)");
   def_op(m, plan, "head_fused", mk_head_fused);
+  def_op(m, plan, "prn", mk_prn);
+  m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, blocks, classes, kpad)");
+  m.def("prn_item_kind", &prn_item_kind, "weight-gradient item kind of a conv (cin, cout, k, stride)");
+  m.def("prn_struct_bytes", []() {
+    return std::vector<int>{(int)sizeof(PrnBn), (int)sizeof(PrnBlock), (int)sizeof(PrnItem)};
+  }, "sizeof PrnBn, PrnBlock, PrnItem (descriptor tables built in Python)");
   m.def("head_fused_supported", &head_fused_supported,
         "whether head_fused covers (N, HW, C, classes, kpad)");
   def_op(m, plan, "maxpool_fwd", mk_maxpool_fwd);
@@ -1082,14 +1130,6 @@ PYBIND11_MODULE(_C, m) {
     g.Ncol = mode == MODE_FWD ? c.K : c.C;
     return conv_direct_covers(g, mode);
   }, "whether conv_gemm(mode, geom) runs the direct 3x3 kernel");
-  m.def("persist_stage_fwd", [](ptr_t x0, ptr_t bn0_scale, ptr_t bn0_shift, ptr_t w, ptr_t gamma,
-                                ptr_t beta, ptr_t y, ptr_t stats, ptr_t bar, ptr_t err, int N,
-                                int L, float eps, ptr_t stream) {
-    PersistArgs a{P<const bf16>(x0), P<const float>(bn0_scale), P<const float>(bn0_shift),
-                  P<const bf16>(w), P<const float>(gamma), P<const float>(beta), P<bf16>(y),
-                  P<float>(stats), P<unsigned>(bar), P<int>(err), N, L, eps};
-    persist_stage_fwd(a, S(stream));
-  }, "prototype: L chained CIFAR stage-3 convs (3x3 64->64, 8x8) in one persistent launch");
   m.def("conv_ring_covers", [](int mode, std::vector<int> geom) {
     GemmArgs g{};
     g.g = geom_from(geom);

@@ -1,0 +1,1226 @@
+// Persistent small-batch CIFAR ResNet v2 step: the whole forward in one launch, the
+// whole backward (with its weight gradients) in one more.
+//
+// Why: at the per-rank batches of the strong-scaling headline config (global batch 128
+// over 4-8 GPUs = 16-32 images per rank) every CIFAR conv is a few MFMA microseconds
+// wrapped in a ~1.5 us kernel boundary plus a global-memory round trip of its operands
+// (profiles/cifar_direct_conv_phases.md); ~110 dependent launches set the step time.
+// Here one 512-thread workgroup owns one image for the whole network
+// (resnet_model_official.py:217-278, building_block :94-130):
+//   * the image's activations stay on-chip between layers: a conv's fp32 accumulators
+//     are rounded to bf16 in registers, the next BatchNorm + ReLU is applied from the
+//     registers straight into an LDS halo, and the next conv reads its B operand there;
+//     global memory only receives the tensors the backward needs (write-only);
+//   * BatchNorm's batch statistics are the only cross-image dependency: each workgroup
+//     publishes its image's per-channel (sum, sum of squares) -- or, backward, (sum g,
+//     sum g*xhat) -- in its own slot, one grid barrier, then every workgroup combines
+//     all slots in the same fixed order (fp64) -> bitwise-identical tables everywhere;
+//   * the next layer's weights are prefetched into registers by waves 1-7 while the
+//     current layer computes and waits (wave 0 polls the barrier), then stored to LDS;
+//   * MFMA orientation D[channel][pixel] = W[channel][k] x Act[k][pixel]
+//     (v_mfma_f32_16x16x32_bf16): a lane's accumulator holds 4 consecutive channels of
+//     one pixel, i.e. one 8-byte NHWC store / LDS write after the bf16 rounding;
+//   * pixels are kept in a "canonical" order per stage: parity-class-major on the 32x32
+//     and 16x16 maps, so every stride-2 dgrad tile (sub-pixel decomposition: 1, 2, 2 or
+//     4 taps per output parity class) is made of pixels of one class.
+// In the backward launch the workgroups beyond the N image workgroups compute the 52
+// weight gradients (dW = sum_p dy x im2col(relu(bn(x)))) per image group into fp32
+// slabs, each item as soon as the image workgroups' barrier counter says its dy is
+// published; the existing deterministic grouped reduce sums the slabs afterwards.
+//
+// Hand-off protocol (MI355X_MICROARCH.md, "Valid forms" row 1): every byte another
+// workgroup reads inside the launch (BN slots, output gradients) is stored
+// write-through (sc1), every storing wave drains (s_waitcnt vmcnt(0)) before its
+// workgroup's lane 0 adds to the barrier counter, consumers poll the counter with
+// relaxed agent loads and read the bytes with sc1 loads.  Every spin is bounded (2 s
+// of wall clock): a timed-out wait sets *err and the workgroup exits.
+// The grid must be co-resident: one workgroup per CU (LDS), grid <= CUs (host checks).
+#include <algorithm>
+#include <stdexcept>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace dtr {
+
+namespace {
+
+constexpr int PT = PRN_THREADS;
+constexpr int NW = PT / 64;                  // waves per workgroup
+constexpr long long kSpinTicks = 200000000;  // 2 s at 100 MHz
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// ---- geometry ---------------------------------------------------------------------
+template <int S>
+struct Stg {                                  // stage S: R x R maps, C channels
+  static constexpr int R = 32 >> S, C = 16 << S, U = C / 8, W2 = R + 2;
+  static constexpr int NPB = R * R / 16, NCB = C / 16;   // 16-pixel / 16-channel blocks
+  static constexpr int WPB = NPB >= NW ? 1 : NW / NPB;   // waves per pixel block
+  static constexpr int PBW = NPB >= NW ? NPB / NW : 1;   // pixel blocks per wave
+  static constexpr int CBW = NCB / WPB;                  // channel blocks per wave
+  static constexpr int TPW = PBW * CBW;                  // 16x16 tiles per wave
+  static_assert(CBW >= 1 && TPW <= 8, "tiles");
+};
+
+// canonical pixel index -> (h, w): parity-class-major on 32x32 / 16x16, row-major on 8x8
+template <int S>
+__device__ __forceinline__ void canon(int p, int& h, int& w) {
+  constexpr int R = Stg<S>::R;
+  if constexpr (R > 8) {
+    constexpr int Q = R * R / 4, H2 = R / 2;
+    const int cls = p / Q, idx = p - cls * Q;
+    h = 2 * (idx / H2) + (cls >> 1);
+    w = 2 * (idx % H2) + (cls & 1);
+  } else {
+    h = p / R;
+    w = p % R;
+  }
+}
+
+// this wave's tile t -> (pixel block, channel block)
+template <int S>
+__device__ __forceinline__ void tile_of(int wave, int t, int& pb, int& cb) {
+  using G = Stg<S>;
+  pb = (wave / G::WPB) * G::PBW + t / G::CBW;
+  cb = (wave % G::WPB) * G::CBW + t % G::CBW;
+}
+
+// LDS halo element offset: pixel `pix` (row-major in the (R+2)^2 halo, column hc),
+// channel c (multiple of 4) of a U-unit (8 channels per 16-B unit) image; units XOR-
+// swizzled by the halo column so the 16 pixel lanes of a fragment read spread over banks
+template <int U>
+__device__ __forceinline__ int haddr(int pix, int hc, int c) {
+  return (pix * U + ((c >> 3) ^ (hc & (U - 1)))) * 8 + (c & 7);
+}
+
+__device__ __forceinline__ bf16x8 lds16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ float ld_sc1_f(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_f(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 8-byte write-through store / load of 4 bf16 (buffer ops with the sc1 cache bit)
+__device__ __forceinline__ void st_sc1_b64(bf16* base, long elem, bf16x4 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 16);
+}
+__device__ __forceinline__ bf16x8 ld_sc1_b128(const bf16* base, long elem) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(base), 0, 0x7fffffff,
+                                                    0x00020000);
+  return __builtin_bit_cast(bf16x8, (u32x4)__builtin_amdgcn_raw_buffer_load_b128(rs, (int)(elem * 2), 0, 16));
+}
+
+// Opaque copies of the lane / wave ids: every per-tile address is derived from them
+// inside each block's code instead of being hoisted to the kernel entry and kept live
+// across the whole network (which spilled hundreds of registers).
+__device__ __forceinline__ int opaque_v(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ int opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// ---- grid barrier ---------------------------------------------------------------------
+// Wait until `target` arrivals; lane 0 of wave 0 polls.  Returns false when the wait
+// timed out (*err set): the caller exits.
+__device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* err, int* flag) {
+  if (threadIdx.x == 0) {
+    const long long t0 = wall_clock64();
+    int ok = 1;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > kSpinTicks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *flag = ok;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// drain (all waves, or only wave 0 -- the one that stored the hand-off bytes) + arrive;
+// the caller then issues its weight prefetch (waves 1-7) and waits (grid_wait)
+__device__ __forceinline__ void grid_arrive(unsigned* bar, bool drain_all) {
+  if (drain_all || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- weights: global -> registers (waves 1-7) -> LDS -----------------------------------
+struct WLoad {
+  const bf16* src;
+  int rows, K, KP;      // LDS rows x K (padded row KP; columns [K, KP - 8) zero)
+  int dgrad, cin, cout; // dgrad: rows = ci of HWIO [tap][ci][co], k = tap * cout + co
+};
+
+template <int NR>
+__device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
+  const int t = (int)threadIdx.x - 64;
+  if (t < 0 || L.src == nullptr) return;
+  const int upr = L.K / 8, units = L.rows * upr;
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int u = t + i * (PT - 64);
+    if (u < units) {
+      const int row = u / upr, j = u - row * upr;
+      long off;
+      if (L.dgrad) {
+        const int cu = L.cout / 8, tap = j / cu;
+        off = ((long)tap * L.cin + row) * L.cout + (j - tap * cu) * 8;
+      } else {
+        off = (long)row * L.K + j * 8;
+      }
+      r[i] = *reinterpret_cast<const bf16x8*>(L.src + off);
+    }
+  }
+}
+
+template <int NR>
+__device__ __forceinline__ void w_store(const WLoad& L, const bf16x8 (&r)[NR], bf16* wl) {
+  if (L.src == nullptr) return;
+  const int tid = threadIdx.x, t = tid - 64;
+  const int upr = L.K / 8, units = L.rows * upr;
+  if (t >= 0) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int u = t + i * (PT - 64);
+      if (u < units) {
+        const int row = u / upr, j = u - row * upr;
+        *reinterpret_cast<bf16x8*>(wl + row * L.KP + j * 8) = r[i];
+      }
+    }
+  }
+  const int pad = (L.KP - 8 - L.K) / 8;   // zero columns up to the last k-step
+  for (int q = tid; q < L.rows * pad; q += PT) {
+    const int row = q / pad, j = upr + (q - row * pad);
+    *reinterpret_cast<bf16x8*>(wl + row * L.KP + j * 8) = bf16x8{};
+  }
+}
+
+// 16-B weight units of a conv, and the prefetch registers waves 1-7 need for them
+__host__ __device__ constexpr int conv_units(int co, int ci, int ks) { return co * ks * ks * ci / 8; }
+__host__ __device__ constexpr int nreg(int units) { return (units + PT - 65) / (PT - 64); }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+__host__ __device__ constexpr int kpad_of(int K) { return ((K + 31) / 32) * 32 + 8; }
+
+__device__ __forceinline__ WLoad wl_fwd(const bf16* src, int co, int ci, int ks) {
+  return WLoad{src, co, ks * ks * ci, kpad_of(ks * ks * ci), 0, ci, co};
+}
+__device__ __forceinline__ WLoad wl_dgrad(const bf16* src, int co, int ci, int ks) {
+  return WLoad{src, ci, ks * ks * co, kpad_of(ks * ks * co), 1, ci, co};
+}
+
+// ---- convolutions on the LDS halo ------------------------------------------------------
+// acc[t] += sum_k W[channel][k] * Act[k][pixel] over this wave's tiles of output stage SO.
+// Forward (FLIP = false): input halo of CI channels at resolution R_SO * STR, tap (r, s)
+// of output pixel (h, w) at halo (h*STR + r + off, w*STR + s + off), off = 1 for 1x1.
+// Stride-1 dgrad (FLIP = true, 3x3): halo (h + 2 - r, w + 2 - s) of the output gradient.
+// Weights in LDS: [channel][k = tap * CI + ci] rows of KP.
+template <int SO, int CI, int KSZ, int STR, bool FLIP>
+__device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const bf16* wl,
+                                         int wave, int lane) {
+  lane = opaque_v(lane);
+  using G = Stg<SO>;
+  constexpr int RI = G::R * STR, W2I = RI + 2, UI = CI >= 8 ? CI / 8 : 1;
+  constexpr int K = KSZ * KSZ * CI, KS = (K + 31) / 32, KP = kpad_of(K);
+  constexpr int OFF = KSZ == 1 ? 1 : 0;
+  const int fr = lane & 15, fq = lane >> 4;
+  int hb[G::PBW], hcb[G::PBW];
+#pragma unroll
+  for (int i = 0; i < G::PBW; ++i) {
+    int pb, cb, h, w;
+    tile_of<SO>(wave, i * G::CBW, pb, cb);
+    canon<SO>(pb * 16 + fr, h, w);
+    hcb[i] = w * STR + OFF;
+    hb[i] = (h * STR + OFF) * W2I + hcb[i];
+  }
+  int cb0, pb0;
+  tile_of<SO>(wave, 0, pb0, cb0);
+#pragma unroll 2
+  for (int ks = 0; ks < KS; ++ks) {
+    const int k = ks * 32 + fq * 8;
+    int tap = k / CI;
+    const int c = k - tap * CI;
+    tap = tap < KSZ * KSZ ? tap : KSZ * KSZ - 1;   // padded k: zero weights
+    const int tr = FLIP ? KSZ - 1 - tap / KSZ : tap / KSZ;
+    const int ts = FLIP ? KSZ - 1 - tap % KSZ : tap % KSZ;
+    bf16x8 a[G::CBW];
+#pragma unroll
+    for (int j = 0; j < G::CBW; ++j) a[j] = lds16(wl + ((cb0 + j) * 16 + fr) * KP + k);
+#pragma unroll
+    for (int i = 0; i < G::PBW; ++i) {
+      const bf16x8 b = lds16(hal + haddr<UI>(hb[i] + tr * W2I + ts, hcb[i] + ts, c));
+#pragma unroll
+      for (int j = 0; j < G::CBW; ++j) acc[i * G::CBW + j] = mfma16(a[j], b, acc[i * G::CBW + j]);
+    }
+  }
+}
+
+// Stride-2 dgrad into output stage SO (high resolution, parity-class-major pixels) from
+// the output gradient of CO channels at resolution R_SO / 2 in the halo `hal`:
+//   3x3 (PROJ = false): dx(2i+a, 2j+b) = sum over taps r = a+1 (mod 2), s = b+1 (mod 2)
+//     of dy(i + di, j + dj) W[r][s], di = (a + 1 - r) / 2 -- 1, 2, 2 or 4 taps per class;
+//   1x1 (PROJ): dx(2i, 2j) = dy(i, j) Wp (class 0 only).
+// Weights [ci][k = tap * CO + co].  A wave's pixel blocks all lie in one class.
+template <int SO, int CO, bool PROJ>
+__device__ __forceinline__ void dgrad_s2_acc(f32x4 (&acc)[8], const bf16* hal, const bf16* wl,
+                                             int wave, int lane) {
+  lane = opaque_v(lane);
+  using G = Stg<SO>;
+  static_assert(G::R > 8, "class-major output");
+  constexpr int RL = G::R / 2, W2L = RL + 2, UL = CO / 8;
+  constexpr int KP = kpad_of(PROJ ? CO : 9 * CO);
+  const int fr = lane & 15, fq = lane >> 4;
+  int pb0, cb0;
+  tile_of<SO>(wave, 0, pb0, cb0);
+  const int cls = (pb0 * 16) / (G::R * G::R / 4);
+  const int ca = cls >> 1, cbit = cls & 1;
+  if (PROJ && cls != 0) return;
+  int il[G::PBW], jl[G::PBW];
+#pragma unroll
+  for (int i = 0; i < G::PBW; ++i) {
+    int pb, cb, h, w;
+    tile_of<SO>(wave, i * G::CBW, pb, cb);
+    canon<SO>(pb * 16 + fr, h, w);
+    il[i] = h >> 1;
+    jl[i] = w >> 1;
+  }
+  const int nr = PROJ ? 1 : (ca ? 2 : 1), ns = PROJ ? 1 : (cbit ? 2 : 1);
+  for (int ri = 0; ri < nr; ++ri) {
+    const int r = PROJ ? 0 : (ca ? 2 * ri : 1), di = PROJ ? 0 : (ca ? 1 - ri : 0);
+    for (int si = 0; si < ns; ++si) {
+      const int s = PROJ ? 0 : (cbit ? 2 * si : 1), dj = PROJ ? 0 : (cbit ? 1 - si : 0);
+      const int tap = PROJ ? 0 : r * 3 + s;
+#pragma unroll
+      for (int kk = 0; kk < CO / 32; ++kk) {
+        const int c = kk * 32 + fq * 8;
+        const int k = tap * CO + c;
+        bf16x8 av[G::CBW];
+#pragma unroll
+        for (int j = 0; j < G::CBW; ++j) av[j] = lds16(wl + ((cb0 + j) * 16 + fr) * KP + k);
+#pragma unroll
+        for (int i = 0; i < G::PBW; ++i) {
+          const int hr = il[i] + di + 1, hc = jl[i] + dj + 1;
+          const bf16x8 b = lds16(hal + haddr<UL>(hr * W2L + hc, hc, c));
+#pragma unroll
+          for (int j = 0; j < G::CBW; ++j) acc[i * G::CBW + j] = mfma16(av[j], b, acc[i * G::CBW + j]);
+        }
+      }
+    }
+  }
+}
+
+// ---- register tensors (bf16x4 per tile: 4 channels of one pixel) ------------------------
+template <int S>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[8]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// global NHWC element offset (within the image) of this lane's tile-t values
+template <int S>
+__device__ __forceinline__ int gofs(int wave, int lane, int t) {
+  using G = Stg<S>;
+  int pb, cb, h, w;
+  tile_of<S>(wave, t, pb, cb);
+  canon<S>(pb * 16 + (lane & 15), h, w);
+  return (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4);
+}
+
+template <int S>
+__device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, int wave, int lane) {
+  lane = opaque_v(lane);
+#pragma unroll
+  for (int t = 0; t < Stg<S>::TPW; ++t)
+    v[t] = *reinterpret_cast<const bf16x4*>(img_base + gofs<S>(wave, lane, t));
+}
+
+template <int S>
+__device__ __forceinline__ void store_regs(const bf16x4 (&v)[8], bf16* img_base, int wave, int lane,
+                                           bool sc1) {
+  lane = opaque_v(lane);
+#pragma unroll
+  for (int t = 0; t < Stg<S>::TPW; ++t) {
+    const int o = gofs<S>(wave, lane, t);
+    if (sc1) st_sc1_b64(img_base, o, v[t]);
+    else *reinterpret_cast<bf16x4*>(img_base + o) = v[t];
+  }
+}
+
+// v (stage S, this lane's tiles) -> halo interior, optionally BN + ReLU (LDS table
+// sc[c], sh[c]); the 1-pixel border is zeroed
+template <int S, bool BN>
+__device__ __forceinline__ void to_halo(bf16* hal, const bf16x4 (&v)[8], const float* sc,
+                                        const float* sh, int wave, int lane) {
+  lane = opaque_v(lane);
+  using G = Stg<S>;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < G::TPW; ++t) {
+    int pb, cb, h, w;
+    tile_of<S>(wave, t, pb, cb);
+    canon<S>(pb * 16 + fr, h, w);
+    const int c0 = cb * 16 + 4 * fq;
+    bf16x4 o = v[t];
+    if constexpr (BN) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)fmaxf((float)v[t][r] * sc[c0 + r] + sh[c0 + r], 0.f);
+    }
+    *reinterpret_cast<bf16x4*>(hal + haddr<G::U>((h + 1) * G::W2 + w + 1, w + 1, c0)) = o;
+  }
+  // border: 4 (R + 1) pixels x U units
+  constexpr int NB = 4 * (G::R + 1);
+  for (int q = threadIdx.x; q < NB * G::U; q += PT) {
+    const int b = q / G::U, u = q - b * G::U;
+    int hr, hc;
+    if (b < G::W2) { hr = 0; hc = b; }
+    else if (b < 2 * G::W2) { hr = G::R + 1; hc = b - G::W2; }
+    else if (b < 2 * G::W2 + G::R) { hr = b - 2 * G::W2 + 1; hc = 0; }
+    else { hr = b - 2 * G::W2 - G::R + 1; hc = G::R + 1; }
+    *reinterpret_cast<bf16x8*>(hal + haddr<G::U>(hr * G::W2 + hc, hc, u * 8)) = bf16x8{};
+  }
+}
+
+// Per-channel sums of two per-value quantities over this image -> red[wave][2][64];
+// f(t, r, x1, x2) fills them for value r of tile t.  Then wave 0 folds the waves that
+// hold each channel in a fixed order and stores the image's 2 x C sums to `slot` (sc1).
+template <int S, bool GLOBAL = true, typename F>
+__device__ __forceinline__ void image_sums(F f, float* red, float* slot, int wave, int lane) {
+  lane = opaque_v(lane);
+  using G = Stg<S>;
+  const int fr = lane & 15, fq = lane >> 4;
+  float s1[G::CBW][4], s2[G::CBW][4];
+#pragma unroll
+  for (int j = 0; j < G::CBW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < G::TPW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a, b;
+      f(t, r, a, b);
+      s1[t % G::CBW][r] += a;
+      s2[t % G::CBW][r] += b;
+    }
+#pragma unroll
+  for (int j = 0; j < G::CBW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      }
+  if (fr == 0) {
+    int pb, cb0;
+    tile_of<S>(wave, 0, pb, cb0);
+#pragma unroll
+    for (int j = 0; j < G::CBW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = (cb0 + j) * 16 + 4 * fq + r;
+        red[wave * 128 + c] = s1[j][r];
+        red[wave * 128 + 64 + c] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  // wave 0 alone stores the slot: it is the wave that drains before the barrier arrive
+  if (threadIdx.x < G::C) {
+    const int c = threadIdx.x;
+    const int grp = (c / 16) / G::CBW;   // waves w with w % WPB == grp hold channel c
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if (w % G::WPB == grp) v += red[w * 128 + which * 64 + c];
+      if (GLOBAL) st_sc1_f(slot + which * 64 + c, v);
+      else slot[which * 64 + c] = v;
+    }
+  }
+}
+
+// After the barrier: the N images' slots of one BN -> fp64 sums (fixed order), in
+// dsum[0..C) and dsum[64..64+C).  512 threads = 4 interleaved image slices x 128 values.
+__device__ __forceinline__ void combine_slots(const float* slots, int N, double* dred,
+                                              double* dsum) {
+  const int tid = threadIdx.x, v = tid & 127, part = tid >> 7;
+  double a = 0.0;
+  for (int n = part; n < N; n += 4) a += (double)ld_sc1_f(slots + (long)n * PRN_SLOT + v);
+  dred[part * 128 + v] = a;
+  __syncthreads();
+  if (tid < 128) dsum[tid] = (dred[tid] + dred[128 + tid]) + (dred[256 + tid] + dred[384 + tid]);
+  __syncthreads();
+}
+
+// forward BN: sums -> scale/shift (+ mean/rstd) table in LDS; image 0 publishes the batch
+// statistics and updates the moving averages (TF FusedBatchNorm semantics, bn_fused.h)
+__device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const double* dsum, int C, double M,
+                                             float eps, float momentum, int update_moving,
+                                             bool img0, float* tbl) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    const double dm = dsum[c] / M;
+    const double var = fmax(dsum[64 + c] / M - dm * dm, 0.0);
+    const float fmu = (float)dm, fvar = (float)var;
+    const float rs = rsqrtf(fvar + eps);
+    const float sc = bn.gamma[c] * rs;
+    const float sh = bn.beta[c] - fmu * sc;
+    tbl[c] = sc;
+    tbl[64 + c] = sh;
+    tbl[128 + c] = fmu;
+    tbl[192 + c] = rs;
+    if (img0) {
+      bn.mean[c] = fmu;
+      bn.rstd[c] = rs;
+      bn.scale[c] = sc;
+      bn.shift[c] = sh;
+      if (update_moving) {
+        const float uvar = M > 1.0 ? (float)(var * M / (M - 1.0)) : fvar;
+        const float mm = bn.mmean[c], mv = bn.mvar[c];
+        bn.mmean[c] = mm - (1.f - momentum) * (mm - fmu);
+        bn.mvar[c] = mv - (1.f - momentum) * (mv - uvar);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// backward BN: sums (sum g, sum g*xhat) -> coefficient table [a, b, c, mean, rstd, scale,
+// shift] x 64 (dh = a g - b - c xhat, bn_bwd_apply's formula); image 0 writes dgamma/dbeta
+__device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const double* dsum, int C, float M,
+                                             bool img0, float* tbl) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    const float sg = (float)dsum[c], sgx = (float)dsum[64 + c];
+    const float rs = bn.rstd[c];
+    const float a = bn.gamma[c] * rs;
+    tbl[c] = a;
+    tbl[64 + c] = a * sg / M;
+    tbl[128 + c] = a * sgx / M;
+    tbl[192 + c] = bn.mean[c];
+    tbl[256 + c] = rs;
+    tbl[320 + c] = bn.scale[c];
+    tbl[384 + c] = bn.shift[c];
+    if (img0) {
+      bn.dbeta[c] = sg;
+      bn.dgamma[c] = sgx;
+    }
+  }
+  __syncthreads();
+}
+
+// the forward BN table of a BN the forward launch finalized (backward launch: read back)
+__device__ __forceinline__ void bn_load_table(const PrnBn& bn, int C, float* tbl) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    tbl[c] = bn.scale[c];
+    tbl[64 + c] = bn.shift[c];
+    tbl[128 + c] = bn.mean[c];
+    tbl[192 + c] = bn.rstd[c];
+  }
+}
+
+// ---- LDS carve-up (bytes) ------------------------------------------------------------
+constexpr int HALO_B = 34 * 34 * 16 * 2;                 // 32x32x16 map + border
+constexpr int W1_B = 64 * kpad_of(576) * 2;               // 64 rows x 9*64 (+pad)
+constexpr int W2_B = 64 * kpad_of(32) * 2;                // projection (64 x 32 fwd / 32 x 64 dgrad)
+constexpr int TBL_B = 7 * 64 * 4;
+constexpr int RED_B = 8 * 128 * 4;                        // [8 waves][128] fp32 == [4][128] fp64
+constexpr int MISC_B = 256;
+constexpr int OFF_HA = 0, OFF_HB = OFF_HA + HALO_B, OFF_W1 = OFF_HB + HALO_B,
+              OFF_W2 = OFF_W1 + W1_B, OFF_TBL = OFF_W2 + W2_B, OFF_TBL2 = OFF_TBL + TBL_B,
+              OFF_RED = OFF_TBL2 + TBL_B, OFF_DSUM = OFF_RED + RED_B, OFF_MISC = OFF_DSUM + 128 * 8,
+              LDS_TOTAL = OFF_MISC + MISC_B;
+static_assert(LDS_TOTAL <= 163840, "LDS");
+
+struct Smem {
+  bf16 *ha, *hb, *w1, *w2;
+  float *tbl, *tbl2, *red;
+  double *dred, *dsum;
+  int* flag;
+};
+__device__ __forceinline__ Smem carve(char* s) {
+  Smem m;
+  m.ha = reinterpret_cast<bf16*>(s + OFF_HA);
+  m.hb = reinterpret_cast<bf16*>(s + OFF_HB);
+  m.w1 = reinterpret_cast<bf16*>(s + OFF_W1);
+  m.w2 = reinterpret_cast<bf16*>(s + OFF_W2);
+  m.tbl = reinterpret_cast<float*>(s + OFF_TBL);
+  m.tbl2 = reinterpret_cast<float*>(s + OFF_TBL2);
+  m.red = reinterpret_cast<float*>(s + OFF_RED);
+  m.dred = reinterpret_cast<double*>(s + OFF_RED);
+  m.dsum = reinterpret_cast<double*>(s + OFF_DSUM);
+  m.flag = reinterpret_cast<int*>(s + OFF_MISC);
+  return m;
+}
+
+// round accumulators (+ optional bf16 residual) to bf16 registers
+template <int S, bool RES>
+__device__ __forceinline__ void round_acc(bf16x4 (&o)[8], const f32x4 (&acc)[8], const bf16x4 (&res)[8]) {
+#pragma unroll
+  for (int t = 0; t < Stg<S>::TPW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[t][r] = (bf16)(RES ? acc[t][r] + (float)res[t][r] : acc[t][r]);
+}
+
+// =====================================================================================
+// forward
+// =====================================================================================
+template <int S_, int STR_, bool PROJ_>
+struct BlkTag {
+  static constexpr int S = S_, STR = STR_;
+  static constexpr bool PROJ = PROJ_;
+};
+
+struct FwdCtx {
+  const PrnArgs* a;
+  Smem m;
+  int img, wave, lane;
+  unsigned nbar;     // barriers passed
+};
+
+// forward BN statistics of v (stage S) into this image's slot of BN `bi`
+template <int S>
+__device__ __forceinline__ void fwd_stats(FwdCtx& x, const bf16x4 (&v)[8], int bi, int wave, int lane) {
+  float* slot = x.a->fslot + ((long)bi * x.a->N + x.img) * PRN_SLOT;
+  image_sums<S>([&](int t, int r, float& s1, float& s2) {
+    const float f = (float)v[t][r];
+    s1 = f;
+    s2 = f * f;
+  }, x.m.red, slot, wave, lane);
+}
+
+__device__ __forceinline__ void fwd_arrive(FwdCtx& x) { grid_arrive(x.a->bar, false); }
+__device__ __forceinline__ bool fwd_wait(FwdCtx& x) {
+  ++x.nbar;
+  return grid_wait(x.a->bar, x.nbar * (unsigned)x.a->N, x.a->err, x.m.flag);
+}
+
+__device__ __forceinline__ void fwd_combine(FwdCtx& x, int bi, int C, double M) {
+  const PrnArgs& a = *x.a;
+  combine_slots(a.fslot + (long)bi * a.N * PRN_SLOT, a.N, x.m.dred, x.m.dsum);
+  bn_fwd_table(a.bns[bi], x.m.dsum, C, M, a.eps, a.momentum, a.update_moving, x.img == 0, x.m.tbl);
+}
+
+// prefetch registers for the next block's conv1 after a stage-S block (stage S or S+1)
+template <int S>
+__host__ __device__ constexpr int nreg_next_fwd() {
+  return S < 2 ? cmax(nreg(conv_units(16 << S, 16 << S, 3)), nreg(conv_units(32 << S, 16 << S, 3)))
+               : nreg(conv_units(64, 64, 3));
+}
+
+// One building block, output stage S; STR 2: transition (input stage S-1, projection);
+// PROJ with STR 1: stage-0 block 0 (1x1 stride-1 projection).  On entry W1 (W2) hold
+// conv1's (the projection's) weights; on exit they hold the next block's.
+template <int S, int STR, bool PROJ>
+__device__ __forceinline__ bool block_fwd(FwdCtx& x, bf16x4 (&xr)[8], int bi_next,
+                                          const WLoad& next_w1, const WLoad& next_wp,
+                                          const PrnBlock& B) {
+  constexpr int SI = STR == 2 ? S - 1 : S;
+  using GI = Stg<SI>;
+  using G = Stg<S>;
+  const PrnArgs& a = *x.a;
+  const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
+  const double Mi = (double)a.N * GI::R * GI::R, Mo = (double)a.N * G::R * G::R;
+  const long img_o = (long)x.img * G::R * G::R * G::C;
+  // BN1 + ReLU of the block input -> halo A (input stage)
+  fwd_combine(x, B.bn1, GI::C, Mi);
+  to_halo<SI, true>(x.m.ha, xr, x.m.tbl, x.m.tbl + 64, wave, lane);
+  __syncthreads();
+  bf16x4 pr[8], hr[8];
+  f32x4 acc[8];
+  if constexpr (PROJ) {
+    zero_acc<S>(acc);
+    conv_acc<S, GI::C, 1, STR, false>(acc, x.m.ha, x.m.w2, wave, lane);
+    round_acc<S, false>(pr, acc, pr);
+  }
+  zero_acc<S>(acc);
+  conv_acc<S, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, wave, lane);
+  round_acc<S, false>(hr, acc, hr);
+  fwd_stats<S>(x, hr, B.bn2, wave, lane);
+  store_regs<S>(hr, B.h1 + img_o, wave, lane, false);
+  fwd_arrive(x);
+  {
+    bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
+    const WLoad L2 = wl_fwd(B.w2f, G::C, G::C, 3);
+    w_prefetch(L2, w2r);
+    if (!fwd_wait(x)) return false;
+    // BN2 + ReLU -> halo A, conv2 (+ residual)
+    fwd_combine(x, B.bn2, G::C, Mo);
+    to_halo<S, true>(x.m.ha, hr, x.m.tbl, x.m.tbl + 64, wave, lane);
+    w_store(L2, w2r, x.m.w1);
+  }
+  __syncthreads();
+  zero_acc<S>(acc);
+  conv_acc<S, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, wave, lane);
+  if constexpr (PROJ) round_acc<S, true>(xr, acc, pr);
+  else round_acc<S, true>(xr, acc, xr);
+  fwd_stats<S>(x, xr, bi_next, wave, lane);
+  store_regs<S>(xr, B.out + img_o, wave, lane, false);
+  fwd_arrive(x);
+  bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
+  w_prefetch(next_w1, w1r);
+  w_prefetch(next_wp, wpr);
+  if (!fwd_wait(x)) return false;
+  w_store(next_w1, w1r, x.m.w1);   // visible after the next block's first __syncthreads
+  w_store(next_wp, wpr, x.m.w2);
+  return true;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  FwdCtx x;
+  x.a = &a;
+  x.m = carve(smem);
+  x.img = blockIdx.x;
+  x.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  x.lane = threadIdx.x & 63;
+  x.nbar = 0;
+  const int tid = threadIdx.x;
+
+  // ---- stem: 3x3 8 -> 16 on the 32x32 image (no BN before it) ----
+  {
+    const bf16* src = a.x_in + (long)x.img * 1024 * 8;
+    for (int q = tid; q < 34 * 34; q += PT) {
+      const int hr = q / 34, hc = q - hr * 34;
+      bf16x8 v = {};
+      if (hr >= 1 && hr <= 32 && hc >= 1 && hc <= 32)
+        v = *reinterpret_cast<const bf16x8*>(src + ((hr - 1) * 32 + hc - 1) * 8);
+      *reinterpret_cast<bf16x8*>(x.m.ha + q * 8) = v;
+    }
+    constexpr int SKP = kpad_of(72);
+    for (int q = tid; q < 16 * (SKP / 8); q += PT) {
+      const int row = q / (SKP / 8), j = q - row * (SKP / 8);
+      bf16x8 v = {};
+      if (j < 9) v = *reinterpret_cast<const bf16x8*>(a.stem_w + row * 72 + j * 8);
+      *reinterpret_cast<bf16x8*>(x.m.w1 + row * SKP + j * 8) = v;
+    }
+    __syncthreads();
+  }
+  const PrnBlock& B0 = a.blocks[0];
+  bf16x4 xr[8];
+  {
+    f32x4 acc[8];
+    zero_acc<0>(acc);
+    conv_acc<0, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.wave, x.lane);
+    round_acc<0, false>(xr, acc, xr);
+    fwd_stats<0>(x, xr, B0.bn1, x.wave, x.lane);
+    store_regs<0>(xr, B0.x + (long)x.img * 1024 * 16, x.wave, x.lane, false);
+    fwd_arrive(x);
+    const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
+    WLoad LP{};
+    if (B0.wpf) LP = wl_fwd(B0.wpf, 16, 16, 1);
+    bf16x8 w1r[nreg(conv_units(16, 16, 3))], wpr[1];
+    w_prefetch(L1, w1r);
+    w_prefetch(LP, wpr);
+    if (!fwd_wait(x)) return;
+    w_store(L1, w1r, x.m.w1);
+    w_store(LP, wpr, x.m.w2);
+  }
+
+  // ---- blocks: per stage a transition block then identity blocks (straight-line
+  //      stages, no per-block switch: one register allocation region per variant) ----
+  const int nps = a.nblocks / 3;   // blocks per stage
+  auto run = [&](auto tag, int bi) -> bool {
+    constexpr int S = decltype(tag)::S, STR = decltype(tag)::STR;
+    constexpr bool PROJ = decltype(tag)::PROJ;
+    const PrnBlock& B = a.blocks[bi];
+    const bool last = bi + 1 == a.nblocks;
+    const int bnx = last ? 2 * a.nblocks : a.blocks[bi + 1].bn1;
+    WLoad n1{}, np{};
+    if (!last) {
+      const PrnBlock& Bn = a.blocks[bi + 1];
+      const int so = Bn.stage, si = Bn.stride == 2 ? so - 1 : so;
+      n1 = wl_fwd(Bn.w1f, 16 << so, 16 << si, 3);
+      if (Bn.wpf) np = wl_fwd(Bn.wpf, 16 << so, 16 << si, 1);
+    }
+    return block_fwd<S, STR, PROJ>(x, xr, bnx, n1, np, B);
+  };
+  if (!run(BlkTag<0, 1, true>{}, 0)) return;
+  for (int bi = 1; bi < nps; ++bi)
+    if (!run(BlkTag<0, 1, false>{}, bi)) return;
+  if (!run(BlkTag<1, 2, true>{}, nps)) return;
+  for (int bi = nps + 1; bi < 2 * nps; ++bi)
+    if (!run(BlkTag<1, 1, false>{}, bi)) return;
+  if (!run(BlkTag<2, 2, true>{}, 2 * nps)) return;
+  for (int bi = 2 * nps + 1; bi < 3 * nps; ++bi)
+    if (!run(BlkTag<2, 1, false>{}, bi)) return;
+
+  // ---- head (head.hip head_fused numerics): final BN + ReLU + average pool, dense,
+  //      softmax cross-entropy row, dense dgrad, pool gradient, final BN backward sums
+  const int fb = 2 * a.nblocks;
+  const int dunits = 64 * a.kpad / 8;
+  bf16x8 dwv = {};
+  if (tid < dunits) dwv = *reinterpret_cast<const bf16x8*>(a.dense_w + tid * 8);
+  fwd_combine(x, fb, 64, (double)a.N * 64);
+  float* tbl = x.m.tbl;
+  // dense weights -> W1 as fp32 [64][kpad]
+  float* wd = reinterpret_cast<float*>(x.m.w1);
+  if (tid < dunits)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wd[tid * 8 + j] = (float)dwv[j];
+  float* pool_s = x.m.tbl2;          // [0, 64) pooled, [64, 128) dp, [128, 192) g, [256, 384) sums
+  image_sums<2, false>([&](int t, int r, float& s1, float& s2) {
+    int pb, cb;
+    tile_of<2>(x.wave, t, pb, cb);
+    const int c = cb * 16 + 4 * (x.lane >> 4) + r;
+    s1 = fmaxf((float)xr[t][r] * tbl[c] + tbl[64 + c], 0.f);
+    s2 = 0.f;
+  }, x.m.red, pool_s + 256, x.wave, x.lane);
+  __syncthreads();
+  if (tid < 64) {
+    const bf16 pb = (bf16)(pool_s[256 + tid] / 64.f);
+    a.pooled[(long)x.img * 64 + tid] = pb;
+    pool_s[tid] = (float)pb;
+  }
+  __syncthreads();
+  if (x.wave == 0) {
+    const int lane = x.lane;
+    const int y = a.labels[x.img];
+    float z = -INFINITY;
+    if (lane < a.classes) {
+      float acc = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < 64; ++c) acc += pool_s[c] * wd[c * a.kpad + lane];
+      z = acc + a.dense_b[lane];
+    }
+    float mx = z;
+    int amax = lane < a.classes ? lane : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {   // first max on ties, like tf.argmax
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(amax, o, 64);
+      if (om > mx || (om == mx && oa < amax)) {
+        mx = om;
+        amax = oa;
+      }
+    }
+    const float se = wave_sum(lane < a.classes ? __expf(z - mx) : 0.f);
+    const float lse = mx + __logf(se);
+    const float zy = __shfl(z, (y >= 0 && y < a.classes) ? y : 0, 64);
+    float g = 0.f;
+    if (lane < a.classes) g = (__expf(z - lse) - (lane == y ? 1.f : 0.f)) * a.grad_scale;
+    if (lane < a.kpad) {
+      const bf16 gb = (bf16)g;
+      a.dlogits[(long)x.img * a.kpad + lane] = gb;
+      a.ws[(long)x.img * a.kpad + lane] = g;
+      pool_s[128 + lane] = (float)gb;
+    }
+    if (lane == 0) {
+      float* rs = a.ws + (long)a.N * a.kpad + 2 * x.img;
+      rs[0] = lse - ((y >= 0 && y < a.classes) ? zy : lse);
+      rs[1] = (amax == y) ? 1.f : 0.f;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float d = 0.f;
+    for (int k = 0; k < a.kpad; ++k) d += pool_s[128 + k] * wd[tid * a.kpad + k];
+    const float db = (float)(bf16)d;
+    const float dp = (float)(bf16)(db * (1.f / 64.f));
+    pool_s[64 + tid] = dp;
+    a.dpool[(long)x.img * 64 + tid] = dp;
+  }
+  __syncthreads();
+  // final BN backward sums of g = dp * relu'(bn(x)) (consumed by the backward launch)
+  float* bslot = a.bslot + ((long)fb * a.N + x.img) * PRN_SLOT;
+  image_sums<2>([&](int t, int r, float& s1, float& s2) {
+    int pb, cb;
+    tile_of<2>(x.wave, t, pb, cb);
+    const int c = cb * 16 + 4 * (x.lane >> 4) + r;
+    const float xf = (float)xr[t][r];
+    const float gg = (xf * tbl[c] + tbl[64 + c] > 0.f) ? pool_s[64 + c] : 0.f;
+    s1 = gg;
+    s2 = gg * (xf - tbl[128 + c]) * tbl[192 + c];
+  }, x.m.red, bslot, x.wave, x.lane);
+}
+
+// =====================================================================================
+// backward
+// =====================================================================================
+namespace {
+
+struct BwdCtx {
+  const PrnArgs* a;
+  Smem m;
+  int img, wave, lane;
+  unsigned nbar;
+};
+
+__device__ __forceinline__ void bwd_arrive(BwdCtx& x) { grid_arrive(x.a->bar + 1, true); }
+__device__ __forceinline__ bool bwd_wait(BwdCtx& x) {
+  ++x.nbar;
+  return grid_wait(x.a->bar + 1, x.nbar * (unsigned)x.a->N, x.a->err, x.m.flag);
+}
+
+// g = da * relu'(bn(xs)), xhat = (xs - mean) rstd with the forward table tb; sums -> slot
+template <int S>
+__device__ __forceinline__ void bwd_sums(BwdCtx& x, const bf16x4 (&da)[8], const bf16x4 (&xs)[8],
+                                         const float* tb, int bi, int wave, int lane) {
+  lane = opaque_v(lane);
+  float* slot = x.a->bslot + ((long)bi * x.a->N + x.img) * PRN_SLOT;
+  image_sums<S>([&](int t, int r, float& s1, float& s2) {
+    int pb, cb;
+    tile_of<S>(wave, t, pb, cb);
+    const int c = cb * 16 + 4 * (lane >> 4) + r;
+    const float xf = (float)xs[t][r];
+    const float gg = (xf * tb[c] + tb[64 + c] > 0.f) ? (float)da[t][r] : 0.f;
+    s1 = gg;
+    s2 = gg * (xf - tb[128 + c]) * tb[192 + c];
+  }, x.m.red, slot, wave, lane);
+}
+
+// dh = a g - b - c xhat (+ add) with the backward coefficient table cf
+template <int S, bool ADD>
+__device__ __forceinline__ void bwd_apply(bf16x4 (&out)[8], const bf16x4 (&da)[8],
+                                          const bf16x4 (&xs)[8], const bf16x4 (&add)[8],
+                                          const float* cf, int wave, int lane) {
+  lane = opaque_v(lane);
+#pragma unroll
+  for (int t = 0; t < Stg<S>::TPW; ++t) {
+    int pb, cb;
+    tile_of<S>(wave, t, pb, cb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = cb * 16 + 4 * (lane >> 4) + r;
+      const float xf = (float)xs[t][r];
+      const float gg = (xf * cf[320 + c] + cf[384 + c] > 0.f) ? (float)da[t][r] : 0.f;
+      const float xh = (xf - cf[192 + c]) * cf[256 + c];
+      float o = cf[c] * gg - cf[64 + c] - cf[128 + c] * xh;
+      if (ADD) o += (float)add[t][r];
+      out[t][r] = (bf16)o;
+    }
+  }
+}
+
+__device__ __forceinline__ void bwd_combine(BwdCtx& x, int bi, int C, float M) {
+  const PrnArgs& a = *x.a;
+  combine_slots(a.bslot + (long)bi * a.N * PRN_SLOT, a.N, x.m.dred, x.m.dsum);
+  bn_bwd_table(a.bns[bi], x.m.dsum, C, M, x.img == 0, x.m.tbl2);
+}
+
+// One block's backward: dout (stage S) in, dx (input stage) out (in `dout`).  On entry
+// W1 holds conv2's dgrad weights; on exit the previous block's (`next_w2`).
+template <int S, int STR, bool PROJ>
+__device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WLoad& next_w2,
+                                          const PrnBlock& B) {
+  constexpr int SI = STR == 2 ? S - 1 : S;
+  using GI = Stg<SI>;
+  using G = Stg<S>;
+  const PrnArgs& a = *x.a;
+  const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
+  const long img_o = (long)x.img * G::R * G::R * G::C;
+  const long img_i = (long)x.img * GI::R * GI::R * GI::C;
+  bf16x4 hs[8], xs[8];
+  load_regs<S>(hs, B.h1 + img_o, wave, lane);     // BN2 input (saved by the forward)
+  load_regs<SI>(xs, B.x + img_i, wave, lane);     // BN1 input
+  bn_load_table(a.bns[B.bn2], G::C, x.m.tbl);
+  // publish dout (conv2 / projection weight gradients), stage it for conv2's dgrad
+  store_regs<S>(dout, B.dout + img_o, wave, lane, true);
+  to_halo<S, false>(x.m.hb, dout, nullptr, nullptr, wave, lane);
+  __syncthreads();
+  f32x4 acc[8];
+  zero_acc<S>(acc);
+  conv_acc<S, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, wave, lane);
+  bf16x4 da[8];
+  round_acc<S, false>(da, acc, da);
+  bwd_sums<S>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
+  bwd_arrive(x);
+  {
+    const WLoad L1 = wl_dgrad(B.w1b, G::C, GI::C, 3);
+    WLoad LP{};
+    if (PROJ) LP = wl_dgrad(B.wpb, G::C, GI::C, 1);
+    bf16x8 w1r[nreg(conv_units(G::C, GI::C, 3))], wpr[1];
+    w_prefetch(L1, w1r);
+    w_prefetch(LP, wpr);
+    if (!bwd_wait(x)) return false;
+    bwd_combine(x, B.bn2, G::C, (float)a.N * G::R * G::R);
+    bf16x4 dh[8];
+    bwd_apply<S, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
+    store_regs<S>(dh, B.dh1 + img_o, wave, lane, true);
+    to_halo<S, false>(x.m.ha, dh, nullptr, nullptr, wave, lane);
+    bn_load_table(a.bns[B.bn1], GI::C, x.m.tbl);
+    w_store(L1, w1r, x.m.w1);
+    w_store(LP, wpr, x.m.w2);
+  }
+  __syncthreads();
+  zero_acc<SI>(acc);
+  if constexpr (STR == 2) {
+    dgrad_s2_acc<SI, G::C, false>(acc, x.m.ha, x.m.w1, wave, lane);
+    dgrad_s2_acc<SI, G::C, true>(acc, x.m.hb, x.m.w2, wave, lane);
+  } else {
+    conv_acc<S, G::C, 3, 1, true>(acc, x.m.ha, x.m.w1, wave, lane);
+    if constexpr (PROJ) conv_acc<S, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, wave, lane);
+  }
+  round_acc<SI, false>(da, acc, da);
+  bwd_sums<SI>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
+  bwd_arrive(x);
+  bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
+  w_prefetch(next_w2, w2r);
+  if (!bwd_wait(x)) return false;
+  bwd_combine(x, B.bn1, GI::C, (float)a.N * GI::R * GI::R);
+  if constexpr (PROJ) bwd_apply<SI, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  else bwd_apply<SI, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  w_store(next_w2, w2r, x.m.w1);   // visible after the next block's first __syncthreads
+  return true;
+}
+
+// ---- weight-gradient items ---------------------------------------------------------------
+// dW[co][tap][ci] = sum_{images, p} dy[p][co] * A[p @ tap][ci], A = relu(bn(x)) (or x):
+// per image, dy [Ro^2][CO] and the A halo [(Ri+2)^2][CI] go to LDS pixel-major; MFMA
+// fragments by the transposed read ds_read_b64_tr_b16 (conv_wgrad_direct.hip's scheme);
+// waves = WT tile groups x (8 / WT) pixel slices, summed in LDS in a fixed order.
+template <int CO, int CI, int KSZ, int STR, int RO, int WT>
+__device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wave, int lane) {
+  constexpr int RI = RO * STR, W2 = RI + 2, OFF = KSZ == 1 ? 1 : 0;
+  constexpr int KN = KSZ * KSZ * CI, NB = (KN + 15) / 16, MB = CO / 16;
+  constexpr int TILES = MB * NB, TPW = TILES / WT, WKS = NW / WT;
+  constexpr int KSI = RO * RO / 32, KPW = KSI / WKS;   // k-steps per image / per wave
+  static_assert(TILES % WT == 0 && KSI % WKS == 0 && TPW <= 36, "wgrad tiles");
+  static_assert(NB % TPW == 0, "a wave's tiles share one output-channel block");
+  bf16* dys = reinterpret_cast<bf16*>(smem);                    // [RO*RO][CO]
+  bf16* hal = dys + RO * RO * CO;                               // [W2*W2][CI]
+  float* tb = reinterpret_cast<float*>(hal + W2 * W2 * CI);     // [2][64]
+  const int tid = threadIdx.x;
+  wave = opaque_s(wave);
+  lane = opaque_v(lane);
+  const int tg = wave % WT, kq = wave / WT;
+  const int gq = lane >> 4, li = lane & 15, qr = li >> 2, pc = li & 3;
+  if (it.scale != nullptr && tid < CI) {
+    tb[tid] = it.scale[tid];
+    tb[64 + tid] = it.shift[tid];
+  }
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int n = it.img0; n < it.img0 + it.nimg; ++n) {
+    __syncthreads();   // the previous image's operands are dead; tb written
+    constexpr int DU = RO * RO * CO / 8;
+    for (int q = tid; q < DU; q += PT)
+      *reinterpret_cast<bf16x8*>(dys + q * 8) = ld_sc1_b128(it.dy, (long)n * RO * RO * CO + q * 8);
+    constexpr int CU = CI / 8;
+    for (int q = tid; q < W2 * W2 * CU; q += PT) {
+      const int pix = q / CU, u = q - pix * CU;
+      const int hr = pix / W2, hc = pix - hr * W2;
+      bf16x8 v = {};
+      if (hr >= 1 && hr <= RI && hc >= 1 && hc <= RI) {
+        v = *reinterpret_cast<const bf16x8*>(it.x + (((long)n * RI + hr - 1) * RI + hc - 1) * CI + u * 8);
+        if (it.scale != nullptr) v = affine_relu8(v, tb + u * 8, tb + 64 + u * 8);
+      }
+      *reinterpret_cast<bf16x8*>(hal + pix * CI + u * 8) = v;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int ks = kq * KPW + kk;
+      const int r1 = ks * 32 + 4 * gq + qr, r2 = r1 + 16;     // output pixels of this lane
+      int hp[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = e ? r2 : r1, oh = p / RO, ow = p - oh * RO;
+        hp[e] = (oh * STR + OFF) * W2 + ow * STR + OFF;
+      }
+      const int mbw = (tg * TPW) / NB;                            // this wave's channel block
+      bf16x8 af;
+      {
+        const s16x4 lo = lds_read_tr16(dys + r1 * CO + mbw * 16 + 4 * pc);
+        const s16x4 hi = lds_read_tr16(dys + r2 * CO + mbw * 16 + 4 * pc);
+        af = __builtin_bit_cast(bf16x8, (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int nb = (tg * TPW + t) % NB;
+        const int col = nb * 16 + 4 * pc;                         // (tap, ci) of this lane's address
+        int tap = col / CI;
+        const int ci = col - tap * CI;
+        tap = tap < KSZ * KSZ ? tap : KSZ * KSZ - 1;
+        const int toff = (tap / KSZ) * W2 + tap % KSZ;
+        const s16x4 lo = lds_read_tr16(hal + (hp[0] + toff) * CI + ci);
+        const s16x4 hi = lds_read_tr16(hal + (hp[1] + toff) * CI + ci);
+        const bf16x8 bfr =
+            __builtin_bit_cast(bf16x8, (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        acc[t] = mfma16(af, bfr, acc[t]);
+      }
+    }
+  }
+  // fixed-order sum of the WKS pixel slices (slice 0 accumulates), then the slab
+  float* red = reinterpret_cast<float*>(smem);
+  for (int s = 1; s < WKS; ++s) {
+    __syncthreads();
+    if (kq == s)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+        *reinterpret_cast<f32x4*>(red + ((tg * TPW + t) * 64 + lane) * 4) = acc[t];
+    __syncthreads();
+    if (kq == 0)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+        acc[t] += *reinterpret_cast<const f32x4*>(red + ((tg * TPW + t) * 64 + lane) * 4);
+  }
+  if (kq == 0) {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tile = tg * TPW + t, mb = tile / NB, nb = tile - mb * NB;
+      const int n = nb * 16 + li;
+      if (n < KN)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) it.part[(long)(mb * 16 + 4 * gq + i) * KN + n] = acc[t][i];
+    }
+  }
+  __syncthreads();
+}
+
+constexpr int PRN_KINDS = 9;
+// LDS of the weight-gradient role per kind: dy + halo + table
+__host__ __device__ constexpr int wg_lds(int co, int ci, int str, int ro) {
+  return ro * ro * co * 2 + (ro * str + 2) * (ro * str + 2) * ci * 2 + 512;
+}
+
+__device__ __forceinline__ void run_item(const PrnItem& it, char* smem, int wave, int lane) {
+  switch (it.kind) {
+    case 0: wgrad_item<16, 16, 3, 1, 32, 1>(it, smem, wave, lane); break;   // stage-0 3x3
+    case 1: wgrad_item<32, 32, 3, 1, 16, 2>(it, smem, wave, lane); break;   // stage-1 3x3
+    case 2: wgrad_item<64, 64, 3, 1, 8, 8>(it, smem, wave, lane); break;    // stage-2 3x3
+    case 3: wgrad_item<32, 16, 3, 2, 16, 2>(it, smem, wave, lane); break;   // 3x3/2 16->32
+    case 4: wgrad_item<64, 32, 3, 2, 8, 8>(it, smem, wave, lane); break;    // 3x3/2 32->64
+    case 5: wgrad_item<16, 16, 1, 1, 32, 1>(it, smem, wave, lane); break;   // 1x1 16->16
+    case 6: wgrad_item<32, 16, 1, 2, 16, 2>(it, smem, wave, lane); break;   // 1x1/2 16->32
+    case 7: wgrad_item<64, 32, 1, 2, 8, 8>(it, smem, wave, lane); break;    // 1x1/2 32->64
+    case 8: wgrad_item<16, 8, 3, 1, 32, 1>(it, smem, wave, lane); break;    // stem 8->16
+    default: break;
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if ((int)blockIdx.x >= a.N) {
+    // ---- weight-gradient role: items w, w + W, ... in readiness order ----
+    const int w = blockIdx.x - a.N, W = gridDim.x - a.N;
+    int* flag = reinterpret_cast<int*>(smem + OFF_MISC);
+    for (int i = w; i < a.nitems; i += W) {
+      const PrnItem& it = a.items[i];
+      if (!grid_wait(a.bar + 1, (unsigned)it.ready * (unsigned)a.N, a.err, flag)) return;
+      run_item(it, smem, wave, lane);
+    }
+    return;
+  }
+  BwdCtx x;
+  x.a = &a;
+  x.m = carve(smem);
+  x.img = blockIdx.x;
+  x.wave = wave;
+  x.lane = lane;
+  x.nbar = 0;
+  const int nb = a.nblocks;
+  const PrnBlock& BL = a.blocks[nb - 1];
+  {   // the last block's conv2 dgrad weights (stage 2: 64 x 576)
+    const WLoad L = wl_dgrad(BL.w2b, 64, 64, 3);
+    bf16x8 r[nreg(conv_units(64, 64, 3))];
+    w_prefetch(L, r);
+    w_store(L, r, x.m.w1);
+  }
+  // ---- final BN backward: dXL = a g - b - c xhat, g = dpool * relu'(bn(XL)) ----
+  using G2 = Stg<2>;
+  bf16x4 dout[8];
+  {
+    const int fb = 2 * nb;
+    bf16x4 xs[8];
+    load_regs<2>(xs, BL.out + (long)x.img * 64 * 64, wave, lane);
+    bf16x4 dp[8];
+    float* dps = x.m.tbl;   // dpool row
+    if (tid < 64) dps[tid] = a.dpool[(long)x.img * 64 + tid];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < G2::TPW; ++t) {
+      int pb, cb;
+      tile_of<2>(wave, t, pb, cb);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dp[t][r] = (bf16)dps[cb * 16 + 4 * (lane >> 4) + r];
+    }
+    bwd_combine(x, fb, 64, (float)a.N * 64);
+    bwd_apply<2, false>(dout, dp, xs, dout, x.m.tbl2, wave, lane);
+  }
+  // ---- blocks, last to first (straight-line stages, as in the forward) ----
+  const int nps = nb / 3;
+  auto run = [&](auto tag, int bi) -> bool {
+    constexpr int S = decltype(tag)::S, STR = decltype(tag)::STR;
+    constexpr bool PROJ = decltype(tag)::PROJ;
+    WLoad n2{};
+    if (bi > 0) {
+      const PrnBlock& Bp = a.blocks[bi - 1];
+      n2 = wl_dgrad(Bp.w2b, 16 << Bp.stage, 16 << Bp.stage, 3);
+    }
+    return block_bwd<S, STR, PROJ>(x, dout, n2, a.blocks[bi]);
+  };
+  for (int bi = nb - 1; bi > 2 * nps; --bi)
+    if (!run(BlkTag<2, 1, false>{}, bi)) return;
+  if (!run(BlkTag<2, 2, true>{}, 2 * nps)) return;
+  for (int bi = 2 * nps - 1; bi > nps; --bi)
+    if (!run(BlkTag<1, 1, false>{}, bi)) return;
+  if (!run(BlkTag<1, 2, true>{}, nps)) return;
+  for (int bi = nps - 1; bi > 0; --bi)
+    if (!run(BlkTag<0, 1, false>{}, bi)) return;
+  if (!run(BlkTag<0, 1, true>{}, 0)) return;
+  // ---- the stem output's gradient: published for the stem's weight gradient ----
+  store_regs<0>(dout, a.dx0 + (long)x.img * 1024 * 16, wave, lane, true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(a.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- host ------------------------------------------------------------------------------
+size_t prn_lds_bytes() { return LDS_TOTAL; }
+
+bool prn_supported(int N, int nblocks, int classes, int kpad) {
+  return N >= 1 && N <= 128 && nblocks >= 3 && nblocks % 3 == 0 && classes >= 1 &&
+         classes <= kpad && kpad <= 64 && kpad % 16 == 0;
+}
+
+int prn_item_kind(int cin, int cout, int ksize, int stride) {
+  if (cin == 8 && cout == 16 && ksize == 3 && stride == 1) return 8;
+  if (ksize == 3 && stride == 1 && cin == cout) return cin == 16 ? 0 : cin == 32 ? 1 : cin == 64 ? 2 : -1;
+  if (ksize == 3 && stride == 2) return cin == 16 && cout == 32 ? 3 : cin == 32 && cout == 64 ? 4 : -1;
+  if (ksize == 1 && stride == 1 && cin == 16 && cout == 16) return 5;
+  if (ksize == 1 && stride == 2) return cin == 16 && cout == 32 ? 6 : cin == 32 && cout == 64 ? 7 : -1;
+  return -1;
+}
+
+static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS_TOTAL &&
+                  wg_lds(16, 8, 1, 32) <= LDS_TOTAL,
+              "weight-gradient LDS");
+
+void prn_forward(const PrnArgs& a, hipStream_t s) {
+  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad) || a.N > cu_count())
+    throw std::invalid_argument("prn_forward: unsupported shape (N <= CUs, 3n blocks, <= 64 classes)");
+  hipLaunchKernelGGL(prn_fwd_kernel, dim3(a.N), dim3(PT), LDS_TOTAL, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
+  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad))
+    throw std::invalid_argument("prn_backward: unsupported shape");
+  const int grid = a.N + std::max(1, wgrad_wgs);
+  if (grid > cu_count())
+    throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
+  hipLaunchKernelGGL(prn_bwd_kernel, dim3(grid), dim3(PT), LDS_TOTAL, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+}  // namespace dtr

@@ -199,23 +199,84 @@ void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s)
 bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 
-// Persistent multi-layer prototype (persist.hip): L chained 3x3 64 -> 64 convs on 8x8
-// maps (CIFAR stage 3) in one launch, grid barriers between layers.
-struct PersistArgs {
-  const bf16* x0;            // [N,8,8,64] stage input (pre-activation)
-  const float* bn0_scale;    // BN+ReLU of the first conv's input
-  const float* bn0_shift;
-  const bf16* w;             // [L][64 co][3][3][64 ci]
-  const float* gamma;        // [L][64]: BN of each conv's output (the next conv's input)
+// ---- Persistent small-batch CIFAR step (cifar_persist.hip) ----
+// The whole CIFAR ResNet v2 (6n+2, building blocks, 16/32/64 channels on 32/16/8 maps;
+// resnet_model_official.py:217-278) forward in ONE launch and its backward in ONE
+// launch: one 512-thread workgroup per image keeps the image's activations on-chip
+// (registers + LDS halos) across layers; grid barriers only where BatchNorm batch
+// statistics need the whole batch.  In the backward launch the remaining CUs compute
+// the weight gradients (per image group, fp32 slabs for the grouped reduce) as soon
+// as the image workgroups have published each layer's output gradient.
+struct PrnBn {               // one BatchNorm (all device pointers)
+  const float* gamma;
   const float* beta;
-  bf16* y;                   // [L][N,8,8,64] conv outputs (odd layers: + block input)
-  float* stats;              // [L][2][64] batch sum / sum of squares, zeroed by the caller
-  unsigned* bar;             // grid-barrier counter, zeroed by the caller
-  int* err;                  // set on a timed-out barrier
-  int N, L;
-  float eps;
+  float* mmean;              // moving statistics (updated by image 0)
+  float* mvar;
+  float* mean;               // batch statistics (written by image 0)
+  float* rstd;
+  float* scale;
+  float* shift;
+  float* dgamma;             // gradients in the flat fp32 gradient buffer (image 0)
+  float* dbeta;
 };
-void persist_stage_fwd(const PersistArgs& a, hipStream_t s);
+struct PrnBlock {            // one building block (resnet_model_official.py:94-130)
+  bf16* x;                   // block input [N][R_in][R_in][C_in], NHWC (saved)
+  bf16* h1;                  // conv1 output [N][R][R][C] (saved)
+  bf16* out;                 // block output (the next block's x)
+  const bf16* w1f;           // forward weights, OHWI [co][kh][kw][ci]
+  const bf16* w2f;
+  const bf16* wpf;           // projection shortcut (nullptr: identity)
+  const bf16* w1b;           // dgrad weights, HWIO [kh][kw][ci][co]
+  const bf16* w2b;
+  const bf16* wpb;
+  bf16* dout;                // backward: gradient of `out` (published for the weight gradients)
+  bf16* dh1;                 // backward: gradient of h1 (after BN2's backward)
+  int stage;                 // output stage 0..2 (32x32x16, 16x16x32, 8x8x64)
+  int stride;                // 1 or 2 (the first block of stages 1 and 2)
+  int bn1, bn2;              // PrnBn indices of the block's two BatchNorms
+};
+struct PrnItem {             // backward weight-gradient work item: one conv x one image group
+  const bf16* dy;            // [N][Ro][Ro][CO] output gradient (published by the image workgroups)
+  const bf16* x;             // [N][Ri][Ri][CI] conv input before its BatchNorm (stem: the image)
+  const float* scale;        // BN+ReLU of x (nullptr: none -- the stem)
+  const float* shift;
+  float* part;               // [CO][taps*CI] fp32 slab of this image group
+  int kind;                  // conv shape class (prn_item_kind)
+  int img0, nimg;
+  int ready;                 // backward barrier arrivals (x images) after which dy is complete
+};
+struct PrnArgs {
+  const PrnBlock* blocks;
+  int nblocks;
+  const PrnBn* bns;          // [2 * nblocks + 1]: block i's BNs at 2i, 2i+1; the final BN last
+  const bf16* x_in;          // [N][32][32][8] input images (channels 3..7 zero)
+  const bf16* stem_w;        // OHWI [16][3][3][8]
+  float* fslot;              // [2 * nblocks + 1][N][128] forward BN partial sums (sum, sum sq)
+  float* bslot;              // [2 * nblocks + 1][N][128] backward BN partial sums (sum g, sum g xhat)
+  unsigned* bar;             // [2] barrier counters (forward, backward), zeroed every step
+  int* err;                  // set when a barrier wait times out
+  const bf16* dense_w;       // [64][kpad] bf16 HWIO
+  const float* dense_b;
+  const int* labels;
+  bf16* pooled;              // [N][64]
+  bf16* dlogits;             // [N][kpad]
+  float* ws;                 // softmax_xent workspace: [N][kpad] gradient rows, then [N][2]
+  float* dpool;              // [N][64] fp32: average-pool gradient per channel (dact)
+  bf16* dx0;                 // backward: gradient of the stem output [N][32][32][16]
+  const PrnItem* items;      // backward weight-gradient items, in readiness order
+  int nitems;
+  int N, classes, kpad;
+  float grad_scale;          // 1 / global batch
+  float momentum, eps;
+  int update_moving;
+};
+enum { PRN_THREADS = 512, PRN_SLOT = 128 };
+bool prn_supported(int N, int nblocks, int classes, int kpad);
+size_t prn_lds_bytes();
+void prn_forward(const PrnArgs& a, hipStream_t s);
+void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);
+// item kind of a conv (stage of its output, kernel size, stride; stem = 8 input channels)
+int prn_item_kind(int cin, int cout, int ksize, int stride);
 
 struct WgradArgs {
   const bf16* dy;           // [N,Ho,Wo,K]

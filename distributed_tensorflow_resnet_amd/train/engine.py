@@ -250,6 +250,14 @@ class Engine:
                           else None)
         self._build_weight_layout()
         self._alloc_activations()
+        # Persistent small-batch CIFAR step (train/persist.py, csrc/cifar_persist.hip): the
+        # forward and the backward each as ONE launch (tune persist: -1 auto = per-rank
+        # batch <= 32 on a supported CIFAR network, 0 off, 1 whenever supported)
+        from . import persist as _persist
+        pm = tune.get("persist")
+        ok = pm != 0 and _persist.supported(self)
+        self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
+        self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
@@ -466,7 +474,10 @@ class Engine:
         self.bn_acc_on = self.bn_bacc_on = bool(tune.get("bn_acc"))
         rep = self.nat.bn_acc_rep()
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
-        self.bn_acc = torch.zeros(max(_ceil(tot, 2) * 2, 2), dtype=torch.float64, device=dev)
+        # (+ 2 doubles: the persistent step's two barrier counters, zeroed with the
+        # accumulators at the start of every step -- train/persist.py)
+        self.bn_acc = torch.zeros(max(_ceil(tot, 2) * 2, 2) + 2, dtype=torch.float64, device=dev)
+        self.prn_bar = self.bn_acc.data_ptr() + 8 * (self.bn_acc.numel() - 2)
         off = 0
         for b in self.bns.values():
             n = 2 * rep * b.spec.channels
@@ -993,6 +1004,8 @@ class Engine:
 
     # ------------------------------------------------------------------ plan
     def _build_train_plan(self):
+        if self.persist:
+            return self._build_persist_plan()
         plan, spec, N = self.plan, self.spec, self.N
         self.seg = {}
         for e in self.bns.values():
@@ -1225,7 +1238,13 @@ class Engine:
         self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
 
-        # ---- optimizer
+        self._emit_optimizer(plan)
+
+    def _emit_optimizer(self, plan):
+        """Optimizer segment (fused SGD-momentum + wd + bf16 re-pack, global_step += 1)
+        and the `cost` segment (1/2 sum v^2 of the weights)."""
+        spec = self.spec
+        sp = self.scalars.data_ptr()
         b2 = plan.size()
         s = self.sched
         plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
@@ -1252,6 +1271,84 @@ class Engine:
         self.seg["cost"] = (b3, plan.size())
         missing = [s.name for s in self.params.train_slots if s.name not in self.ready_index]
         assert not missing, f"gradients never produced: {missing[:4]}"
+
+    def _build_persist_plan(self):
+        """The persistent small-batch step (train/persist.py): input, ONE forward launch;
+        the head's batch folds and the dense weight gradient on the side stream; ONE
+        backward launch (dgrad chain + BN backward on one workgroup per image, weight
+        gradients on the remaining CUs); the grouped slab reduces and bucket all-reduces;
+        the optimizer."""
+        plan, spec, N = self.plan, self.spec, self.N
+        self.seg = {}
+        for e in self.bns.values():
+            e.pending = None
+        self._n_allreduce, self._allreduce_bytes = 0, 0
+        self._head_fused = False
+        b0 = plan.size()
+        self._t_fwd0 = plan.timing_point("fwd_begin")
+        # BN accumulators + the two barrier counters start every step at zero
+        zero = (self.bn_acc.data_ptr(), self.bn_acc.numel() * 8)
+        if self.input_mode == "cifar_u8":
+            plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
+                               spec.image_w, self.cpad_in, 4, self.data_seed,
+                               self.gstep.data_ptr(), 1, 0, *zero)
+        else:
+            plan.memset(*zero)
+        ptrs, ints, floats = self.prn.args(self.prn_bar, BN_DECAY, BN_EPS)
+        plan.prn(0, ptrs, ints, floats)
+        self.seg["fwd"] = (b0, plan.size())
+
+        b1 = plan.size()
+        self._t_bwd0 = plan.timing_point("bwd_begin")
+        self._pending = dict(self.prn.pending())
+        self._produced = set(self._pending) | {"dense/bias"}
+        self._flushed, self._reduced = set(), set()
+        self._side_q, self._side_blocks = [], 0
+        self._main_wgrad = False
+        self._reduce_main = True   # the slab reduces run on the main stream
+        sp = self.scalars.data_ptr()
+        F = spec.dense_in
+        off, spl, pps = self.wg_off["dense"]
+        dpart = self.wg_part.data_ptr() + 4 * off
+        self._pending[self.dense_name] = (dpart, self.dense_grad, spl, self.kpad,
+                                          spec.num_classes, 1, F, F)
+        self._produced.add(self.dense_name)
+        side = self.fork_wgrad
+        if side:   # the head's batch folds + the dense wgrad overlap the backward launch
+            ev = plan.new_event()
+            plan.record(ev)
+            plan.use_stream(1)
+            plan.wait(ev)
+        plan.softmax_xent_reduce(self.xent_ws.data_ptr(), self.kpad, N, spec.num_classes, sp,
+                                 sp + 4, self.dense_bias_grad)
+        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0, dpart,
+                        self._dense_geom(N), spl, pps)
+        if side:
+            plan.use_stream(0)
+        plan.prn(1, ptrs, ints, floats)
+        if side:
+            ev = plan.new_event()
+            plan.use_stream(1)
+            plan.record(ev)
+            plan.use_stream(0)
+            plan.wait(ev)
+        # per bucket: its slab reduces, then (world > 1) its all-reduce on the comm stream
+        for bi, (lo, hi, names) in enumerate(self.buckets):
+            for gnames in self.reduce_groups[bi]:
+                self._emit_reduce(plan, gnames)
+            self._mark(plan, *names)
+            self._flushed.add(bi)
+            if self.comm is not None:
+                self._emit_allreduce(plan, lo, hi, side_dep=False)
+        self._t_bwd_done = plan.timing_point("bwd_compute_done")
+        self._join_comm(plan)
+        self._t_joined = plan.timing_point("allreduce_joined")
+        self.seg["bwd"] = (b1, plan.size())
+        self._emit_optimizer(plan)
+
+    def persist_error(self) -> bool:
+        """Whether a persistent launch's barrier wait ever timed out (diagnostics)."""
+        return self.prn is not None and bool(self.prn.err.item())
 
     # ------------------------------------------------------------------ running
     def repack(self):

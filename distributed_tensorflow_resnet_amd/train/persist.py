@@ -1,0 +1,186 @@
+"""Persistent small-batch CIFAR step: descriptor tables + plan ops (csrc/cifar_persist.hip).
+
+At the per-rank batches of the strong-scaling headline config (global batch 128 over
+4-8 GPUs = 16-32 images per rank; reference README.md:16-22, resnet_cifar_main.py:326-340)
+the launch-per-layer step is a chain of ~110 dependent kernel boundaries.  This path
+runs the CIFAR ResNet v2 (resnet_model_official.py:217-278) forward as ONE launch and
+its backward as ONE launch: one 512-thread workgroup per image keeps the image's
+activations on-chip across layers, grid barriers only where BatchNorm needs batch
+statistics, and the CUs beyond the images compute the weight gradients (fp32 slabs per
+image group) while the backward's dgrad chain continues.  The step is then:
+
+    [augment] -> prn forward -> (side: softmax-xent batch folds, dense wgrad)
+              -> prn backward -> grouped slab reduces (+ bucket all-reduces) -> optimizer
+
+Selected by the engine (tune ``persist``: -1 auto = per-rank batch <= 32 on a supported
+CIFAR spec, 0 off, 1 on when supported).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+PRN_BN = np.dtype([(k, "<u8") for k in ("gamma", "beta", "mmean", "mvar", "mean", "rstd",
+                                        "scale", "shift", "dgamma", "dbeta")])
+PRN_BLOCK = np.dtype([(k, "<u8") for k in ("x", "h1", "out", "w1f", "w2f", "wpf", "w1b", "w2b",
+                                           "wpb", "dout", "dh1")] +
+                     [(k, "<i4") for k in ("stage", "stride", "bn1", "bn2")])
+PRN_ITEM = np.dtype([(k, "<u8") for k in ("dy", "x", "scale", "shift", "part")] +
+                    [(k, "<i4") for k in ("kind", "img0", "nimg", "ready")])
+SLOT = 128          # floats per (BatchNorm, image) partial-sum slot
+AUTO_MAX_BATCH = 32
+
+
+def supported(eng) -> bool:
+    """Whether the persistent kernels cover this engine's network and batch."""
+    spec, nat = eng.spec, eng.nat
+    if not spec.dataset.startswith("cifar") or spec.maxpool or eng.stem_s2d:
+        return False
+    if spec.image_h != 32 or spec.image_w != 32 or spec.dense_in != 64:
+        return False
+    st = spec.stem
+    if (st.kh, st.kw, st.stride, st.cout) != (3, 3, 1, 16) or st.cin > 8:
+        return False
+    nb = len(spec.blocks)
+    if nb % 3 or any(b.kind != "building" for b in spec.blocks):
+        return False
+    n = nb // 3
+    for i, b in enumerate(spec.blocks):
+        stage = i // n
+        if b.cout != 16 << stage or b.ho != 32 >> stage:
+            return False
+        first = i % n == 0
+        if (b.proj is not None) != first or b.stride != (2 if first and stage else 1):
+            return False
+    cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
+    return eng.N < cus and bool(nat.prn_supported(eng.N, nb, spec.num_classes, eng.kpad))
+
+
+def _stage(b) -> int:
+    return int(math.log2(b.cout // 16))
+
+
+class PersistStep:
+    """Device tables and buffers of the persistent step for one Engine."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        nat, spec, N, dev = eng.nat, eng.spec, eng.N, eng.device
+        sizes = nat.prn_struct_bytes()
+        assert sizes == [PRN_BN.itemsize, PRN_BLOCK.itemsize, PRN_ITEM.itemsize], sizes
+        blocks = spec.blocks
+        nb = len(blocks)
+        self.nblocks = nb
+        # BatchNorm table: block i's two BNs at 2i, 2i + 1, the final BN last
+        order = [bn for b in blocks for bn in b.bns] + [spec.final_bn]
+        bn_rows = np.zeros(len(order), dtype=PRN_BN)
+        for r, bs in zip(bn_rows, order):
+            e = eng.bns[bs.name]
+            r["gamma"], r["beta"], r["mmean"], r["mvar"] = e.gamma, e.beta, e.mmean, e.mvar
+            r["mean"], r["rstd"] = e.mean.data_ptr(), e.rstd.data_ptr()
+            r["scale"], r["shift"] = e.scale.data_ptr(), e.shift.data_ptr()
+            r["dgamma"], r["dbeta"] = e.dgamma, e.dbeta
+        self.bn_dev = self._dev(bn_rows)
+        nbn = len(order)
+        self.fslot = torch.zeros(nbn * N * SLOT, device=dev)
+        self.bslot = torch.zeros(nbn * N * SLOT, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.dpool = torch.zeros((N, 64), device=dev)
+        self.dx0 = torch.empty_like(eng.X[0])
+        # per-block backward gradients published to the weight-gradient workgroups
+        self.dout = [torch.empty_like(eng.X[i + 1]) for i in range(nb)]
+        self.dh1 = [torch.empty_like(eng.H1[i]) for i in range(nb)]
+        rows = np.zeros(nb, dtype=PRN_BLOCK)
+        for i, (r, b) in enumerate(zip(rows, blocks)):
+            c1, c2 = eng.convs[b.convs[0].name], eng.convs[b.convs[1].name]
+            r["x"], r["h1"], r["out"] = (eng.X[i].data_ptr(), eng.H1[i].data_ptr(),
+                                         eng.X[i + 1].data_ptr())
+            r["w1f"], r["w2f"], r["w1b"], r["w2b"] = c1.ohwi, c2.ohwi, c1.hwio, c2.hwio
+            if b.proj is not None:
+                cp = eng.convs[b.proj.name]
+                r["wpf"], r["wpb"] = cp.ohwi, cp.hwio
+            r["dout"], r["dh1"] = self.dout[i].data_ptr(), self.dh1[i].data_ptr()
+            r["stage"], r["stride"] = _stage(b), b.stride
+            r["bn1"], r["bn2"] = 2 * i, 2 * i + 1
+        self.block_dev = self._dev(rows)
+        self._build_items()
+
+    def _dev(self, arr):
+        return torch.from_numpy(arr.view(np.uint8).copy()).to(self.eng.device)
+
+    def _build_items(self):
+        """Weight-gradient work items in the order the backward publishes their dy:
+        per block (last first) conv2 and the projection after the block's first
+        backward barrier, conv1 after its second; the stem after the final arrive.
+        Images are grouped (<= 16 groups: the grouped reduce reads one slab per group)."""
+        eng, spec, N = self.eng, self.eng.spec, self.eng.N
+        nat = eng.nat
+        blocks = spec.blocks
+        nb = len(blocks)
+        self.group = max(1, math.ceil(N / 16))
+        groups = [(g0, min(self.group, N - g0)) for g0 in range(0, N, self.group)]
+        self.splits = len(groups)
+        convs = []   # (name, dy, x, bn scale, bn shift, ready)
+        for j, i in enumerate(range(nb - 1, -1, -1)):
+            b = blocks[i]
+            bn1, bn2 = eng.bns[b.bns[0].name], eng.bns[b.bns[1].name]
+            d_out, d_h1 = self.dout[i].data_ptr(), self.dh1[i].data_ptr()
+            convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 1))
+            if b.proj is not None:
+                convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 1))
+            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 2))
+        convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 1))
+        tot = 0
+        self.part_off = {}
+        for name, *_ in convs:
+            c = eng.convs[name]
+            s = c.spec
+            self.part_off[name] = tot
+            tot += self.splits * s.cout * s.kh * s.kw * c.cin
+        self.part = torch.empty(max(tot, 1), device=eng.device)
+        items = []
+        for name, dy, x, bn, ready in convs:
+            c = eng.convs[name]
+            s = c.spec
+            kind = nat.prn_item_kind(c.cin, s.cout, s.kh, s.stride)
+            assert kind >= 0, (name, c.cin, s.cout, s.kh, s.stride)
+            slab = s.cout * s.kh * s.kw * c.cin
+            for gi, (g0, gn) in enumerate(groups):
+                r = np.zeros(1, dtype=PRN_ITEM)[0]
+                r["dy"], r["x"] = dy, x
+                if bn is not None:
+                    r["scale"], r["shift"] = bn.scale.data_ptr(), bn.shift.data_ptr()
+                r["part"] = self.part.data_ptr() + 4 * (self.part_off[name] + gi * slab)
+                r["kind"], r["img0"], r["nimg"], r["ready"] = kind, g0, gn, ready
+                items.append(r)
+        self.items = np.array(items, dtype=PRN_ITEM)
+        self.item_dev = self._dev(self.items)
+        cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
+        self.wgrad_wgs = max(1, min(cus - N, len(items)))
+        self.convs = [c[0] for c in convs]
+
+    def pending(self):
+        """_pending entries (grouped-reduce descriptors) of every conv's slabs."""
+        eng = self.eng
+        out = {}
+        for name in self.convs:
+            c = eng.convs[name]
+            s = c.spec
+            out[c.name] = (self.part.data_ptr() + 4 * self.part_off[name], c.grad, self.splits,
+                           s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
+        return out
+
+    def args(self, bar_ptr: int, bn_decay: float, bn_eps: float):
+        eng, spec = self.eng, self.eng.spec
+        ptrs = [self.block_dev.data_ptr(), self.bn_dev.data_ptr(), eng.x_in.data_ptr(),
+                eng.convs[spec.stem.name].ohwi, self.fslot.data_ptr(), self.bslot.data_ptr(),
+                bar_ptr, self.err.data_ptr(), eng.dense_hwio, eng.dense_bias,
+                eng.labels.data_ptr(), eng.pooled.data_ptr(), eng.dlogits.data_ptr(),
+                eng.xent_ws.data_ptr(), self.dpool.data_ptr(), self.dx0.data_ptr(),
+                self.item_dev.data_ptr()]
+        ints = [self.nblocks, len(self.items), eng.N, spec.num_classes, eng.kpad, 1,
+                self.wgrad_wgs]
+        floats = [1.0 / eng.global_batch, bn_decay, bn_eps]
+        return ptrs, ints, floats

@@ -50,6 +50,9 @@ ENGINE = {
     "dgrad1x1_stream": (1, "1x1 stride-1 dgrads carrying BN-backward sums whose weights fit "
                            "in VGPRs (the expanding conv at stages 1-2, the first conv at "
                            "stage 3) on the streaming kernel bn_dgrad1x1 (store + sums)"),
+    "persist": (-1, "persistent small-batch CIFAR step (forward and backward each ONE launch, "
+                    "one workgroup per image; train/persist.py): -1 auto = per-rank batch <= 32, "
+                    "0 off, 1 whenever the network is supported"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 

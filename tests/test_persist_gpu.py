@@ -1,30 +1,173 @@
-"""Persistent multi-layer prototype (csrc/persist.hip): L chained CIFAR stage-3 convs in
-one launch with grid barriers == the PyTorch fp32 reference of the same chain
-(batch-statistics BN between layers, residual on every second conv, bf16 rounding where
-the kernel rounds); repeated launches reuse nothing but the weights."""
-import os
-import sys
-
+"""Persistent small-batch CIFAR step (csrc/cifar_persist.hip, train/persist.py) against
+the launch-per-layer engine and the fp32 autograd oracle of the same network."""
 import pytest
 import torch
 
+from distributed_tensorflow_resnet_amd.models.params import ParamStore
+from distributed_tensorflow_resnet_amd.models.resnet_torch import TorchResNet
+from distributed_tensorflow_resnet_amd.models.spec import cifar_spec
+from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule
+
 pytestmark = pytest.mark.gpu
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                "scripts"))
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("N,L", [(4, 4), (16, 6), (32, 16)])
-def test_persistent_stage_matches_reference(gpu, N, L):
-    import persist_probe as pp
+def _engine(monkeypatch, spec, N, gpu, persist, input_mode="nhwc"):
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
+    eng = Engine(spec, N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu,
+                 input_mode=input_mode, use_graph=False)
+    assert eng.persist == (persist == 1)
+    return eng
 
-    from distributed_tensorflow_resnet_amd.ops import functional as fn
 
-    nat = fn.native()
-    ins = pp.make_inputs(N, L, gpu, seed=N + L)
-    ref = pp.reference(*ins)
-    for _ in range(2):
-        y, _ = pp.run_persistent(nat, *ins)
-        for i in range(L):
-            rel = ((y[i].float() - ref[i].float()).norm() / ref[i].float().norm()).item()
-            assert rel < 2e-2, f"layer {i}: rel err {rel}"
+def _batch(spec, N, gpu, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    imgs = torch.randn(N, spec.image_h, spec.image_w, 3, generator=g).to(torch.bfloat16).float()
+    labels = torch.randint(0, spec.num_classes, (N,), generator=g)
+    return imgs.to(gpu), labels.to(gpu)
+
+
+def _pair(monkeypatch, spec, N, gpu):
+    ep = _engine(monkeypatch, spec, N, gpu, 1)
+    er = _engine(monkeypatch, spec, N, gpu, 0)
+    er.params.master.copy_(ep.params.master)
+    er.params.stats.copy_(ep.params.stats)
+    er.repack()
+    imgs, labels = _batch(spec, N, gpu)
+    for e in (ep, er):
+        e.set_batch(imgs, labels)
+    return ep, er, imgs, labels
+
+
+@pytest.mark.parametrize("size,N", [(8, 16), (20, 32), (50, 16)])
+def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N):
+    """Saved activations, batch statistics and head outputs of the one-launch forward
+    vs the per-layer forward (same weights, same batch): bf16-rounding agreement."""
+    spec = cifar_spec(size)
+    ep, er, _, _ = _pair(monkeypatch, spec, N, gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    for e in (ep, er):
+        e._run("fwd", st)
+    torch.cuda.synchronize()
+    assert not ep.persist_error()
+    worst = 0.0
+    for i in range(len(spec.blocks)):
+        for a, b in ((ep.X[i + 1], er.X[i + 1]), (ep.H1[i], er.H1[i])):
+            worst = max(worst, _rel(a, b))
+    assert _rel(ep.X[0], er.X[0]) < 1e-2
+    assert worst < 5e-2, worst
+    for name, bp in ep.bns.items():
+        br = er.bns[name]
+        assert _rel(bp.mean, br.mean) < 5e-2 + 1e-3 * br.mean.abs().max().item(), name
+        assert _rel(bp.rstd, br.rstd) < 2e-2, name
+    assert _rel(ep.pooled, er.pooled) < 3e-2
+    assert _rel(ep.dlogits.float(), er.dlogits.float()) < 3e-2
+    assert _rel(ep.params.stats, er.params.stats) < 1e-3   # moving averages
+
+
+@pytest.mark.parametrize("size,N", [(8, 16), (8, 32)])
+def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N):
+    """Whole training step (forward + backward + slab reduces): per-tensor gradients
+    vs the bf16-emulating fp32 oracle, like test_engine_step_matches_autograd_shallow."""
+    spec = cifar_spec(size)
+    ep = _engine(monkeypatch, spec, N, gpu, 1)
+    imgs, labels = _batch(spec, N, gpu)
+    ep.set_batch(imgs, labels)
+    store = ParamStore(spec, device=gpu)
+    store.master.copy_(ep.params.master)
+    store.stats.copy_(ep.params.stats)
+    st = torch.cuda.current_stream().cuda_stream
+    ep._run("fwd", st)
+    ep._run_bwd(st)
+    torch.cuda.synchronize()
+    assert not ep.persist_error()
+    model = TorchResNet(spec, store, emulate_bf16=True)
+    logits = model(imgs, True)
+    xent, _ = model.loss(logits, labels, 2e-4)
+    xent.backward()
+    g_ref = store.master.grad.detach()
+    assert abs(ep.scalars[0].item() / N - xent.item()) < 1e-2 * max(1.0, xent.item())
+    worst = sorted(((_rel(ep.grad[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]),
+                     s.name) for s in ep.params.train_slots), reverse=True)
+    print("worst per-tensor gradient rel err:", worst[:4], "global", _rel(ep.grad, g_ref))
+    assert _rel(ep.grad, g_ref) < 5e-2, worst[:5]
+    assert _rel(ep.params.stats, store.stats) < 1e-3
+
+
+@pytest.mark.parametrize("size,N", [(20, 32), (50, 16)])
+def test_persistent_step_matches_per_layer_engine(gpu, monkeypatch, size, N):
+    """Deep nets: the persistent gradient is as close to the per-layer engine's as the
+    per-layer engine is to the fp32 oracle (bf16 chaos), and points the same way."""
+    spec = cifar_spec(size)
+    ep, er, imgs, labels = _pair(monkeypatch, spec, N, gpu)
+    st = torch.cuda.current_stream().cuda_stream
+    for e in (ep, er):
+        e._run("fwd", st)
+        e._run_bwd(st)
+    torch.cuda.synchronize()
+    assert not ep.persist_error()
+    err = _rel(ep.grad, er.grad)
+    cos = torch.nn.functional.cosine_similarity(ep.grad, er.grad, dim=0).item()
+    print(f"persistent vs per-layer: rel {err:.4f} cos {cos:.5f}")
+    assert cos > 0.98 and err < 0.2
+    for name, bp in ep.bns.items():   # BN parameter gradients written by image 0
+        br = er.bns[name]
+        n = bp.spec.channels
+        gp = ep.grad[(bp.dgamma - ep.grad.data_ptr()) // 4:][:n]
+        gr = er.grad[(br.dgamma - er.grad.data_ptr()) // 4:][:n]
+        assert torch.isfinite(gp).all(), name
+        assert torch.nn.functional.cosine_similarity(gp, gr, dim=0).item() > 0.9, name
+
+
+def test_persistent_step_is_deterministic(gpu, monkeypatch):
+    """Fixed-order slot combines and slab reduces: two runs are bitwise equal."""
+    spec = cifar_spec(20)
+    eng = _engine(monkeypatch, spec, 32, gpu, 1)
+    imgs, labels = _batch(spec, 32, gpu)
+    eng.set_batch(imgs, labels)
+    st = torch.cuda.current_stream().cuda_stream
+    out = []
+    for _ in range(3):
+        eng._run("fwd", st)
+        eng._run_bwd(st)
+        torch.cuda.synchronize()
+        out.append(eng.grad.clone())
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
+    assert not eng.persist_error()
+
+
+def test_persistent_training_tracks_per_layer(gpu, monkeypatch):
+    """Eight full steps (optimizer, augmentation, moving averages) of both paths on the
+    same uint8 batch: the losses track each other and go down."""
+    spec = cifar_spec(20)
+    N = 16
+    losses = {}
+    for p in (1, 0):
+        eng = _engine(monkeypatch, spec, N, gpu, p, input_mode="cifar_u8")
+        eng.fill_synthetic(0)
+        ls = []
+        for _ in range(8):
+            eng.step()
+            ls.append(eng.metrics(reduce=False)["cross_entropy"])
+        losses[p] = ls
+        if p:
+            assert not eng.persist_error()
+    print("persistent", [round(v, 4) for v in losses[1]], "per-layer", [round(v, 4) for v in losses[0]])
+    assert losses[1][-1] < losses[1][0]
+    for a, b in zip(losses[1], losses[0]):
+        assert abs(a - b) < 0.05 * max(1.0, abs(b))
+
+
+def test_persistent_auto_selection(gpu, monkeypatch):
+    """tune persist -1: on at per-rank batch <= 32, off above; never for ImageNet."""
+    from distributed_tensorflow_resnet_amd.models.spec import imagenet_spec
+
+    monkeypatch.setenv("DTR_TUNE", "persist=-1")
+    mk = lambda spec, N: Engine(spec, N, weight_decay=2e-4,  # noqa: E731
+                                lr_schedule=cifar_lr_schedule(), device=gpu)
+    assert mk(cifar_spec(8), 32).persist
+    assert not mk(cifar_spec(8), 64).persist
+    assert not mk(imagenet_spec(18, image_hw=64), 8).persist
