@@ -50,6 +50,43 @@ static ConvGeom geom_from(const std::vector<int>& v) {
   return ConvGeom{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10]};
 }
 
+// Split-K workspace a plan owns per stream (fp32 slice slabs + last-arriver tile counters
+// of the split-K conv_gemm loops).  Sized while the plan's conv ops are recorded
+// (conv_gemm_splitk_need), so a running step never allocates; ops of one stream run in
+// stream order and share it, ops of different streams never do.
+struct PlanSplitK {
+  float* part = nullptr;
+  size_t bytes = 0;
+  unsigned* cnt = nullptr;
+  size_t cnt_n = 0;
+  void reserve(size_t b, size_t tiles) {
+    if (b <= bytes && tiles <= cnt_n) return;
+    (void)hipDeviceSynchronize();   // recording after a run: nothing may still read the old ones
+    if (b > bytes) {
+      void* p = nullptr;
+      if (hipMalloc(&p, b) != hipSuccess) throw std::runtime_error("split-K workspace: hipMalloc failed");
+      (void)hipFree(part);
+      part = static_cast<float*>(p);
+      bytes = b;
+    }
+    if (tiles > cnt_n) {
+      void* p = nullptr;
+      if (hipMalloc(&p, tiles * sizeof(unsigned)) != hipSuccess ||
+          hipMemset(p, 0, tiles * sizeof(unsigned)) != hipSuccess)
+        throw std::runtime_error("split-K counters: hipMalloc failed");
+      (void)hipFree(cnt);
+      cnt = static_cast<unsigned*>(p);
+      cnt_n = tiles;
+    }
+  }
+  ~PlanSplitK() {
+    (void)hipFree(part);
+    (void)hipFree(cnt);
+  }
+};
+// set while a plan records an op: the workspace of the plan's current stream
+static thread_local PlanSplitK* g_rec_splitk = nullptr;
+
 // ---------------------------------------------------------------- op makers
 // Partials a consumer prologue (bn_prefin_table / bn_prefin_sums, bn_fused.h)
 // combines for C channels: C/4 float4 groups, PFIN_ROUNDS rounds of PFIN_ITEMS.
@@ -181,6 +218,20 @@ static Launch mk_conv_gemm(int mode, ptr_t a, ptr_t b, ptr_t out, ptr_t out_f32,
     const bool ok = grp == 0 ? T <= cap : (grp <= cap && (T + grp - 1) / grp <= cap);
     if (!ok || (grp != 0 && (which == 0 ? g.fin.gpart : g.bfin.gpart) == nullptr))
       throw std::invalid_argument("fused BN finalize: tile count exceeds the combine bound");
+  }
+  if (g_rec_splitk != nullptr) {   // a plan op: its stream's workspace, sized now
+    size_t tiles = 0;
+    const size_t need = conv_gemm_splitk_need(g, mode, &tiles);
+    if (need > 0) {
+      PlanSplitK* ws = g_rec_splitk;
+      ws->reserve(need, tiles);
+      return [g, mode, ws](hipStream_t s) {
+        GemmArgs a = g;
+        a.sk_part = ws->part;
+        a.sk_cnt = ws->cnt;
+        conv_gemm(a, mode, s);
+      };
+    }
   }
   return [g, mode](hipStream_t s) { conv_gemm(g, mode, s); };
 }
@@ -676,6 +727,11 @@ struct IssueWorker {
 
 struct Plan {
   std::vector<PlanOp> ops;
+  std::unique_ptr<PlanSplitK> splitk[3];   // per stream (PLAN_STREAMS)
+  PlanSplitK* splitk_ws(int stream) {
+    if (!splitk[stream]) splitk[stream].reset(new PlanSplitK());
+    return splitk[stream].get();
+  }
   std::vector<std::string> names;
   std::vector<hipEvent_t> events;
   std::vector<hipEvent_t> tevents;            // timing events (OP_TIMING)
@@ -947,7 +1003,18 @@ static void def_op(py::module_& m, py::class_<Plan>& plan, const char* name,
     if (e != hipSuccess)
       throw std::runtime_error(std::string(name) + " launch failed: " + hipGetErrorString(e));
   });
-  plan.def(name, [maker, name](Plan& p, Args... args) { return p.add(maker(args...), name); });
+  plan.def(name, [maker, name](Plan& p, Args... args) {
+    g_rec_splitk = p.splitk_ws(p.cur);
+    Launch l;
+    try {
+      l = maker(args...);
+    } catch (...) {
+      g_rec_splitk = nullptr;
+      throw;
+    }
+    g_rec_splitk = nullptr;
+    return p.add(std::move(l), name);
+  });
 }
 
 namespace dtr {
@@ -1121,6 +1188,16 @@ PYBIND11_MODULE(_C, m) {
 
   // host-side helpers that mirror the launchers' internal choices
   m.def("conv_gemm_bm", &conv_gemm_bm);
+  m.def("conv_gemm_splitk_bytes", [](int mode, std::vector<int> geom) {
+    GemmArgs g{};
+    g.g = geom_from(geom);
+    const ConvGeom& c = g.g;
+    g.M = mode == MODE_FWD ? c.N * c.Ho * c.Wo : c.N * c.H * c.W;
+    g.Ncol = mode == MODE_FWD ? c.K : c.C;
+    g.Kdim = c.kh * c.kw * (mode == MODE_FWD ? c.C : c.K);
+    size_t tiles = 0;
+    return (long long)conv_gemm_splitk_need(g, mode, &tiles);
+  }, "split-K slab bytes conv_gemm would use for a plain conv of this geometry (0: none)");
   m.def("conv_gemm_bn", &conv_gemm_bn);
   m.def("conv_direct_covers", [](int mode, std::vector<int> geom) {
     GemmArgs g{};

@@ -577,6 +577,9 @@ static bool conv_gemm_fast(const GemmArgs& a, int mode) {
   return pick_ksplit(tiles, (a.Kdim + 63) / 64) > 1;
 }
 
+// Split-K workspace of an immediate (non-plan) launch: grown on demand, per device.  Plan
+// launches never come here -- the plan owns one workspace per stream, sized when the op is
+// recorded (conv_gemm_splitk_need) and passed in GemmArgs::sk_part / sk_cnt.
 struct SplitKWorkspace {
   float* part = nullptr;
   size_t part_bytes = 0;
@@ -595,10 +598,12 @@ static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s, flo
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cap);
     if (cap != hipStreamCaptureStatusNone) return false;
+    (void)hipStreamSynchronize(s);   // the old buffers are no longer read in flight
     if (part_bytes > w.part_bytes) {
       void* p = nullptr;
       if (hipMalloc(&p, part_bytes) != hipSuccess) return false;
-      w.part = static_cast<float*>(p);   // the old buffer may still be read in flight: kept
+      (void)hipFree(w.part);
+      w.part = static_cast<float*>(p);
       w.part_bytes = part_bytes;
     }
     if (tiles > w.cnt_n) {
@@ -606,6 +611,7 @@ static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s, flo
       const size_t n = tiles < 4096 ? 4096 : tiles;
       if (hipMalloc(&p, n * sizeof(unsigned)) != hipSuccess) return false;
       if (hipMemsetAsync(p, 0, n * sizeof(unsigned), s) != hipSuccess) return false;
+      (void)hipFree(w.cnt);
       w.cnt = static_cast<unsigned*>(p);
       w.cnt_n = n;
     }
@@ -614,6 +620,13 @@ static bool splitk_workspace(size_t part_bytes, size_t tiles, hipStream_t s, flo
   *cnt = w.cnt;
   return true;
 }
+
+// Sizing query (conv_gemm_splitk_need): the launchers run their selection logic and
+// record the split-K slab bytes and tile counters they would use, launching nothing.
+struct SplitKNeed {
+  size_t bytes = 0, tiles = 0;
+};
+static thread_local SplitKNeed* g_sk_query = nullptr;
 
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
 static void launch_nbuf(const GemmArgs& a0, hipStream_t s);
@@ -636,6 +649,8 @@ static void launch_cfg(const GemmArgs& a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int MODE, int FLAGS, int NBUF>
 static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
+  // sizing query: only the FAST / ring split-K branch below records a need
+  const bool query = g_sk_query != nullptr;
   a.wt = wt_store_enabled() && (long)a.M * a.Ncol * 2 < (1L << 31) ? 1 : 0;
   const int Acin = (MODE == MODE_FWD) ? a.g.C : a.g.K;
   size_t lds = (size_t)NBUF * (BM + BN) * 64 * sizeof(bf16);
@@ -645,6 +660,7 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
   dim3 grid((a.M + BM - 1) / BM, (a.Ncol + BN - 1) / BN, a.par ? 4 : 1);
   // the pipelined FAST loop is instantiated for the wide-column (ImageNet) tiles
   if constexpr (NBUF == 1) {   // general loop only (launch_cfg: one-tile K loops)
+    if (query) return;
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, 1>), grid,
                        dim3(256), lds, s, a);
     DTR_CHECK_LAUNCH();
@@ -655,10 +671,21 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
       if (ring || conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
         const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
-        float* part = nullptr;
-        unsigned* cnt = nullptr;
-        if (S > 1 && splitk_workspace((size_t)S * tiles * BM * BN * sizeof(float),
-                                      (size_t)tiles, s, &part, &cnt)) {
+        const size_t need = (size_t)S * tiles * BM * BN * sizeof(float);
+        if (g_sk_query) {
+          if (S > 1) {
+            g_sk_query->bytes = need;
+            g_sk_query->tiles = (size_t)tiles;
+          }
+          return;
+        }
+        float* part = a.sk_part;
+        unsigned* cnt = a.sk_cnt;
+        // a plan's op brings its stream's workspace (sized at record time); an immediate
+        // call uses the per-device one
+        const bool ok = part != nullptr ? true
+                                         : splitk_workspace(need, (size_t)tiles, s, &part, &cnt);
+        if (S > 1 && ok) {
           a.ksplit = S;
           a.sk_part = part;
           a.sk_cnt = cnt;
@@ -674,6 +701,7 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
         return;
       }
     }
+    if (query) return;
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE, FLAGS, false, NBUF>), grid,
                        dim3(256), lds, s, a);
     DTR_CHECK_LAUNCH();
@@ -766,8 +794,24 @@ bool conv_gemm_uses_ring(const GemmArgs& a0, int mode) {
   return conv_ring_covers(a, mode);
 }
 
+size_t conv_gemm_splitk_need(const GemmArgs& a, int mode, size_t* tiles) {
+  SplitKNeed need;
+  if (!conv_direct_covers(a, mode)) {
+    g_sk_query = &need;
+    try {
+      conv_gemm(a, mode, nullptr);
+    } catch (...) {
+      g_sk_query = nullptr;
+      throw;
+    }
+    g_sk_query = nullptr;
+  }
+  if (tiles) *tiles = need.tiles;
+  return need.bytes;
+}
+
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s) {
-  if (conv_direct(a, mode, s)) return;
+  if (g_sk_query == nullptr && conv_direct(a, mode, s)) return;
   if (a.abwd.x != nullptr)
     throw std::runtime_error("conv_gemm: the fused BN backward (abwd) is direct-conv only");
   if (mode == MODE_FWD) {

@@ -181,6 +181,9 @@ bool bnf1x1_covers(int M, int C, int K);
 void bnf1x1(const BnfArgs& a, hipStream_t s);
 
 void conv_gemm(const GemmArgs& a, int mode, hipStream_t s);
+// Split-K slab bytes (and tile counters) conv_gemm would use for this conv, 0 = none;
+// launches nothing.  Plans size their per-stream workspace with it at record time.
+size_t conv_gemm_splitk_need(const GemmArgs& a, int mode, size_t* tiles);
 void set_conv_splitk(int max_slices);   // split-K of under-filled FAST grids (1 = off)
 void set_conv_parity(int enabled);      // stride-2 dgrads by output parity class
 // Direct halo-tiled 3x3/s1 kernel for small C (conv_direct.hip); false = not covered.

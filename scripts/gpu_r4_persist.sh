@@ -2,7 +2,7 @@
 # Persistent CIFAR step: numerics tests, then bs16/32 A/B against the per-layer engine.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail
-timeout -k 10 400 python3 -u -m pytest tests/test_persist_gpu.py -x -v -s --timeout 120 --timeout-method thread > gpurun_out/persist_tests.log 2>&1
+timeout -k 10 400 python3 -u -m pytest tests/test_persist_gpu.py tests/test_plan_gpu.py -x -v -s --timeout 120 --timeout-method thread > gpurun_out/persist_tests.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|Error|error|worst|persistent|rel" gpurun_out/persist_tests.log | tail -40
 [ $rc -eq 0 ] || exit $rc
