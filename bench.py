@@ -118,6 +118,10 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
     procs = []
     out0 = tempfile.TemporaryFile(mode="w+")
     for r in range(n):
+        # HSA_ENABLE_IPC_MODE_LEGACY=0 selects ROCm's dmabuf IPC: the hosts of the MI355X
+        # pool only support dmabuf IPC, and under the legacy mode RCCL's intra-node P2P
+        # (xGMI) buffer exchange fails with "hipIpcGetMemHandle: invalid argument".  An
+        # explicit user value is kept.
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))

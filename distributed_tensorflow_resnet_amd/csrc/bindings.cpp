@@ -1130,7 +1130,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("library_path", &Comm::library_path)
       .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
       .def_static("library", &Comm::library)
-      .def_static("rccl_available", &Comm::rccl_available);
+      .def_static("rccl_available", &Comm::rccl_available)
+      .def_static("rccl_version", &Comm::rccl_version);
   m.attr("COMM_F32") = (int)COMM_F32;
   m.attr("COMM_BF16") = (int)COMM_BF16;
   m.attr("COMM_F64") = (int)COMM_F64;

@@ -38,6 +38,7 @@ struct RcclApi {
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclCommGetAsyncError) async_error = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclGetVersion) get_version = nullptr;   // optional (reporting only)
   std::string path;
 };
 
@@ -78,6 +79,7 @@ const RcclApi& api() {
     DTR_SYM(async_error, ncclCommGetAsyncError)
     DTR_SYM(error_string, ncclGetErrorString)
 #undef DTR_SYM
+    a.get_version = reinterpret_cast<decltype(a.get_version)>(dlsym(h, "ncclGetVersion"));
   });
   if (!err.empty()) throw std::runtime_error(err);
   return a;
@@ -210,6 +212,16 @@ std::string Comm::unique_id() {
 }
 
 std::string Comm::library() { return api().path; }
+
+int Comm::rccl_version() {
+  try {
+    const RcclApi& a = api();
+    int v = 0;
+    if (a.get_version && a.get_version(&v) == ncclSuccess) return v;
+  } catch (...) {
+  }
+  return -1;
+}
 
 bool Comm::rccl_available() {
   try {

@@ -83,6 +83,7 @@ class Comm {
   static std::string unique_id();   // ncclGetUniqueId, 128 opaque bytes
   static std::string library();     // path of the librccl the symbols come from
   static bool rccl_available();     // every RCCL entry point resolves (no throw)
+  static int rccl_version();        // ncclGetVersion of the loaded librccl, -1 if unknown
 
  private:
   std::unique_ptr<Transport> t_;

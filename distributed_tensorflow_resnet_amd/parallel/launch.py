@@ -30,6 +30,9 @@ def _spawn(nproc, script, args, port, addr, extra_env):
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
                     "LOCAL_WORLD_SIZE": str(nproc), "MASTER_ADDR": addr,
                     "MASTER_PORT": str(port)})
+        # dmabuf IPC: the only IPC mode the MI355X hosts support; RCCL's intra-node P2P
+        # (xGMI) buffer exchange fails under the legacy mode ("hipIpcGetMemHandle:
+        # invalid argument").  An explicit user value wins.
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, script] + list(args), env=env,
                                       start_new_session=True))

@@ -1481,7 +1481,12 @@ class Engine:
                 "allreduce_ops": self._n_allreduce if nat else len(self.bucket_sched),
                 "allreduce_bytes": (self._allreduce_bytes if nat else
                                     sum((hi - lo) * per for _, lo, hi in self.bucket_sched)),
-                "rccl_library": self.comm.library_path if nat else None}
+                "rccl_library": self.comm.library_path if nat else None,
+                "rccl_version": (self.nat.Comm.rccl_version()
+                                 if nat and transport == "rccl" else None),
+                # the communication environment of this run (RCCL / HSA knobs)
+                "env": {k: v for k, v in sorted(os.environ.items())
+                        if k.startswith(("NCCL_", "RCCL_", "HSA_"))}}
 
     def capture(self, warmup: int = 2):
         """Run `warmup` real steps on a side stream, then capture one step."""

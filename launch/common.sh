@@ -6,7 +6,9 @@
 set -euo pipefail
 REPO="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 PY="${PYTHON:-python3}"
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+# dmabuf IPC: the only IPC mode the MI355X hosts support -- under the legacy mode RCCL's
+# intra-node P2P (xGMI) buffer exchange fails with "hipIpcGetMemHandle: invalid argument"
+export HSA_ENABLE_IPC_MODE_LEGACY="${HSA_ENABLE_IPC_MODE_LEGACY:-0}"
 export MASTER_ADDR="${MASTER_ADDR:-127.0.0.1}"
 
 # run_bg NAME LOGFILE CMD... : start CMD in its own process group, record the PID
