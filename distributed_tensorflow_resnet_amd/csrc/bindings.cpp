@@ -1162,6 +1162,8 @@ PYBIND11_MODULE(_C, m) {
         "whether bn_bwd_apply_acc (finalize fused into the apply) covers (M, C)");
   def_op(m, plan, "head_fused", mk_head_fused);
   def_op(m, plan, "prn", mk_prn);
+  m.def("prn_set_probe", [](ptr_t p) { prn_set_probe(P<long long>(p)); },
+        "diagnostics: image 0 of the persistent launches records (tag, wall clock) pairs here");
   m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, blocks, classes, kpad)");
   m.def("prn_item_kind", &prn_item_kind, "weight-gradient item kind of a conv (cin, cout, k, stride)");
   m.def("prn_struct_bytes", []() {

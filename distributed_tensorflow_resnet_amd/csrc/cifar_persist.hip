@@ -589,7 +589,20 @@ struct FwdCtx {
   Smem m;
   int img, wave, lane;
   unsigned nbar;     // barriers passed
+  int pc;            // probe stamps written
 };
+
+// diagnostics: image 0's lane 0 records (tag, wall clock) pairs (prn_set_probe)
+template <typename Ctx>
+__device__ __forceinline__ void probe(Ctx& x, int tag) {
+  if (x.a->probe != nullptr) {
+    if (x.img == 0 && threadIdx.x == 0) {
+      x.a->probe[2 * x.pc] = tag;
+      x.a->probe[2 * x.pc + 1] = wall_clock64();
+    }
+    ++x.pc;
+  }
+}
 
 // forward BN statistics of v (stage S) into this image's slot of BN `bi`
 template <int S>
@@ -636,9 +649,12 @@ __device__ __forceinline__ bool block_fwd(FwdCtx& x, bf16x4 (&xr)[8], int bi_nex
   const double Mi = (double)a.N * GI::R * GI::R, Mo = (double)a.N * G::R * G::R;
   const long img_o = (long)x.img * G::R * G::R * G::C;
   // BN1 + ReLU of the block input -> halo A (input stage)
+  probe(x, 100 + S);
   fwd_combine(x, B.bn1, GI::C, Mi);
+  probe(x, 1);
   to_halo<SI, true>(x.m.ha, xr, x.m.tbl, x.m.tbl + 64, wave, lane);
   __syncthreads();
+  probe(x, 2);
   bf16x4 pr[8], hr[8];
   f32x4 acc[8];
   if constexpr (PROJ) {
@@ -649,33 +665,44 @@ __device__ __forceinline__ bool block_fwd(FwdCtx& x, bf16x4 (&xr)[8], int bi_nex
   zero_acc<S>(acc);
   conv_acc<S, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, wave, lane);
   round_acc<S, false>(hr, acc, hr);
+  probe(x, 3);
   fwd_stats<S>(x, hr, B.bn2, wave, lane);
   store_regs<S>(hr, B.h1 + img_o, wave, lane, false);
+  probe(x, 4);
   fwd_arrive(x);
+  probe(x, 5);
   {
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
     const WLoad L2 = wl_fwd(B.w2f, G::C, G::C, 3);
     w_prefetch(L2, w2r);
     if (!fwd_wait(x)) return false;
+    probe(x, 6);
     // BN2 + ReLU -> halo A, conv2 (+ residual)
     fwd_combine(x, B.bn2, G::C, Mo);
+    probe(x, 7);
     to_halo<S, true>(x.m.ha, hr, x.m.tbl, x.m.tbl + 64, wave, lane);
     w_store(L2, w2r, x.m.w1);
   }
   __syncthreads();
+  probe(x, 8);
   zero_acc<S>(acc);
   conv_acc<S, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, wave, lane);
   if constexpr (PROJ) round_acc<S, true>(xr, acc, pr);
   else round_acc<S, true>(xr, acc, xr);
+  probe(x, 9);
   fwd_stats<S>(x, xr, bi_next, wave, lane);
   store_regs<S>(xr, B.out + img_o, wave, lane, false);
+  probe(x, 10);
   fwd_arrive(x);
+  probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
   w_prefetch(next_wp, wpr);
   if (!fwd_wait(x)) return false;
+  probe(x, 12);
   w_store(next_w1, w1r, x.m.w1);   // visible after the next block's first __syncthreads
   w_store(next_wp, wpr, x.m.w2);
+  probe(x, 13);
   return true;
 }
 
@@ -690,7 +717,9 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
   x.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   x.lane = threadIdx.x & 63;
   x.nbar = 0;
+  x.pc = 0;
   const int tid = threadIdx.x;
+  probe(x, 0);
 
   // ---- stem: 3x3 8 -> 16 on the 32x32 image (no BN before it) ----
   {
@@ -762,6 +791,7 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
 
   // ---- head (head.hip head_fused numerics): final BN + ReLU + average pool, dense,
   //      softmax cross-entropy row, dense dgrad, pool gradient, final BN backward sums
+  probe(x, 200);
   const int fb = 2 * a.nblocks;
   const int dunits = 64 * a.kpad / 8;
   bf16x8 dwv = {};
@@ -859,6 +889,7 @@ struct BwdCtx {
   Smem m;
   int img, wave, lane;
   unsigned nbar;
+  int pc;
 };
 
 __device__ __forceinline__ void bwd_arrive(BwdCtx& x) { grid_arrive(x.a->bar + 1, true); }
@@ -925,6 +956,7 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
   const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
   const long img_o = (long)x.img * G::R * G::R * G::C;
   const long img_i = (long)x.img * GI::R * GI::R * GI::C;
+  probe(x, 100 + S);
   bf16x4 hs[8], xs[8];
   load_regs<S>(hs, B.h1 + img_o, wave, lane);     // BN2 input (saved by the forward)
   load_regs<SI>(xs, B.x + img_i, wave, lane);     // BN1 input
@@ -938,8 +970,11 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
   conv_acc<S, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, wave, lane);
   bf16x4 da[8];
   round_acc<S, false>(da, acc, da);
+  probe(x, 3);
   bwd_sums<S>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
+  probe(x, 4);
   bwd_arrive(x);
+  probe(x, 5);
   {
     const WLoad L1 = wl_dgrad(B.w1b, G::C, GI::C, 3);
     WLoad LP{};
@@ -948,7 +983,9 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
     w_prefetch(L1, w1r);
     w_prefetch(LP, wpr);
     if (!bwd_wait(x)) return false;
+    probe(x, 6);
     bwd_combine(x, B.bn2, G::C, (float)a.N * G::R * G::R);
+    probe(x, 7);
     bf16x4 dh[8];
     bwd_apply<S, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
     store_regs<S>(dh, B.dh1 + img_o, wave, lane, true);
@@ -958,6 +995,7 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
     w_store(LP, wpr, x.m.w2);
   }
   __syncthreads();
+  probe(x, 8);
   zero_acc<SI>(acc);
   if constexpr (STR == 2) {
     dgrad_s2_acc<SI, G::C, false>(acc, x.m.ha, x.m.w1, wave, lane);
@@ -967,12 +1005,17 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
     if constexpr (PROJ) conv_acc<S, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, wave, lane);
   }
   round_acc<SI, false>(da, acc, da);
+  probe(x, 9);
   bwd_sums<SI>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
+  probe(x, 10);
   bwd_arrive(x);
+  probe(x, 11);
   bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
   w_prefetch(next_w2, w2r);
   if (!bwd_wait(x)) return false;
+  probe(x, 12);
   bwd_combine(x, B.bn1, GI::C, (float)a.N * GI::R * GI::R);
+  probe(x, 13);
   if constexpr (PROJ) bwd_apply<SI, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   else bwd_apply<SI, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   w_store(next_w2, w2r, x.m.w1);   // visible after the next block's first __syncthreads
@@ -1128,6 +1171,8 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   x.wave = wave;
   x.lane = lane;
   x.nbar = 0;
+  x.pc = 0;
+  probe(x, 0);
   const int nb = a.nblocks;
   const PrnBlock& BL = a.blocks[nb - 1];
   {   // the last block's conv2 dgrad weights (stage 2: 64 x 576)
@@ -1178,6 +1223,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   for (int bi = nps - 1; bi > 0; --bi)
     if (!run(BlkTag<0, 1, false>{}, bi)) return;
   if (!run(BlkTag<0, 1, true>{}, 0)) return;
+  probe(x, 200);
   // ---- the stem output's gradient: published for the stem's weight gradient ----
   store_regs<0>(dout, a.dx0 + (long)x.img * 1024 * 16, wave, lane, true);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1186,6 +1232,9 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
 }
 
 // ---- host ------------------------------------------------------------------------------
+static long long* g_prn_probe = nullptr;
+void prn_set_probe(long long* p) { g_prn_probe = p; }
+
 size_t prn_lds_bytes() { return LDS_TOTAL; }
 
 bool prn_supported(int N, int nblocks, int classes, int kpad) {
@@ -1209,7 +1258,9 @@ static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS
 void prn_forward(const PrnArgs& a, hipStream_t s) {
   if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad) || a.N > cu_count())
     throw std::invalid_argument("prn_forward: unsupported shape (N <= CUs, 3n blocks, <= 64 classes)");
-  hipLaunchKernelGGL(prn_fwd_kernel, dim3(a.N), dim3(PT), LDS_TOTAL, s, a);
+  PrnArgs b = a;
+  b.probe = g_prn_probe;
+  hipLaunchKernelGGL(prn_fwd_kernel, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }
 
@@ -1219,7 +1270,9 @@ void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
   const int grid = a.N + std::max(1, wgrad_wgs);
   if (grid > cu_count())
     throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
-  hipLaunchKernelGGL(prn_bwd_kernel, dim3(grid), dim3(PT), LDS_TOTAL, s, a);
+  PrnArgs b = a;
+  b.probe = g_prn_probe;
+  hipLaunchKernelGGL(prn_bwd_kernel, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }
 

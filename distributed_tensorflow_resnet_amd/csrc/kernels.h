@@ -272,8 +272,10 @@ struct PrnArgs {
   float grad_scale;          // 1 / global batch
   float momentum, eps;
   int update_moving;
+  long long* probe = nullptr;   // diagnostics: image 0's (tag, wall clock) phase stamps
 };
 enum { PRN_THREADS = 512, PRN_SLOT = 128 };
+void prn_set_probe(long long* p);   // diagnostics (scripts/prn_probe.py); nullptr = off
 bool prn_supported(int N, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
 void prn_forward(const PrnArgs& a, hipStream_t s);

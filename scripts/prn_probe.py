@@ -1,0 +1,79 @@
+"""Phase timeline of the persistent CIFAR launches (csrc/cifar_persist.hip): image 0's
+lane 0 stamps the wall clock (100 MHz) at every phase boundary; this prints, per
+phase transition, the mean and total time over all blocks of the forward and of the
+backward launch.  python scripts/prn_probe.py [batch] [resnet_size]"""
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DTR_TUNE", "persist=1")
+from distributed_tensorflow_resnet_amd.models.spec import cifar_spec  # noqa: E402
+from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule  # noqa: E402
+
+NAMES = {
+    "fwd": {0: "start", 1: "BN1 combine", 2: "halo+sync", 3: "conv1", 4: "stats+store", 5: "arrive",
+            6: "wait", 7: "BN2 combine", 8: "halo+wstore+sync", 9: "conv2", 10: "stats+store",
+            11: "arrive", 12: "wait", 13: "wstore", 200: "blocks done"},
+    "bwd": {0: "start", 3: "dout publish+halo+conv2 dgrad", 4: "bwd sums", 5: "arrive", 6: "wait",
+            7: "BN2 combine", 8: "apply+publish+halo+wstore+sync", 9: "conv1 dgrad", 10: "bwd sums",
+            11: "arrive", 12: "wait", 13: "BN1 combine", 200: "blocks done"},
+}
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    size = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    eng = Engine(cifar_spec(size), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
+                 device=torch.device("cuda", 0))
+    assert eng.persist
+    eng.fill_synthetic(0)
+    for _ in range(20):
+        eng.step()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream().cuda_stream
+    for seg in ("fwd", "bwd"):
+        buf = torch.zeros(2 * 4096, dtype=torch.int64, device="cuda")
+        eng.nat.prn_set_probe(buf.data_ptr())
+        for _ in range(3):   # the last run's stamps
+            buf.zero_()
+            eng._run("fwd", st)
+            if seg == "bwd":
+                eng.nat.prn_set_probe(buf.data_ptr())
+            eng._run_bwd(st)
+            torch.cuda.synchronize()
+        eng.nat.prn_set_probe(0)
+        if seg == "fwd":   # re-run the forward alone with the probe on
+            buf.zero_()
+            eng.nat.prn_set_probe(buf.data_ptr())
+            eng._run("fwd", st)
+            torch.cuda.synchronize()
+            eng.nat.prn_set_probe(0)
+        v = buf.view(-1, 2).cpu().tolist()
+        stamps = [(t, c) for t, c in v if c != 0]
+        acc = defaultdict(list)
+        for (t0, c0), (t1, c1) in zip(stamps, stamps[1:]):
+            if t1 >= 100 and t1 < 200:
+                continue
+            acc[t1].append((c1 - c0) / 100.0)
+        total = (stamps[-1][1] - stamps[0][1]) / 100.0
+        print(f"== {seg} (N={N}, resnet{size}): {total:.1f} us from first to last stamp")
+        for t in sorted(acc):
+            xs = acc[t]
+            print(f"  {str(NAMES[seg].get(t, t)):34s} n={len(xs):3d} mean {sum(xs)/len(xs):7.2f} us  total {sum(xs):8.1f} us")
+        stage_t = defaultdict(float)
+        cur = None
+        for (t0, c0), (t1, c1) in zip(stamps, stamps[1:]):
+            if t0 >= 100 and t0 < 200:
+                cur = t0 - 100
+            if cur is not None:
+                stage_t[cur] += (c1 - c0) / 100.0
+        print("  per stage:", {k: round(v, 1) for k, v in sorted(stage_t.items())})
+    step = eng.step_timed()
+    print("step_timed:", {k: round(v, 4) for k, v in step.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -97,29 +97,39 @@ def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N):
     assert _rel(ep.params.stats, store.stats) < 1e-3
 
 
-@pytest.mark.parametrize("size,N", [(20, 32), (50, 16)])
-def test_persistent_step_matches_per_layer_engine(gpu, monkeypatch, size, N):
-    """Deep nets: the persistent gradient is as close to the per-layer engine's as the
-    per-layer engine is to the fp32 oracle (bf16 chaos), and points the same way."""
+@pytest.mark.parametrize("size,N", [(20, 32), (50, 16), (50, 32)])
+def test_persistent_step_within_bf16_noise_deep(gpu, monkeypatch, size, N):
+    """Deep random-init ResNets are chaotic under bf16 rounding (test_engine_gpu.py,
+    test_engine_step_within_bf16_noise_deep): the persistent gradient must be at least
+    as close to the bf16-emulating oracle as fp32 is, point the same way as the
+    per-layer engine's, and every BatchNorm parameter gradient must be finite."""
     spec = cifar_spec(size)
     ep, er, imgs, labels = _pair(monkeypatch, spec, N, gpu)
+    out = {}
+    for emu in (True, False):
+        store = ParamStore(spec, device=gpu)
+        store.master.copy_(ep.params.master)
+        store.stats.copy_(ep.params.stats)
+        model = TorchResNet(spec, store, emulate_bf16=emu)
+        xent, _ = model.loss(model(imgs, True), labels, 2e-4)
+        xent.backward()
+        out[emu] = (xent.item(), store.master.grad.detach().clone())
     st = torch.cuda.current_stream().cuda_stream
     for e in (ep, er):
         e._run("fwd", st)
         e._run_bwd(st)
     torch.cuda.synchronize()
     assert not ep.persist_error()
-    err = _rel(ep.grad, er.grad)
+    (x_emu, g_emu), (_, g_32) = out[True], out[False]
+    assert abs(ep.scalars[0].item() / N - x_emu) < 2e-2 * max(1.0, x_emu)
+    noise = _rel(g_32, g_emu)
+    err, err_layer = _rel(ep.grad, g_emu), _rel(er.grad, g_emu)
     cos = torch.nn.functional.cosine_similarity(ep.grad, er.grad, dim=0).item()
-    print(f"persistent vs per-layer: rel {err:.4f} cos {cos:.5f}")
-    assert cos > 0.98 and err < 0.2
-    for name, bp in ep.bns.items():   # BN parameter gradients written by image 0
-        br = er.bns[name]
-        n = bp.spec.channels
-        gp = ep.grad[(bp.dgamma - ep.grad.data_ptr()) // 4:][:n]
-        gr = er.grad[(br.dgamma - er.grad.data_ptr()) // 4:][:n]
-        assert torch.isfinite(gp).all(), name
-        assert torch.nn.functional.cosine_similarity(gp, gr, dim=0).item() > 0.9, name
+    print(f"persistent-vs-emu {err:.3f}, per-layer-vs-emu {err_layer:.3f}, fp32-vs-emu "
+          f"{noise:.3f}; persistent-vs-per-layer cos {cos:.4f}")
+    assert err <= max(0.05, noise), (err, noise)
+    assert cos > 0.9
+    assert torch.isfinite(ep.grad).all()
 
 
 def test_persistent_step_is_deterministic(gpu, monkeypatch):
