@@ -469,41 +469,41 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
 }
 
 // Persistent small-batch CIFAR step (cifar_persist.hip).  mode 0: forward launch, 1:
-// backward launch.  ptrs = [blocks, bns, x_in, stem_w, fslot, bslot, bar, err, dense_w,
-// dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N,
+// backward launch.  ptrs = [blocks, bns, x_in, stem_w, pool_acc, bar, err, dense_w,
+// dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N, P,
 // classes, kpad, update_moving, wgrad_wgs]; floats = [grad_scale, momentum, eps].
 static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::vector<float> f) {
-  if (p.size() != 17 || n.size() != 7 || f.size() != 3)
-    throw std::invalid_argument("prn: 17 pointers, 7 ints, 3 floats");
+  if (p.size() != 16 || n.size() != 8 || f.size() != 3)
+    throw std::invalid_argument("prn: 16 pointers, 8 ints, 3 floats");
   PrnArgs a{};
   a.blocks = P<const PrnBlock>(p[0]);
   a.bns = P<const PrnBn>(p[1]);
   a.x_in = P<const bf16>(p[2]);
   a.stem_w = P<const bf16>(p[3]);
-  a.fslot = P<float>(p[4]);
-  a.bslot = P<float>(p[5]);
-  a.bar = P<unsigned>(p[6]);
-  a.err = P<int>(p[7]);
-  a.dense_w = P<const bf16>(p[8]);
-  a.dense_b = P<const float>(p[9]);
-  a.labels = P<const int>(p[10]);
-  a.pooled = P<bf16>(p[11]);
-  a.dlogits = P<bf16>(p[12]);
-  a.ws = P<float>(p[13]);
-  a.dpool = P<float>(p[14]);
-  a.dx0 = P<bf16>(p[15]);
-  a.items = P<const PrnItem>(p[16]);
+  a.pool_acc = P<double>(p[4]);
+  a.bar = P<unsigned>(p[5]);
+  a.err = P<int>(p[6]);
+  a.dense_w = P<const bf16>(p[7]);
+  a.dense_b = P<const float>(p[8]);
+  a.labels = P<const int>(p[9]);
+  a.pooled = P<bf16>(p[10]);
+  a.dlogits = P<bf16>(p[11]);
+  a.ws = P<float>(p[12]);
+  a.dpool = P<float>(p[13]);
+  a.dx0 = P<bf16>(p[14]);
+  a.items = P<const PrnItem>(p[15]);
   a.nblocks = n[0];
   a.nitems = n[1];
   a.N = n[2];
-  a.classes = n[3];
-  a.kpad = n[4];
-  a.update_moving = n[5];
-  const int wgs = n[6];
+  a.P = n[3];
+  a.classes = n[4];
+  a.kpad = n[5];
+  a.update_moving = n[6];
+  const int wgs = n[7];
   a.grad_scale = f[0];
   a.momentum = f[1];
   a.eps = f[2];
-  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad))
+  if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad))
     throw std::invalid_argument("prn: unsupported shape");
   if (mode == 0) return [a](hipStream_t s) { prn_forward(a, s); };
   if (mode == 1) return [a, wgs](hipStream_t s) { prn_backward(a, wgs, s); };
@@ -1164,7 +1164,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "prn", mk_prn);
   m.def("prn_set_probe", [](ptr_t p) { prn_set_probe(P<long long>(p)); },
         "diagnostics: image 0 of the persistent launches records (tag, wall clock) pairs here");
-  m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, blocks, classes, kpad)");
+  m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, slices, blocks, classes, kpad)");
   m.def("prn_item_kind", &prn_item_kind, "weight-gradient item kind of a conv (cin, cout, k, stride)");
   m.def("prn_struct_bytes", []() {
     return std::vector<int>{(int)sizeof(PrnBn), (int)sizeof(PrnBlock), (int)sizeof(PrnItem)};

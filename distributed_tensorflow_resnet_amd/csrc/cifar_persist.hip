@@ -1,40 +1,44 @@
-// Persistent small-batch CIFAR ResNet v2 step: the whole forward in one launch, the
-// whole backward (with its weight gradients) in one more.
+// Persistent small-batch CIFAR step: the whole forward in one launch, the whole
+// backward (with its weight gradients) in one more.
 //
 // Why: at the per-rank batches of the strong-scaling headline config (global batch 128
 // over 4-8 GPUs = 16-32 images per rank) every CIFAR conv is a few MFMA microseconds
 // wrapped in a ~1.5 us kernel boundary plus a global-memory round trip of its operands
 // (profiles/cifar_direct_conv_phases.md); ~110 dependent launches set the step time.
-// Here one 512-thread workgroup owns one image for the whole network
-// (resnet_model_official.py:217-278, building_block :94-130):
-//   * the image's activations stay on-chip between layers: a conv's fp32 accumulators
+// Here each image is split into P row slices and one 512-thread workgroup owns one slice
+// for the whole network (resnet_model_official.py:217-278, building_block :94-130):
+//   * the slice's activations stay on-chip between layers: a conv's fp32 accumulators
 //     are rounded to bf16 in registers, the next BatchNorm + ReLU is applied from the
 //     registers straight into an LDS halo, and the next conv reads its B operand there;
-//     global memory only receives the tensors the backward needs (write-only);
-//   * BatchNorm's batch statistics are the only cross-image dependency: each workgroup
-//     publishes its image's per-channel (sum, sum of squares) -- or, backward, (sum g,
-//     sum g*xhat) -- in its own slot, one grid barrier, then every workgroup combines
-//     all slots in the same fixed order (fp64) -> bitwise-identical tables everywhere;
-//   * the next layer's weights are prefetched into registers by waves 1-7 while the
-//     current layer computes and waits (wave 0 polls the barrier), then stored to LDS;
+//   * a 3x3 conv needs one halo row from each neighbouring slice: the forward reads it
+//     from the tensor the neighbour publishes anyway (the activations saved for the
+//     backward, stored write-through before the barrier) and applies BN + ReLU itself;
+//     the backward recomputes the neighbour's BN-backward output rows from what the
+//     neighbour published before the barrier (its dgrad output) plus saved tensors;
+//   * BatchNorm's batch statistics are the only cross-slice dependency: each workgroup
+//     adds its slice's per-channel sums into fp64 replicas with memory-side atomics
+//     (exact: fp32 partials summed in fp64, so the result does not depend on the order),
+//     one grid barrier, then every workgroup reads the sums -- one round trip;
+//   * the next layer's weights are prefetched into registers by waves 1-7 between the
+//     barrier's arrive and its wait (wave 0 polls), then stored to LDS;
 //   * MFMA orientation D[channel][pixel] = W[channel][k] x Act[k][pixel]
 //     (v_mfma_f32_16x16x32_bf16): a lane's accumulator holds 4 consecutive channels of
 //     one pixel, i.e. one 8-byte NHWC store / LDS write after the bf16 rounding;
-//   * pixels are kept in a "canonical" order per stage: parity-class-major on the 32x32
+//   * pixels are kept in a "canonical" order per slice: parity-class-major on the 32x32
 //     and 16x16 maps, so every stride-2 dgrad tile (sub-pixel decomposition: 1, 2, 2 or
 //     4 taps per output parity class) is made of pixels of one class.
-// In the backward launch the workgroups beyond the N image workgroups compute the 52
-// weight gradients (dW = sum_p dy x im2col(relu(bn(x)))) per image group into fp32
-// slabs, each item as soon as the image workgroups' barrier counter says its dy is
-// published; the existing deterministic grouped reduce sums the slabs afterwards.
+// In the backward launch the workgroups beyond the N x P slices compute the 52 weight
+// gradients (dW = sum_p dy x im2col(relu(bn(x)))) per image group into fp32 slabs, each
+// item as soon as the slices' barrier counter says its dy is published; the existing
+// deterministic grouped reduce sums the slabs afterwards.
 //
 // Hand-off protocol (MI355X_MICROARCH.md, "Valid forms" row 1): every byte another
-// workgroup reads inside the launch (BN slots, output gradients) is stored
-// write-through (sc1), every storing wave drains (s_waitcnt vmcnt(0)) before its
-// workgroup's lane 0 adds to the barrier counter, consumers poll the counter with
-// relaxed agent loads and read the bytes with sc1 loads.  Every spin is bounded (2 s
-// of wall clock): a timed-out wait sets *err and the workgroup exits.
-// The grid must be co-resident: one workgroup per CU (LDS), grid <= CUs (host checks).
+// workgroup reads inside the launch (published tensors) is stored write-through (sc1),
+// every wave drains (s_waitcnt vmcnt(0)) before its workgroup's lane 0 adds to the
+// barrier counter, consumers poll the counter with relaxed agent loads and read the bytes
+// with sc1 loads.  BN sums are memory-side atomics, read with sc1 loads after the
+// barrier.  Every spin is bounded (2 s of wall clock): a timed-out wait sets *err and the
+// workgroup exits.  The grid must be co-resident: one workgroup per CU, grid <= CUs.
 #include <algorithm>
 #include <stdexcept>
 
@@ -53,57 +57,66 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // ---- geometry ---------------------------------------------------------------------
-template <int S>
-struct Stg {                                  // stage S: R x R maps, C channels
+template <int S, int P>
+struct Stg {                                  // stage S: R x R maps, C channels, P slices
   static constexpr int R = 32 >> S, C = 16 << S, U = C / 8, W2 = R + 2;
-  static constexpr int NPB = R * R / 16, NCB = C / 16;   // 16-pixel / 16-channel blocks
+  static constexpr int RS = R / P, HR = RS + 2;          // rows per slice, halo rows
+  static constexpr int NPX = R * RS;                     // pixels per slice
+  static constexpr int NPB = NPX / 16, NCB = C / 16;     // 16-pixel / 16-channel blocks
   static constexpr int WPB = NPB >= NW ? 1 : NW / NPB;   // waves per pixel block
   static constexpr int PBW = NPB >= NW ? NPB / NW : 1;   // pixel blocks per wave
-  static constexpr int CBW = NCB / WPB;                  // channel blocks per wave
+  static constexpr int CBW = NCB / WPB > 0 ? NCB / WPB : 1;   // channel blocks per wave
   static constexpr int TPW = PBW * CBW;                  // 16x16 tiles per wave
-  static_assert(CBW >= 1 && TPW <= 8, "tiles");
+  static constexpr bool ALL = NPB * NCB >= NW;           // every wave holds tiles
+  static constexpr bool CLS = R > 8;                     // parity-class-major pixel order
+  static_assert(RS >= 2 && (!CLS || RS % 2 == 0) && NPX % 16 == 0 && TPW <= 8, "slices");
+  static_assert(!CLS || (NPB / 4) % PBW == 0, "a wave's pixel blocks lie in one class");
 };
 
-// canonical pixel index -> (h, w): parity-class-major on 32x32 / 16x16, row-major on 8x8
-template <int S>
-__device__ __forceinline__ void canon(int p, int& h, int& w) {
-  constexpr int R = Stg<S>::R;
-  if constexpr (R > 8) {
-    constexpr int Q = R * R / 4, H2 = R / 2;
-    const int cls = p / Q, idx = p - cls * Q;
-    h = 2 * (idx / H2) + (cls >> 1);
-    w = 2 * (idx % H2) + (cls & 1);
+// slice k's canonical pixel p -> image (h, w): parity-class-major on 32x32 / 16x16
+// (class, class row, class column), row-major on 8x8
+template <int S, int P>
+__device__ __forceinline__ void canon(int k, int p, int& h, int& w) {
+  using G = Stg<S, P>;
+  if constexpr (G::CLS) {
+    constexpr int Q = G::NPX / 4, H2 = G::R / 2;
+    const int cls = p / Q, idx = p - cls * Q, il = idx / H2;
+    h = k * G::RS + 2 * il + (cls >> 1);
+    w = 2 * (idx - il * H2) + (cls & 1);
   } else {
-    h = p / R;
-    w = p % R;
+    h = k * G::RS + p / G::R;
+    w = p % G::R;
   }
 }
 
-// this wave's tile t -> (pixel block, channel block)
-template <int S>
+// this wave's tile t -> (pixel block, channel block); a wave is idle (no tiles) when the
+// slice has fewer tiles than waves and its channel block is past the last
+template <int S, int P>
 __device__ __forceinline__ void tile_of(int wave, int t, int& pb, int& cb) {
-  using G = Stg<S>;
+  using G = Stg<S, P>;
   pb = (wave / G::WPB) * G::PBW + t / G::CBW;
   cb = (wave % G::WPB) * G::CBW + t % G::CBW;
 }
+template <int S, int P>
+__device__ __forceinline__ bool wave_active(int wave) {
+  using G = Stg<S, P>;
+  return G::ALL || (wave % G::WPB) * G::CBW < G::NCB;
+}
 
-// LDS halo element offset: pixel `pix` (row-major in the (R+2)^2 halo, column hc),
-// channel c (multiple of 4) of a U-unit (8 channels per 16-B unit) image; units XOR-
-// swizzled by the halo column so the 16 pixel lanes of a fragment read spread over banks
+// LDS halo element offset: local pixel `pix` (row-major in the HR x W2 slice halo,
+// column lc), channel c (multiple of 4) of a U-unit (8 channels per 16-B unit) image;
+// units XOR-swizzled by the column so a fragment's 16 pixel lanes spread over banks
 template <int U>
-__device__ __forceinline__ int haddr(int pix, int hc, int c) {
-  return (pix * U + ((c >> 3) ^ (hc & (U - 1)))) * 8 + (c & 7);
+__device__ __forceinline__ int haddr(int pix, int lc, int c) {
+  return (pix * U + ((c >> 3) ^ (lc & (U - 1)))) * 8 + (c & 7);
 }
 
 __device__ __forceinline__ bf16x8 lds16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-__device__ __forceinline__ float ld_sc1_f(const float* p) {
+__device__ __forceinline__ double ld_sc1_d(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_sc1_f(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 8-byte write-through store / load of 4 bf16 (buffer ops with the sc1 cache bit)
+// 8-byte write-through store of 4 bf16 / 16-byte sc1 load (buffer ops with the sc1 bit)
 __device__ __forceinline__ void st_sc1_b64(bf16* base, long elem, bf16x4 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 16);
@@ -115,8 +128,8 @@ __device__ __forceinline__ bf16x8 ld_sc1_b128(const bf16* base, long elem) {
 }
 
 // Opaque copies of the lane / wave ids: every per-tile address is derived from them
-// inside each block's code instead of being hoisted to the kernel entry and kept live
-// across the whole network (which spilled hundreds of registers).
+// inside each phase instead of being hoisted to the kernel entry and kept live across
+// the whole network (which spilled hundreds of registers).
 __device__ __forceinline__ int opaque_v(int v) {
   asm volatile("" : "+v"(v));
   return v;
@@ -127,14 +140,25 @@ __device__ __forceinline__ int opaque_s(int v) {
 }
 
 // ---- grid barrier ---------------------------------------------------------------------
-// Wait until `target` arrivals; lane 0 of wave 0 polls.  Returns false when the wait
-// timed out (*err set): the caller exits.
+// Every wave drains its stores / atomics, then lane 0 arrives.  The caller issues its
+// prefetches (waves 1-7) and waits (grid_wait).
+__device__ __forceinline__ void grid_arrive(unsigned* bar) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until `target` arrivals; lane 0 of wave 0 polls every SLEEP x 64 clocks (the
+// weight-gradient workgroups poll 8x less often: ~190 of them on one counter line slow
+// the slices' arrives).  Returns false when the wait timed out (*err set): the caller
+// exits.
+template <int SLEEP = 1>
 __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* err, int* flag) {
   if (threadIdx.x == 0) {
     const long long t0 = wall_clock64();
     int ok = 1;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(SLEEP);
       if (wall_clock64() - t0 > kSpinTicks) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
@@ -145,14 +169,6 @@ __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* e
   }
   __syncthreads();
   return *flag != 0;
-}
-
-// drain (all waves, or only wave 0 -- the one that stored the hand-off bytes) + arrive;
-// the caller then issues its weight prefetch (waves 1-7) and waits (grid_wait)
-__device__ __forceinline__ void grid_arrive(unsigned* bar, bool drain_all) {
-  if (drain_all || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- weights: global -> registers (waves 1-7) -> LDS -----------------------------------
@@ -221,39 +237,43 @@ __device__ __forceinline__ WLoad wl_dgrad(const bf16* src, int co, int ci, int k
 }
 
 // ---- convolutions on the LDS halo ------------------------------------------------------
-// acc[t] += sum_k W[channel][k] * Act[k][pixel] over this wave's tiles of output stage SO.
-// Forward (FLIP = false): input halo of CI channels at resolution R_SO * STR, tap (r, s)
-// of output pixel (h, w) at halo (h*STR + r + off, w*STR + s + off), off = 1 for 1x1.
-// Stride-1 dgrad (FLIP = true, 3x3): halo (h + 2 - r, w + 2 - s) of the output gradient.
+// acc[t] += sum_k W[channel][k] * Act[k][pixel] over this wave's tiles of output stage SO,
+// slice k.  The input halo (CI channels, resolution R_SO * STR, slice rows RS_SO * STR
+// plus one halo row above and below) holds image row hi at local row hi - k*RSI + 1.
+// Forward (FLIP = false): tap (r, s) of output pixel (h, w) reads input (h*STR + r - PAD,
+// w*STR + s - PAD), PAD = 1 for 3x3 (TF fixed padding), 0 for 1x1.
+// Stride-1 dgrad (FLIP = true, 3x3): input (h + 1 - r, w + 1 - s) of the output gradient.
 // Weights in LDS: [channel][k = tap * CI + ci] rows of KP.
-template <int SO, int CI, int KSZ, int STR, bool FLIP>
+template <int SO, int P, int CI, int KSZ, int STR, bool FLIP>
 __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const bf16* wl,
-                                         int wave, int lane) {
+                                         int kslice, int wave, int lane) {
+  using G = Stg<SO, P>;
   lane = opaque_v(lane);
-  using G = Stg<SO>;
-  constexpr int RI = G::R * STR, W2I = RI + 2, UI = CI >= 8 ? CI / 8 : 1;
+  if (!wave_active<SO, P>(wave)) return;
+  constexpr int RI = G::R * STR, RSI = G::RS * STR, W2I = RI + 2, UI = CI >= 8 ? CI / 8 : 1;
   constexpr int K = KSZ * KSZ * CI, KS = (K + 31) / 32, KP = kpad_of(K);
-  constexpr int OFF = KSZ == 1 ? 1 : 0;
+  constexpr int PAD = KSZ == 3 ? 1 : 0;
   const int fr = lane & 15, fq = lane >> 4;
   int hb[G::PBW], hcb[G::PBW];
 #pragma unroll
   for (int i = 0; i < G::PBW; ++i) {
     int pb, cb, h, w;
-    tile_of<SO>(wave, i * G::CBW, pb, cb);
-    canon<SO>(pb * 16 + fr, h, w);
-    hcb[i] = w * STR + OFF;
-    hb[i] = (h * STR + OFF) * W2I + hcb[i];
+    tile_of<SO, P>(wave, i * G::CBW, pb, cb);
+    canon<SO, P>(kslice, pb * 16 + fr, h, w);
+    const int lr = FLIP ? h - kslice * RSI + 2 : h * STR - PAD - kslice * RSI + 1;
+    hcb[i] = FLIP ? w + 2 : w * STR - PAD + 1;
+    hb[i] = lr * W2I + hcb[i];
   }
   int cb0, pb0;
-  tile_of<SO>(wave, 0, pb0, cb0);
+  tile_of<SO, P>(wave, 0, pb0, cb0);
 #pragma unroll 2
   for (int ks = 0; ks < KS; ++ks) {
     const int k = ks * 32 + fq * 8;
     int tap = k / CI;
     const int c = k - tap * CI;
     tap = tap < KSZ * KSZ ? tap : KSZ * KSZ - 1;   // padded k: zero weights
-    const int tr = FLIP ? KSZ - 1 - tap / KSZ : tap / KSZ;
-    const int ts = FLIP ? KSZ - 1 - tap % KSZ : tap % KSZ;
+    const int tr = FLIP ? -(tap / KSZ) : tap / KSZ;
+    const int ts = FLIP ? -(tap % KSZ) : tap % KSZ;
     bf16x8 a[G::CBW];
 #pragma unroll
     for (int j = 0; j < G::CBW; ++j) a[j] = lds16(wl + ((cb0 + j) * 16 + fr) * KP + k);
@@ -266,34 +286,36 @@ __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const
   }
 }
 
-// Stride-2 dgrad into output stage SO (high resolution, parity-class-major pixels) from
-// the output gradient of CO channels at resolution R_SO / 2 in the halo `hal`:
+// Stride-2 dgrad into output stage SO (high resolution, parity-class-major pixels), slice
+// k, from the output gradient of CO channels at resolution R_SO / 2 in the halo `hal`
+// (slice rows RS_SO / 2 + 2 halo rows):
 //   3x3 (PROJ = false): dx(2i+a, 2j+b) = sum over taps r = a+1 (mod 2), s = b+1 (mod 2)
 //     of dy(i + di, j + dj) W[r][s], di = (a + 1 - r) / 2 -- 1, 2, 2 or 4 taps per class;
 //   1x1 (PROJ): dx(2i, 2j) = dy(i, j) Wp (class 0 only).
 // Weights [ci][k = tap * CO + co].  A wave's pixel blocks all lie in one class.
-template <int SO, int CO, bool PROJ>
+template <int SO, int P, int CO, bool PROJ>
 __device__ __forceinline__ void dgrad_s2_acc(f32x4 (&acc)[8], const bf16* hal, const bf16* wl,
-                                             int wave, int lane) {
+                                             int kslice, int wave, int lane) {
+  using G = Stg<SO, P>;
   lane = opaque_v(lane);
-  using G = Stg<SO>;
-  static_assert(G::R > 8, "class-major output");
-  constexpr int RL = G::R / 2, W2L = RL + 2, UL = CO / 8;
+  static_assert(G::CLS, "class-major output");
+  if (!wave_active<SO, P>(wave)) return;
+  constexpr int RL = G::R / 2, RSL = G::RS / 2, W2L = RL + 2, UL = CO / 8;
   constexpr int KP = kpad_of(PROJ ? CO : 9 * CO);
   const int fr = lane & 15, fq = lane >> 4;
   int pb0, cb0;
-  tile_of<SO>(wave, 0, pb0, cb0);
-  const int cls = (pb0 * 16) / (G::R * G::R / 4);
+  tile_of<SO, P>(wave, 0, pb0, cb0);
+  const int cls = (pb0 * 16) / (G::NPX / 4);
   const int ca = cls >> 1, cbit = cls & 1;
   if (PROJ && cls != 0) return;
   int il[G::PBW], jl[G::PBW];
 #pragma unroll
   for (int i = 0; i < G::PBW; ++i) {
     int pb, cb, h, w;
-    tile_of<SO>(wave, i * G::CBW, pb, cb);
-    canon<SO>(pb * 16 + fr, h, w);
-    il[i] = h >> 1;
-    jl[i] = w >> 1;
+    tile_of<SO, P>(wave, i * G::CBW, pb, cb);
+    canon<SO, P>(kslice, pb * 16 + fr, h, w);
+    il[i] = (h >> 1) - kslice * RSL + 1;   // local halo row of dy(i, .)
+    jl[i] = (w >> 1) + 1;
   }
   const int nr = PROJ ? 1 : (ca ? 2 : 1), ns = PROJ ? 1 : (cbit ? 2 : 1);
   for (int ri = 0; ri < nr; ++ri) {
@@ -310,7 +332,7 @@ __device__ __forceinline__ void dgrad_s2_acc(f32x4 (&acc)[8], const bf16* hal, c
         for (int j = 0; j < G::CBW; ++j) av[j] = lds16(wl + ((cb0 + j) * 16 + fr) * KP + k);
 #pragma unroll
         for (int i = 0; i < G::PBW; ++i) {
-          const int hr = il[i] + di + 1, hc = jl[i] + dj + 1;
+          const int hr = il[i] + di, hc = jl[i] + dj;
           const bf16x8 b = lds16(hal + haddr<UL>(hr * W2L + hc, hc, c));
 #pragma unroll
           for (int j = 0; j < G::CBW; ++j) acc[i * G::CBW + j] = mfma16(av[j], b, acc[i * G::CBW + j]);
@@ -321,167 +343,260 @@ __device__ __forceinline__ void dgrad_s2_acc(f32x4 (&acc)[8], const bf16* hal, c
 }
 
 // ---- register tensors (bf16x4 per tile: 4 channels of one pixel) ------------------------
-template <int S>
 __device__ __forceinline__ void zero_acc(f32x4 (&acc)[8]) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// global NHWC element offset (within the image) of this lane's tile-t values
-template <int S>
-__device__ __forceinline__ int gofs(int wave, int lane, int t) {
-  using G = Stg<S>;
+// image NHWC element offset of this lane's tile-t values
+template <int S, int P>
+__device__ __forceinline__ int gofs(int kslice, int wave, int lane, int t) {
+  using G = Stg<S, P>;
   int pb, cb, h, w;
-  tile_of<S>(wave, t, pb, cb);
-  canon<S>(pb * 16 + (lane & 15), h, w);
+  tile_of<S, P>(wave, t, pb, cb);
+  canon<S, P>(kslice, pb * 16 + (lane & 15), h, w);
   return (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4);
 }
 
-template <int S>
-__device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, int wave, int lane) {
+template <int S, int P>
+__device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, int kslice,
+                                          int wave, int lane) {
   lane = opaque_v(lane);
+  if (!wave_active<S, P>(wave)) return;
 #pragma unroll
-  for (int t = 0; t < Stg<S>::TPW; ++t)
-    v[t] = *reinterpret_cast<const bf16x4*>(img_base + gofs<S>(wave, lane, t));
+  for (int t = 0; t < Stg<S, P>::TPW; ++t)
+    v[t] = *reinterpret_cast<const bf16x4*>(img_base + gofs<S, P>(kslice, wave, lane, t));
 }
 
-template <int S>
-__device__ __forceinline__ void store_regs(const bf16x4 (&v)[8], bf16* img_base, int wave, int lane,
-                                           bool sc1) {
+// write-through (sc1) stores: these tensors are read by other workgroups in the launch
+template <int S, int P>
+__device__ __forceinline__ void publish(const bf16x4 (&v)[8], bf16* img_base, int kslice,
+                                        int wave, int lane) {
   lane = opaque_v(lane);
+  if (!wave_active<S, P>(wave)) return;
 #pragma unroll
-  for (int t = 0; t < Stg<S>::TPW; ++t) {
-    const int o = gofs<S>(wave, lane, t);
-    if (sc1) st_sc1_b64(img_base, o, v[t]);
-    else *reinterpret_cast<bf16x4*>(img_base + o) = v[t];
+  for (int t = 0; t < Stg<S, P>::TPW; ++t)
+    st_sc1_b64(img_base, gofs<S, P>(kslice, wave, lane, t), v[t]);
+}
+
+// ---- halos -------------------------------------------------------------------------------
+// Neighbour halo rows: 2 rows x R pixels x U units (always 128 units) -- thread t < 128
+// handles unit t: row sel = t / (R U) (0: image row k*RS - 1, 1: row (k+1)*RS), column,
+// unit.  `ok` is false outside the image (the conv's zero padding).
+template <int S, int P>
+struct Nbr {
+  static constexpr int UNITS = 2 * Stg<S, P>::R * Stg<S, P>::U;
+  static_assert(UNITS <= PT, "neighbour units");
+  int sel, col, u, gofs;   // gofs: image element offset of the unit
+  bool ok;
+  __device__ __forceinline__ Nbr(int kslice) {
+    using G = Stg<S, P>;
+    const int t = threadIdx.x;
+    sel = t / (G::R * G::U);
+    const int rem = t - sel * G::R * G::U;
+    col = rem / G::U;
+    u = rem - col * G::U;
+    const int gr = sel ? (kslice + 1) * G::RS : kslice * G::RS - 1;
+    ok = t < UNITS && gr >= 0 && gr < G::R;
+    gofs = (gr * G::R + col) * G::C + u * 8;
   }
-}
+};
 
-// v (stage S, this lane's tiles) -> halo interior, optionally BN + ReLU (LDS table
-// sc[c], sh[c]); the 1-pixel border is zeroed
-template <int S, bool BN>
+// own values (this wave's tiles; MODE 1: BN + ReLU with the LDS table sc/sh, 0: as is)
+// -> halo rows 1..RS; the neighbour units `nv` (already transformed; zero where !ok)
+// -> rows 0 and RS + 1; the left / right border columns -> zero
+template <int S, int P, int MODE>
 __device__ __forceinline__ void to_halo(bf16* hal, const bf16x4 (&v)[8], const float* sc,
-                                        const float* sh, int wave, int lane) {
+                                        const float* sh, const Nbr<S, P>& nb, bf16x8 nv,
+                                        int kslice, int wave, int lane) {
+  using G = Stg<S, P>;
   lane = opaque_v(lane);
-  using G = Stg<S>;
   const int fr = lane & 15, fq = lane >> 4;
+  if (wave_active<S, P>(wave)) {
 #pragma unroll
-  for (int t = 0; t < G::TPW; ++t) {
-    int pb, cb, h, w;
-    tile_of<S>(wave, t, pb, cb);
-    canon<S>(pb * 16 + fr, h, w);
-    const int c0 = cb * 16 + 4 * fq;
-    bf16x4 o = v[t];
-    if constexpr (BN) {
+    for (int t = 0; t < G::TPW; ++t) {
+      int pb, cb, h, w;
+      tile_of<S, P>(wave, t, pb, cb);
+      canon<S, P>(kslice, pb * 16 + fr, h, w);
+      const int c0 = cb * 16 + 4 * fq;
+      bf16x4 o = v[t];
+      if constexpr (MODE == 1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16)fmaxf((float)v[t][r] * sc[c0 + r] + sh[c0 + r], 0.f);
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)fmaxf((float)v[t][r] * sc[c0 + r] + sh[c0 + r], 0.f);
+      }
+      const int lr = h - kslice * G::RS + 1;
+      *reinterpret_cast<bf16x4*>(hal + haddr<G::U>(lr * G::W2 + w + 1, w + 1, c0)) = o;
     }
-    *reinterpret_cast<bf16x4*>(hal + haddr<G::U>((h + 1) * G::W2 + w + 1, w + 1, c0)) = o;
   }
-  // border: 4 (R + 1) pixels x U units
-  constexpr int NB = 4 * (G::R + 1);
-  for (int q = threadIdx.x; q < NB * G::U; q += PT) {
+  if ((int)threadIdx.x < Nbr<S, P>::UNITS) {
+    const int lr = nb.sel ? G::RS + 1 : 0, lc = nb.col + 1;
+    *reinterpret_cast<bf16x8*>(hal + haddr<G::U>(lr * G::W2 + lc, lc, nb.u * 8)) = nb.ok ? nv : bf16x8{};
+  }
+  // left / right border columns of every halo row
+  for (int q = threadIdx.x; q < 2 * G::HR * G::U; q += PT) {
     const int b = q / G::U, u = q - b * G::U;
-    int hr, hc;
-    if (b < G::W2) { hr = 0; hc = b; }
-    else if (b < 2 * G::W2) { hr = G::R + 1; hc = b - G::W2; }
-    else if (b < 2 * G::W2 + G::R) { hr = b - 2 * G::W2 + 1; hc = 0; }
-    else { hr = b - 2 * G::W2 - G::R + 1; hc = G::R + 1; }
-    *reinterpret_cast<bf16x8*>(hal + haddr<G::U>(hr * G::W2 + hc, hc, u * 8)) = bf16x8{};
+    const int lr = b >> 1, lc = (b & 1) ? G::R + 1 : 0;
+    *reinterpret_cast<bf16x8*>(hal + haddr<G::U>(lr * G::W2 + lc, lc, u * 8)) = bf16x8{};
   }
 }
 
-// Per-channel sums of two per-value quantities over this image -> red[wave][2][64];
-// f(t, r, x1, x2) fills them for value r of tile t.  Then wave 0 folds the waves that
-// hold each channel in a fixed order and stores the image's 2 x C sums to `slot` (sc1).
-template <int S, bool GLOBAL = true, typename F>
-__device__ __forceinline__ void image_sums(F f, float* red, float* slot, int wave, int lane) {
+// Sum over the 16 lanes of a DPP row (the 16 pixel lanes of an MFMA fragment): quad
+// swaps, then the half-row and row mirrors -- VALU-latency DPP moves instead of the
+// LDS-latency ds_bpermute chain __shfl_xor compiles to.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  return v;
+}
+
+// Per-channel sums over this slice of two per-value quantities f(t, r, x1, x2), added to
+// a BN's fp64 accumulator replicas acc [BN_ACC_REP][2][C] (memory-side atomics; exact, so
+// order-independent).  Folding: xor-shuffles over the 16 pixel lanes, then the waves that
+// hold each channel through LDS `red` [8 waves][128] in a fixed order.
+template <int S, int P, typename F>
+__device__ __forceinline__ void bn_sums(F f, float* red, double* acc, int wave, int lane) {
+  using G = Stg<S, P>;
   lane = opaque_v(lane);
-  using G = Stg<S>;
   const int fr = lane & 15, fq = lane >> 4;
-  float s1[G::CBW][4], s2[G::CBW][4];
+  if (wave_active<S, P>(wave)) {
+    float s1[G::CBW][4], s2[G::CBW][4];
 #pragma unroll
-  for (int j = 0; j < G::CBW; ++j)
+    for (int j = 0; j < G::CBW; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
 #pragma unroll
-  for (int t = 0; t < G::TPW; ++t)
+    for (int t = 0; t < G::TPW; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float a, b;
-      f(t, r, a, b);
-      s1[t % G::CBW][r] += a;
-      s2[t % G::CBW][r] += b;
-    }
-#pragma unroll
-  for (int j = 0; j < G::CBW; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      for (int r = 0; r < 4; ++r) {
+        float a, b;
+        f(t, r, a, b);
+        s1[t % G::CBW][r] += a;
+        s2[t % G::CBW][r] += b;
       }
-  if (fr == 0) {
-    int pb, cb0;
-    tile_of<S>(wave, 0, pb, cb0);
 #pragma unroll
     for (int j = 0; j < G::CBW; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int c = (cb0 + j) * 16 + 4 * fq + r;
-        red[wave * 128 + c] = s1[j][r];
-        red[wave * 128 + 64 + c] = s2[j][r];
+        s1[j][r] = row16_sum(s1[j][r]);
+        s2[j][r] = row16_sum(s2[j][r]);
       }
+    if (fr == 0) {
+      int pb, cb0;
+      tile_of<S, P>(wave, 0, pb, cb0);
+#pragma unroll
+      for (int j = 0; j < G::CBW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = (cb0 + j) * 16 + 4 * fq + r;
+          red[wave * 128 + c] = s1[j][r];
+          red[wave * 128 + 64 + c] = s2[j][r];
+        }
+    }
   }
   __syncthreads();
-  // wave 0 alone stores the slot: it is the wave that drains before the barrier arrive
   if (threadIdx.x < G::C) {
     const int c = threadIdx.x;
     const int grp = (c / 16) / G::CBW;   // waves w with w % WPB == grp hold channel c
+    float v1 = 0.f, v2 = 0.f;
 #pragma unroll
-    for (int which = 0; which < 2; ++which) {
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w)
-        if (w % G::WPB == grp) v += red[w * 128 + which * 64 + c];
-      if (GLOBAL) st_sc1_f(slot + which * 64 + c, v);
-      else slot[which * 64 + c] = v;
-    }
+    for (int w = 0; w < NW; ++w)
+      if (w % G::WPB == grp) {
+        v1 += red[w * 128 + c];
+        v2 += red[w * 128 + 64 + c];
+      }
+    double* p = acc + (long)(blockIdx.x % BN_ACC_REP) * 2 * G::C + c;
+    unsafeAtomicAdd(p, (double)v1);
+    unsafeAtomicAdd(p + G::C, (double)v2);
   }
 }
 
-// After the barrier: the N images' slots of one BN -> fp64 sums (fixed order), in
-// dsum[0..C) and dsum[64..64+C).  512 threads = 4 interleaved image slices x 128 values.
-__device__ __forceinline__ void combine_slots(const float* slots, int N, double* dred,
-                                              double* dsum) {
-  const int tid = threadIdx.x, v = tid & 127, part = tid >> 7;
-  double a = 0.0;
-  for (int n = part; n < N; n += 4) a += (double)ld_sc1_f(slots + (long)n * PRN_SLOT + v);
-  dred[part * 128 + v] = a;
-  __syncthreads();
-  if (tid < 128) dsum[tid] = (dred[tid] + dred[128 + tid]) + (dred[256 + tid] + dred[384 + tid]);
-  __syncthreads();
+// After the barrier: the channel's two sums from the BN_ACC_REP replicas (sc1 loads,
+// replicas added in a fixed order)
+__device__ __forceinline__ void acc_read(const double* acc, int C, int c, double& s1, double& s2) {
+  double a[BN_ACC_REP], b[BN_ACC_REP];
+#pragma unroll
+  for (int r = 0; r < BN_ACC_REP; ++r) {
+    a[r] = ld_sc1_d(acc + (long)r * 2 * C + c);
+    b[r] = ld_sc1_d(acc + (long)r * 2 * C + C + c);
+  }
+  s1 = s2 = 0.0;
+#pragma unroll
+  for (int r = 0; r < BN_ACC_REP; ++r) {
+    s1 += a[r];
+    s2 += b[r];
+  }
 }
 
-// forward BN: sums -> scale/shift (+ mean/rstd) table in LDS; image 0 publishes the batch
-// statistics and updates the moving averages (TF FusedBatchNorm semantics, bn_fused.h)
-__device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const double* dsum, int C, double M,
-                                             float eps, float momentum, int update_moving,
-                                             bool img0, float* tbl) {
+// BN parameters prefetched into registers (thread c < C) before a barrier wait
+struct BnRegs {
+  float g, b, mean, rstd, scale, shift;
+};
+__device__ __forceinline__ void bn_prefetch_fwd(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
-    const double dm = dsum[c] / M;
-    const double var = fmax(dsum[64 + c] / M - dm * dm, 0.0);
+    r.g = bn.gamma[c];
+    r.b = bn.beta[c];
+  }
+}
+__device__ __forceinline__ void bn_prefetch_bwd(const PrnBn& bn, int C, BnRegs& r) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    r.g = bn.gamma[c];
+    r.mean = bn.mean[c];
+    r.rstd = bn.rstd[c];
+    r.scale = bn.scale[c];
+    r.shift = bn.shift[c];
+  }
+}
+
+// the forward table (scale, shift, mean, rstd) of a BN the forward launch finalized,
+// into registers before a wait / from registers into LDS [4][64]
+__device__ __forceinline__ void bn_prefetch_tab(const PrnBn& bn, int C, BnRegs& r) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    r.scale = bn.scale[c];
+    r.shift = bn.shift[c];
+    r.mean = bn.mean[c];
+    r.rstd = bn.rstd[c];
+  }
+}
+__device__ __forceinline__ void tab_store(const BnRegs& r, int C, float* tbl) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    tbl[c] = r.scale;
+    tbl[64 + c] = r.shift;
+    tbl[128 + c] = r.mean;
+    tbl[192 + c] = r.rstd;
+  }
+}
+
+// forward BN: sums -> scale/shift/mean/rstd table [4][64] in LDS; workgroup 0 publishes the
+// batch statistics and updates the moving averages (TF FusedBatchNorm, bn_fused.h).
+// Ends with a barrier.
+__device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const BnRegs& pr, int C, double M,
+                                             float eps, float momentum, int update_moving,
+                                             float* tbl) {
+  const int c = threadIdx.x;
+  if (c < C) {
+    double s1, s2;
+    acc_read(bn.acc, C, c, s1, s2);
+    const double dm = s1 / M;
+    const double var = fmax(s2 / M - dm * dm, 0.0);
     const float fmu = (float)dm, fvar = (float)var;
     const float rs = rsqrtf(fvar + eps);
-    const float sc = bn.gamma[c] * rs;
-    const float sh = bn.beta[c] - fmu * sc;
+    const float sc = pr.g * rs;
+    const float sh = pr.b - fmu * sc;
     tbl[c] = sc;
     tbl[64 + c] = sh;
     tbl[128 + c] = fmu;
     tbl[192 + c] = rs;
-    if (img0) {
+    if (blockIdx.x == 0) {
       bn.mean[c] = fmu;
       bn.rstd[c] = rs;
       bn.scale[c] = sc;
@@ -498,22 +613,24 @@ __device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const double* dsum
 }
 
 // backward BN: sums (sum g, sum g*xhat) -> coefficient table [a, b, c, mean, rstd, scale,
-// shift] x 64 (dh = a g - b - c xhat, bn_bwd_apply's formula); image 0 writes dgamma/dbeta
-__device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const double* dsum, int C, float M,
-                                             bool img0, float* tbl) {
+// shift] x 64 (dh = a g - b - c xhat, bn_bwd_apply's formula); workgroup 0 writes
+// dgamma / dbeta.  Ends with a barrier.
+__device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, int C, float M,
+                                             float* tbl) {
   const int c = threadIdx.x;
   if (c < C) {
-    const float sg = (float)dsum[c], sgx = (float)dsum[64 + c];
-    const float rs = bn.rstd[c];
-    const float a = bn.gamma[c] * rs;
+    double d1, d2;
+    acc_read(bn.bacc, C, c, d1, d2);
+    const float sg = (float)d1, sgx = (float)d2;
+    const float a = pr.g * pr.rstd;
     tbl[c] = a;
     tbl[64 + c] = a * sg / M;
     tbl[128 + c] = a * sgx / M;
-    tbl[192 + c] = bn.mean[c];
-    tbl[256 + c] = rs;
-    tbl[320 + c] = bn.scale[c];
-    tbl[384 + c] = bn.shift[c];
-    if (img0) {
+    tbl[192 + c] = pr.mean;
+    tbl[256 + c] = pr.rstd;
+    tbl[320 + c] = pr.scale;
+    tbl[384 + c] = pr.shift;
+    if (blockIdx.x == 0) {
       bn.dbeta[c] = sg;
       bn.dgamma[c] = sgx;
     }
@@ -521,7 +638,7 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const double* dsum
   __syncthreads();
 }
 
-// the forward BN table of a BN the forward launch finalized (backward launch: read back)
+// the forward table of a BN the forward launch finalized (backward launch: read back)
 __device__ __forceinline__ void bn_load_table(const PrnBn& bn, int C, float* tbl) {
   const int c = threadIdx.x;
   if (c < C) {
@@ -532,23 +649,39 @@ __device__ __forceinline__ void bn_load_table(const PrnBn& bn, int C, float* tbl
   }
 }
 
+// 8 values of the BN-backward output a g - b - c xhat (+ add), g = da [x*scale+shift > 0]
+__device__ __forceinline__ bf16x8 bwd8(bf16x8 da, bf16x8 x, bf16x8 add, bool has_add,
+                                       const float* cf, int c0) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float xf = (float)x[j];
+    const float gg = (xf * cf[320 + c] + cf[384 + c] > 0.f) ? (float)da[j] : 0.f;
+    const float xh = (xf - cf[192 + c]) * cf[256 + c];
+    float r = cf[c] * gg - cf[64 + c] - cf[128 + c] * xh;
+    if (has_add) r += (float)add[j];
+    o[j] = (bf16)r;
+  }
+  return o;
+}
+
 // ---- LDS carve-up (bytes) ------------------------------------------------------------
-constexpr int HALO_B = 34 * 34 * 16 * 2;                 // 32x32x16 map + border
+constexpr int HALO_B = (16 + 2) * 34 * 16 * 2;            // P = 2 slice of the 32x32x16 map
 constexpr int W1_B = 64 * kpad_of(576) * 2;               // 64 rows x 9*64 (+pad)
 constexpr int W2_B = 64 * kpad_of(32) * 2;                // projection (64 x 32 fwd / 32 x 64 dgrad)
 constexpr int TBL_B = 7 * 64 * 4;
-constexpr int RED_B = 8 * 128 * 4;                        // [8 waves][128] fp32 == [4][128] fp64
+constexpr int RED_B = 8 * 128 * 4;
 constexpr int MISC_B = 256;
 constexpr int OFF_HA = 0, OFF_HB = OFF_HA + HALO_B, OFF_W1 = OFF_HB + HALO_B,
               OFF_W2 = OFF_W1 + W1_B, OFF_TBL = OFF_W2 + W2_B, OFF_TBL2 = OFF_TBL + TBL_B,
-              OFF_RED = OFF_TBL2 + TBL_B, OFF_DSUM = OFF_RED + RED_B, OFF_MISC = OFF_DSUM + 128 * 8,
+              OFF_RED = OFF_TBL2 + TBL_B, OFF_MISC = OFF_RED + RED_B,
               LDS_TOTAL = OFF_MISC + MISC_B;
 static_assert(LDS_TOTAL <= 163840, "LDS");
 
 struct Smem {
   bf16 *ha, *hb, *w1, *w2;
   float *tbl, *tbl2, *red;
-  double *dred, *dsum;
   int* flag;
 };
 __device__ __forceinline__ Smem carve(char* s) {
@@ -560,43 +693,40 @@ __device__ __forceinline__ Smem carve(char* s) {
   m.tbl = reinterpret_cast<float*>(s + OFF_TBL);
   m.tbl2 = reinterpret_cast<float*>(s + OFF_TBL2);
   m.red = reinterpret_cast<float*>(s + OFF_RED);
-  m.dred = reinterpret_cast<double*>(s + OFF_RED);
-  m.dsum = reinterpret_cast<double*>(s + OFF_DSUM);
   m.flag = reinterpret_cast<int*>(s + OFF_MISC);
   return m;
 }
 
 // round accumulators (+ optional bf16 residual) to bf16 registers
-template <int S, bool RES>
+template <int S, int P, bool RES>
 __device__ __forceinline__ void round_acc(bf16x4 (&o)[8], const f32x4 (&acc)[8], const bf16x4 (&res)[8]) {
 #pragma unroll
-  for (int t = 0; t < Stg<S>::TPW; ++t)
+  for (int t = 0; t < Stg<S, P>::TPW; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[t][r] = (bf16)(RES ? acc[t][r] + (float)res[t][r] : acc[t][r]);
 }
 
-// =====================================================================================
-// forward
-// =====================================================================================
 template <int S_, int STR_, bool PROJ_>
 struct BlkTag {
   static constexpr int S = S_, STR = STR_;
   static constexpr bool PROJ = PROJ_;
 };
 
-struct FwdCtx {
+struct Ctx {
   const PrnArgs* a;
   Smem m;
-  int img, wave, lane;
+  int img, kslice, wave, lane;
   unsigned nbar;     // barriers passed
+  unsigned slices;   // barrier arrivals per barrier (N x P)
   int pc;            // probe stamps written
+  BnRegs bnr;        // prefetched BN parameters of the next combine
+  BnRegs ftr;        // backward: prefetched forward table of the next BN-backward sums
 };
 
-// diagnostics: image 0's lane 0 records (tag, wall clock) pairs (prn_set_probe)
-template <typename Ctx>
+// diagnostics: workgroup 0's lane 0 records (tag, wall clock) pairs (prn_set_probe)
 __device__ __forceinline__ void probe(Ctx& x, int tag) {
   if (x.a->probe != nullptr) {
-    if (x.img == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       x.a->probe[2 * x.pc] = tag;
       x.a->probe[2 * x.pc + 1] = wall_clock64();
     }
@@ -604,27 +734,32 @@ __device__ __forceinline__ void probe(Ctx& x, int tag) {
   }
 }
 
-// forward BN statistics of v (stage S) into this image's slot of BN `bi`
-template <int S>
-__device__ __forceinline__ void fwd_stats(FwdCtx& x, const bf16x4 (&v)[8], int bi, int wave, int lane) {
-  float* slot = x.a->fslot + ((long)bi * x.a->N + x.img) * PRN_SLOT;
-  image_sums<S>([&](int t, int r, float& s1, float& s2) {
+__device__ __forceinline__ bool wait_fwd(Ctx& x) {
+  ++x.nbar;
+  return grid_wait(x.a->bar, x.nbar * x.slices, x.a->err, x.m.flag);
+}
+// Backward: slice workgroup 0 republishes every completed barrier as a count in its own
+// cache line (bar + PRN_READY, 256 B away): the ~190 weight-gradient workgroups poll that
+// line instead of the arrival counter the slices' atomics go to.
+constexpr int PRN_READY = 64;
+__device__ __forceinline__ bool wait_bwd(Ctx& x) {
+  ++x.nbar;
+  const bool ok = grid_wait(x.a->bar + 1, x.nbar * x.slices, x.a->err, x.m.flag);
+  if (ok && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(x.a->bar + PRN_READY, x.nbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ok;
+}
+
+// =====================================================================================
+// forward
+// =====================================================================================
+template <int S, int P>
+__device__ __forceinline__ void fwd_sums(Ctx& x, const bf16x4 (&v)[8], int bi, int wave, int lane) {
+  bn_sums<S, P>([&](int t, int r, float& s1, float& s2) {
     const float f = (float)v[t][r];
     s1 = f;
     s2 = f * f;
-  }, x.m.red, slot, wave, lane);
-}
-
-__device__ __forceinline__ void fwd_arrive(FwdCtx& x) { grid_arrive(x.a->bar, false); }
-__device__ __forceinline__ bool fwd_wait(FwdCtx& x) {
-  ++x.nbar;
-  return grid_wait(x.a->bar, x.nbar * (unsigned)x.a->N, x.a->err, x.m.flag);
-}
-
-__device__ __forceinline__ void fwd_combine(FwdCtx& x, int bi, int C, double M) {
-  const PrnArgs& a = *x.a;
-  combine_slots(a.fslot + (long)bi * a.N * PRN_SLOT, a.N, x.m.dred, x.m.dsum);
-  bn_fwd_table(a.bns[bi], x.m.dsum, C, M, a.eps, a.momentum, a.update_moving, x.img == 0, x.m.tbl);
+  }, x.m.red, x.a->bns[bi].acc, wave, lane);
 }
 
 // prefetch registers for the next block's conv1 after a stage-S block (stage S or S+1)
@@ -634,101 +769,120 @@ __host__ __device__ constexpr int nreg_next_fwd() {
                : nreg(conv_units(64, 64, 3));
 }
 
+// BN + ReLU of the published raw tensor `src` (stage S, this image) into halo `hal`: own
+// values from registers, neighbour rows from src (sc1 loads issued first), table from
+// the BN's accumulators (bnr prefetched).  Ends with a barrier.
+template <int S, int P>
+__device__ __forceinline__ void fwd_bn_halo(Ctx& x, bf16* hal, const bf16x4 (&v)[8],
+                                            const bf16* src, int bi, int wave, int lane) {
+  using G = Stg<S, P>;
+  const PrnArgs& a = *x.a;
+  const Nbr<S, P> nb(x.kslice);
+  bf16x8 nv = {};
+  if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok) nv = ld_sc1_b128(src, nb.gofs);
+  bn_fwd_table(a.bns[bi], x.bnr, G::C, (double)a.N * G::R * G::R, a.eps, a.momentum,
+               a.update_moving, x.m.tbl);
+  if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok)
+    nv = affine_relu8(nv, x.m.tbl + nb.u * 8, x.m.tbl + 64 + nb.u * 8);
+  to_halo<S, P, 1>(hal, v, x.m.tbl, x.m.tbl + 64, nb, nv, x.kslice, wave, lane);
+}
+
 // One building block, output stage S; STR 2: transition (input stage S-1, projection);
 // PROJ with STR 1: stage-0 block 0 (1x1 stride-1 projection).  On entry W1 (W2) hold
-// conv1's (the projection's) weights; on exit they hold the next block's.
-template <int S, int STR, bool PROJ>
-__device__ __forceinline__ bool block_fwd(FwdCtx& x, bf16x4 (&xr)[8], int bi_next,
+// conv1's (the projection's) weights and x.bnr the block's BN1 parameters; on exit the
+// next block's.
+template <int S, int STR, bool PROJ, int P>
+__device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
                                           const WLoad& next_w1, const WLoad& next_wp,
                                           const PrnBlock& B) {
   constexpr int SI = STR == 2 ? S - 1 : S;
-  using GI = Stg<SI>;
-  using G = Stg<S>;
+  using GI = Stg<SI, P>;
+  using G = Stg<S, P>;
   const PrnArgs& a = *x.a;
   const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
-  const double Mi = (double)a.N * GI::R * GI::R, Mo = (double)a.N * G::R * G::R;
   const long img_o = (long)x.img * G::R * G::R * G::C;
-  // BN1 + ReLU of the block input -> halo A (input stage)
+  const long img_i = (long)x.img * GI::R * GI::R * GI::C;
   probe(x, 100 + S);
-  fwd_combine(x, B.bn1, GI::C, Mi);
-  probe(x, 1);
-  to_halo<SI, true>(x.m.ha, xr, x.m.tbl, x.m.tbl + 64, wave, lane);
+  // BN1 + ReLU of the block input -> halo A (input stage)
+  fwd_bn_halo<SI, P>(x, x.m.ha, xr, B.x + img_i, B.bn1, wave, lane);
   __syncthreads();
   probe(x, 2);
   bf16x4 pr[8], hr[8];
   f32x4 acc[8];
   if constexpr (PROJ) {
-    zero_acc<S>(acc);
-    conv_acc<S, GI::C, 1, STR, false>(acc, x.m.ha, x.m.w2, wave, lane);
-    round_acc<S, false>(pr, acc, pr);
+    zero_acc(acc);
+    conv_acc<S, P, GI::C, 1, STR, false>(acc, x.m.ha, x.m.w2, x.kslice, wave, lane);
+    round_acc<S, P, false>(pr, acc, pr);
   }
-  zero_acc<S>(acc);
-  conv_acc<S, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, wave, lane);
-  round_acc<S, false>(hr, acc, hr);
+  zero_acc(acc);
+  conv_acc<S, P, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+  round_acc<S, P, false>(hr, acc, hr);
   probe(x, 3);
-  fwd_stats<S>(x, hr, B.bn2, wave, lane);
-  store_regs<S>(hr, B.h1 + img_o, wave, lane, false);
+  publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
+  fwd_sums<S, P>(x, hr, B.bn2, wave, lane);
   probe(x, 4);
-  fwd_arrive(x);
+  grid_arrive(a.bar);
   probe(x, 5);
   {
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
     const WLoad L2 = wl_fwd(B.w2f, G::C, G::C, 3);
     w_prefetch(L2, w2r);
-    if (!fwd_wait(x)) return false;
+    bn_prefetch_fwd(a.bns[B.bn2], G::C, x.bnr);
+    if (!wait_fwd(x)) return false;
     probe(x, 6);
     // BN2 + ReLU -> halo A, conv2 (+ residual)
-    fwd_combine(x, B.bn2, G::C, Mo);
-    probe(x, 7);
-    to_halo<S, true>(x.m.ha, hr, x.m.tbl, x.m.tbl + 64, wave, lane);
+    fwd_bn_halo<S, P>(x, x.m.ha, hr, B.h1 + img_o, B.bn2, wave, lane);
     w_store(L2, w2r, x.m.w1);
   }
   __syncthreads();
   probe(x, 8);
-  zero_acc<S>(acc);
-  conv_acc<S, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, wave, lane);
-  if constexpr (PROJ) round_acc<S, true>(xr, acc, pr);
-  else round_acc<S, true>(xr, acc, xr);
+  zero_acc(acc);
+  conv_acc<S, P, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+  if constexpr (PROJ) round_acc<S, P, true>(xr, acc, pr);
+  else round_acc<S, P, true>(xr, acc, xr);
   probe(x, 9);
-  fwd_stats<S>(x, xr, bi_next, wave, lane);
-  store_regs<S>(xr, B.out + img_o, wave, lane, false);
+  publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
+  fwd_sums<S, P>(x, xr, bi_next, wave, lane);
   probe(x, 10);
-  fwd_arrive(x);
+  grid_arrive(a.bar);
   probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
   w_prefetch(next_wp, wpr);
-  if (!fwd_wait(x)) return false;
+  bn_prefetch_fwd(a.bns[bi_next], G::C, x.bnr);   // the next BN normalizes this output
+  if (!wait_fwd(x)) return false;
   probe(x, 12);
   w_store(next_w1, w1r, x.m.w1);   // visible after the next block's first __syncthreads
   w_store(next_wp, wpr, x.m.w2);
-  probe(x, 13);
   return true;
 }
 
-}  // namespace
-
-__global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  FwdCtx x;
+template <int P>
+__device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
+  using G0 = Stg<0, P>;
+  Ctx x;
   x.a = &a;
   x.m = carve(smem);
-  x.img = blockIdx.x;
+  x.img = blockIdx.x / P;
+  x.kslice = blockIdx.x % P;
   x.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   x.lane = threadIdx.x & 63;
   x.nbar = 0;
+  x.slices = (unsigned)(a.N * P);
   x.pc = 0;
   const int tid = threadIdx.x;
   probe(x, 0);
 
-  // ---- stem: 3x3 8 -> 16 on the 32x32 image (no BN before it) ----
+  // ---- stem: 3x3 8 -> 16 on the 32x32 image (no BN before it): the slice's rows plus
+  //      one halo row above and below straight from the input ----
   {
     const bf16* src = a.x_in + (long)x.img * 1024 * 8;
-    for (int q = tid; q < 34 * 34; q += PT) {
-      const int hr = q / 34, hc = q - hr * 34;
+    for (int q = tid; q < G0::HR * 34; q += PT) {
+      const int lr = q / 34, lc = q - lr * 34;
+      const int gr = x.kslice * G0::RS + lr - 1, gc = lc - 1;
       bf16x8 v = {};
-      if (hr >= 1 && hr <= 32 && hc >= 1 && hc <= 32)
-        v = *reinterpret_cast<const bf16x8*>(src + ((hr - 1) * 32 + hc - 1) * 8);
+      if (gr >= 0 && gr < 32 && gc >= 0 && gc < 32)
+        v = *reinterpret_cast<const bf16x8*>(src + (gr * 32 + gc) * 8);
       *reinterpret_cast<bf16x8*>(x.m.ha + q * 8) = v;
     }
     constexpr int SKP = kpad_of(72);
@@ -744,19 +898,20 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
   bf16x4 xr[8];
   {
     f32x4 acc[8];
-    zero_acc<0>(acc);
-    conv_acc<0, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.wave, x.lane);
-    round_acc<0, false>(xr, acc, xr);
-    fwd_stats<0>(x, xr, B0.bn1, x.wave, x.lane);
-    store_regs<0>(xr, B0.x + (long)x.img * 1024 * 16, x.wave, x.lane, false);
-    fwd_arrive(x);
+    zero_acc(acc);
+    conv_acc<0, P, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, x.wave, x.lane);
+    round_acc<0, P, false>(xr, acc, xr);
+    publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
+    fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
+    grid_arrive(a.bar);
     const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
     WLoad LP{};
     if (B0.wpf) LP = wl_fwd(B0.wpf, 16, 16, 1);
     bf16x8 w1r[nreg(conv_units(16, 16, 3))], wpr[1];
     w_prefetch(L1, w1r);
     w_prefetch(LP, wpr);
-    if (!fwd_wait(x)) return;
+    bn_prefetch_fwd(a.bns[B0.bn1], 16, x.bnr);
+    if (!wait_fwd(x)) return;
     w_store(L1, w1r, x.m.w1);
     w_store(LP, wpr, x.m.w2);
   }
@@ -777,7 +932,7 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
       n1 = wl_fwd(Bn.w1f, 16 << so, 16 << si, 3);
       if (Bn.wpf) np = wl_fwd(Bn.wpf, 16 << so, 16 << si, 1);
     }
-    return block_fwd<S, STR, PROJ>(x, xr, bnx, n1, np, B);
+    return block_fwd<S, STR, PROJ, P>(x, xr, bnx, n1, np, B);
   };
   if (!run(BlkTag<0, 1, true>{}, 0)) return;
   for (int bi = 1; bi < nps; ++bi)
@@ -789,31 +944,68 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
   for (int bi = 2 * nps + 1; bi < 3 * nps; ++bi)
     if (!run(BlkTag<2, 1, false>{}, bi)) return;
 
-  // ---- head (head.hip head_fused numerics): final BN + ReLU + average pool, dense,
-  //      softmax cross-entropy row, dense dgrad, pool gradient, final BN backward sums
+  // ---- head (head.hip head_fused numerics): final BN + ReLU, the slice's average-pool
+  //      sums (fp64 atomics per image), one barrier; then slice 0 of each image: dense,
+  //      softmax cross-entropy row, dense dgrad, pool gradient ----
   probe(x, 200);
+  using G2 = Stg<2, P>;
   const int fb = 2 * a.nblocks;
   const int dunits = 64 * a.kpad / 8;
   bf16x8 dwv = {};
-  if (tid < dunits) dwv = *reinterpret_cast<const bf16x8*>(a.dense_w + tid * 8);
-  fwd_combine(x, fb, 64, (double)a.N * 64);
-  float* tbl = x.m.tbl;
-  // dense weights -> W1 as fp32 [64][kpad]
-  float* wd = reinterpret_cast<float*>(x.m.w1);
+  if (x.kslice == 0 && tid < dunits) dwv = *reinterpret_cast<const bf16x8*>(a.dense_w + tid * 8);
+  bn_fwd_table(a.bns[fb], x.bnr, 64, (double)a.N * 64, a.eps, a.momentum, a.update_moving, x.m.tbl);
+  const float* tbl = x.m.tbl;
+  {
+    const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
+    if (wave_active<2, P>(wave)) {
+      float s[G2::CBW][4];
+#pragma unroll
+      for (int j = 0; j < G2::CBW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[j][r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < G2::TPW; ++t) {
+        int pb, cb;
+        tile_of<2, P>(wave, t, pb, cb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cb * 16 + 4 * (lane >> 4) + r;
+          s[t % G2::CBW][r] += fmaxf((float)xr[t][r] * tbl[c] + tbl[64 + c], 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < G2::CBW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[j][r] = row16_sum(s[j][r]);
+      if ((lane & 15) == 0) {
+        int pb, cb0;
+        tile_of<2, P>(wave, 0, pb, cb0);
+#pragma unroll
+        for (int j = 0; j < G2::CBW; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x.m.red[wave * 128 + (cb0 + j) * 16 + 4 * (lane >> 4) + r] = s[j][r];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int grp = (tid / 16) / G2::CBW;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if (w % G2::WPB == grp) v += x.m.red[w * 128 + tid];
+      unsafeAtomicAdd(a.pool_acc + (long)x.img * 64 + tid, (double)v);
+    }
+  }
+  grid_arrive(a.bar);
+  if (!wait_fwd(x)) return;
+  if (x.kslice != 0) return;
+  float* pool_s = x.m.tbl2;          // [0, 64) pooled, [64, 128) dp, [128, 192) g
+  float* wd = reinterpret_cast<float*>(x.m.w1);   // dense weights as fp32 [64][kpad]
   if (tid < dunits)
 #pragma unroll
     for (int j = 0; j < 8; ++j) wd[tid * 8 + j] = (float)dwv[j];
-  float* pool_s = x.m.tbl2;          // [0, 64) pooled, [64, 128) dp, [128, 192) g, [256, 384) sums
-  image_sums<2, false>([&](int t, int r, float& s1, float& s2) {
-    int pb, cb;
-    tile_of<2>(x.wave, t, pb, cb);
-    const int c = cb * 16 + 4 * (x.lane >> 4) + r;
-    s1 = fmaxf((float)xr[t][r] * tbl[c] + tbl[64 + c], 0.f);
-    s2 = 0.f;
-  }, x.m.red, pool_s + 256, x.wave, x.lane);
-  __syncthreads();
   if (tid < 64) {
-    const bf16 pb = (bf16)(pool_s[256 + tid] / 64.f);
+    const bf16 pb = (bf16)((float)ld_sc1_d(a.pool_acc + (long)x.img * 64 + tid) / 64.f);
     a.pooled[(long)x.img * 64 + tid] = pb;
     pool_s[tid] = (float)pb;
   }
@@ -861,22 +1053,16 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
     float d = 0.f;
     for (int k = 0; k < a.kpad; ++k) d += pool_s[128 + k] * wd[tid * a.kpad + k];
     const float db = (float)(bf16)d;
-    const float dp = (float)(bf16)(db * (1.f / 64.f));
-    pool_s[64 + tid] = dp;
-    a.dpool[(long)x.img * 64 + tid] = dp;
+    a.dpool[(long)x.img * 64 + tid] = (float)(bf16)(db * (1.f / 64.f));
   }
-  __syncthreads();
-  // final BN backward sums of g = dp * relu'(bn(x)) (consumed by the backward launch)
-  float* bslot = a.bslot + ((long)fb * a.N + x.img) * PRN_SLOT;
-  image_sums<2>([&](int t, int r, float& s1, float& s2) {
-    int pb, cb;
-    tile_of<2>(x.wave, t, pb, cb);
-    const int c = cb * 16 + 4 * (x.lane >> 4) + r;
-    const float xf = (float)xr[t][r];
-    const float gg = (xf * tbl[c] + tbl[64 + c] > 0.f) ? pool_s[64 + c] : 0.f;
-    s1 = gg;
-    s2 = gg * (xf - tbl[128 + c]) * tbl[192 + c];
-  }, x.m.red, bslot, x.wave, x.lane);
+}
+
+}  // namespace
+
+template <int P>
+__global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  prn_forward_body<P>(a, smem);
 }
 
 // =====================================================================================
@@ -884,47 +1070,33 @@ __global__ void __launch_bounds__(PT, 1) prn_fwd_kernel(PrnArgs a) {
 // =====================================================================================
 namespace {
 
-struct BwdCtx {
-  const PrnArgs* a;
-  Smem m;
-  int img, wave, lane;
-  unsigned nbar;
-  int pc;
-};
-
-__device__ __forceinline__ void bwd_arrive(BwdCtx& x) { grid_arrive(x.a->bar + 1, true); }
-__device__ __forceinline__ bool bwd_wait(BwdCtx& x) {
-  ++x.nbar;
-  return grid_wait(x.a->bar + 1, x.nbar * (unsigned)x.a->N, x.a->err, x.m.flag);
-}
-
-// g = da * relu'(bn(xs)), xhat = (xs - mean) rstd with the forward table tb; sums -> slot
-template <int S>
-__device__ __forceinline__ void bwd_sums(BwdCtx& x, const bf16x4 (&da)[8], const bf16x4 (&xs)[8],
+// sums of g = da [xs*scale+shift > 0] and g * xhat with the forward table tb
+template <int S, int P>
+__device__ __forceinline__ void bwd_sums(Ctx& x, const bf16x4 (&da)[8], const bf16x4 (&xs)[8],
                                          const float* tb, int bi, int wave, int lane) {
   lane = opaque_v(lane);
-  float* slot = x.a->bslot + ((long)bi * x.a->N + x.img) * PRN_SLOT;
-  image_sums<S>([&](int t, int r, float& s1, float& s2) {
+  bn_sums<S, P>([&](int t, int r, float& s1, float& s2) {
     int pb, cb;
-    tile_of<S>(wave, t, pb, cb);
+    tile_of<S, P>(wave, t, pb, cb);
     const int c = cb * 16 + 4 * (lane >> 4) + r;
     const float xf = (float)xs[t][r];
     const float gg = (xf * tb[c] + tb[64 + c] > 0.f) ? (float)da[t][r] : 0.f;
     s1 = gg;
     s2 = gg * (xf - tb[128 + c]) * tb[192 + c];
-  }, x.m.red, slot, wave, lane);
+  }, x.m.red, x.a->bns[bi].bacc, wave, lane);
 }
 
 // dh = a g - b - c xhat (+ add) with the backward coefficient table cf
-template <int S, bool ADD>
+template <int S, int P, bool ADD>
 __device__ __forceinline__ void bwd_apply(bf16x4 (&out)[8], const bf16x4 (&da)[8],
                                           const bf16x4 (&xs)[8], const bf16x4 (&add)[8],
                                           const float* cf, int wave, int lane) {
   lane = opaque_v(lane);
+  if (!wave_active<S, P>(wave)) return;
 #pragma unroll
-  for (int t = 0; t < Stg<S>::TPW; ++t) {
+  for (int t = 0; t < Stg<S, P>::TPW; ++t) {
     int pb, cb;
-    tile_of<S>(wave, t, pb, cb);
+    tile_of<S, P>(wave, t, pb, cb);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = cb * 16 + 4 * (lane >> 4) + r;
@@ -938,42 +1110,74 @@ __device__ __forceinline__ void bwd_apply(bf16x4 (&out)[8], const bf16x4 (&da)[8
   }
 }
 
-__device__ __forceinline__ void bwd_combine(BwdCtx& x, int bi, int C, float M) {
-  const PrnArgs& a = *x.a;
-  combine_slots(a.bslot + (long)bi * a.N * PRN_SLOT, a.N, x.m.dred, x.m.dsum);
-  bn_bwd_table(a.bns[bi], x.m.dsum, C, M, x.img == 0, x.m.tbl2);
+// The halo of a BN-backward output (stage S) for the next dgrad: own values from
+// registers; the neighbour rows recomputed here from what the neighbours published
+// before the barrier -- da (their dgrad output; nullptr: the per-channel constant dpc,
+// the pooled head's gradient), the BN input xsrc (saved by the forward) and the residual
+// gradient add (nullptr: none) -- with the coefficient table cf.  The loads are issued
+// (bwd_nbr_issue) right after the barrier wait, before the BN-backward combine, so the
+// two round trips overlap.
+struct NbrBwd {
+  bf16x8 dv, xv, av;
+};
+template <int S, int P>
+__device__ __forceinline__ void bwd_nbr_issue(const Nbr<S, P>& nb, const bf16* da,
+                                              const bf16* xsrc, const bf16* add, NbrBwd& q) {
+  if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok) {
+    q.dv = da ? ld_sc1_b128(da, nb.gofs) : bf16x8{};
+    q.xv = *reinterpret_cast<const bf16x8*>(xsrc + nb.gofs);
+    q.av = add ? ld_sc1_b128(add, nb.gofs) : bf16x8{};
+  }
+}
+template <int S, int P>
+__device__ __forceinline__ void bwd_halo(Ctx& x, bf16* hal, const bf16x4 (&own)[8],
+                                         const Nbr<S, P>& nb, NbrBwd& q, const float* dpc,
+                                         bool has_add, const float* cf, int wave, int lane) {
+  bf16x8 nv = {};
+  if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok) {
+    if (dpc) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q.dv[j] = (bf16)dpc[nb.u * 8 + j];
+    }
+    nv = bwd8(q.dv, q.xv, q.av, has_add, cf, nb.u * 8);
+  }
+  to_halo<S, P, 0>(hal, own, nullptr, nullptr, nb, nv, x.kslice, wave, lane);
 }
 
-// One block's backward: dout (stage S) in, dx (input stage) out (in `dout`).  On entry
-// W1 holds conv2's dgrad weights; on exit the previous block's (`next_w2`).
-template <int S, int STR, bool PROJ>
-__device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WLoad& next_w2,
+// One block's backward: dout (stage S) in registers and its halo in HB, the saved BN2
+// input `hs` in registers, conv2's dgrad weights in W1, BN2's forward table in x.ftr;
+// out: dx (input stage) in `dout`, its halo in HB, and for the previous block `Bn`
+// (nullptr: none) its conv2 dgrad weights (`next_w2`) in W1, its BN2 input in `hs`, its
+// BN2 forward table in x.ftr.  Every global load on the critical path is issued a phase
+// ahead (before a barrier wait, or before the halo work).
+template <int S, int STR, bool PROJ, int P>
+__device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs)[8],
+                                          const WLoad& next_w2, const PrnBlock* Bn,
                                           const PrnBlock& B) {
   constexpr int SI = STR == 2 ? S - 1 : S;
-  using GI = Stg<SI>;
-  using G = Stg<S>;
+  using GI = Stg<SI, P>;
+  using G = Stg<S, P>;
   const PrnArgs& a = *x.a;
   const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
   const long img_o = (long)x.img * G::R * G::R * G::C;
   const long img_i = (long)x.img * GI::R * GI::R * GI::C;
   probe(x, 100 + S);
-  bf16x4 hs[8], xs[8];
-  load_regs<S>(hs, B.h1 + img_o, wave, lane);     // BN2 input (saved by the forward)
-  load_regs<SI>(xs, B.x + img_i, wave, lane);     // BN1 input
-  bn_load_table(a.bns[B.bn2], G::C, x.m.tbl);
-  // publish dout (conv2 / projection weight gradients), stage it for conv2's dgrad
-  store_regs<S>(dout, B.dout + img_o, wave, lane, true);
-  to_halo<S, false>(x.m.hb, dout, nullptr, nullptr, wave, lane);
+  bf16x4 xs[8];
+  load_regs<SI, P>(xs, B.x + img_i, x.kslice, wave, lane);     // BN1 input (used after a barrier)
+  tab_store(x.ftr, G::C, x.m.tbl);
+  publish<S, P>(dout, B.dout + img_o, x.kslice, wave, lane);   // conv2 / projection wgrads
   __syncthreads();
+  probe(x, 1);
   f32x4 acc[8];
-  zero_acc<S>(acc);
-  conv_acc<S, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, wave, lane);
+  zero_acc(acc);
+  conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, x.kslice, wave, lane);
   bf16x4 da[8];
-  round_acc<S, false>(da, acc, da);
+  round_acc<S, P, false>(da, acc, da);
   probe(x, 3);
-  bwd_sums<S>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
+  publish<S, P>(da, B.da2 + img_o, x.kslice, wave, lane);
+  bwd_sums<S, P>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
   probe(x, 4);
-  bwd_arrive(x);
+  grid_arrive(a.bar + 1);
   probe(x, 5);
   {
     const WLoad L1 = wl_dgrad(B.w1b, G::C, GI::C, 3);
@@ -982,42 +1186,55 @@ __device__ __forceinline__ bool block_bwd(BwdCtx& x, bf16x4 (&dout)[8], const WL
     bf16x8 w1r[nreg(conv_units(G::C, GI::C, 3))], wpr[1];
     w_prefetch(L1, w1r);
     w_prefetch(LP, wpr);
-    if (!bwd_wait(x)) return false;
+    bn_prefetch_bwd(a.bns[B.bn2], G::C, x.bnr);
+    bn_prefetch_tab(a.bns[B.bn1], GI::C, x.ftr);
+    if (!wait_bwd(x)) return false;
     probe(x, 6);
-    bwd_combine(x, B.bn2, G::C, (float)a.N * G::R * G::R);
-    probe(x, 7);
+    const Nbr<S, P> nb(x.kslice);
+    NbrBwd q;
+    bwd_nbr_issue<S, P>(nb, B.da2 + img_o, B.h1 + img_o, nullptr, q);
+    bn_bwd_table(a.bns[B.bn2], x.bnr, G::C, (float)a.N * G::R * G::R, x.m.tbl2);
     bf16x4 dh[8];
-    bwd_apply<S, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
-    store_regs<S>(dh, B.dh1 + img_o, wave, lane, true);
-    to_halo<S, false>(x.m.ha, dh, nullptr, nullptr, wave, lane);
-    bn_load_table(a.bns[B.bn1], GI::C, x.m.tbl);
+    bwd_apply<S, P, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
+    publish<S, P>(dh, B.dh1 + img_o, x.kslice, wave, lane);    // conv1 weight gradient
+    bwd_halo<S, P>(x, x.m.ha, dh, nb, q, nullptr, false, x.m.tbl2, wave, lane);
+    tab_store(x.ftr, GI::C, x.m.tbl);
     w_store(L1, w1r, x.m.w1);
     w_store(LP, wpr, x.m.w2);
   }
   __syncthreads();
   probe(x, 8);
-  zero_acc<SI>(acc);
+  zero_acc(acc);
   if constexpr (STR == 2) {
-    dgrad_s2_acc<SI, G::C, false>(acc, x.m.ha, x.m.w1, wave, lane);
-    dgrad_s2_acc<SI, G::C, true>(acc, x.m.hb, x.m.w2, wave, lane);
+    dgrad_s2_acc<SI, P, G::C, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+    dgrad_s2_acc<SI, P, G::C, true>(acc, x.m.hb, x.m.w2, x.kslice, wave, lane);
   } else {
-    conv_acc<S, G::C, 3, 1, true>(acc, x.m.ha, x.m.w1, wave, lane);
-    if constexpr (PROJ) conv_acc<S, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, wave, lane);
+    conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+    if constexpr (PROJ) conv_acc<S, P, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, x.kslice, wave, lane);
   }
-  round_acc<SI, false>(da, acc, da);
+  round_acc<SI, P, false>(da, acc, da);
   probe(x, 9);
-  bwd_sums<SI>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
+  publish<SI, P>(da, B.da1 + img_i, x.kslice, wave, lane);
+  bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
-  bwd_arrive(x);
+  grid_arrive(a.bar + 1);
   probe(x, 11);
   bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
   w_prefetch(next_w2, w2r);
-  if (!bwd_wait(x)) return false;
+  bn_prefetch_bwd(a.bns[B.bn1], GI::C, x.bnr);
+  if (Bn) bn_prefetch_tab(a.bns[Bn->bn2], GI::C, x.ftr);
+  if (!wait_bwd(x)) return false;
   probe(x, 12);
-  bwd_combine(x, B.bn1, GI::C, (float)a.N * GI::R * GI::R);
-  probe(x, 13);
-  if constexpr (PROJ) bwd_apply<SI, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
-  else bwd_apply<SI, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  const Nbr<SI, P> nb(x.kslice);
+  NbrBwd q;
+  bwd_nbr_issue<SI, P>(nb, B.da1 + img_i, B.x + img_i, PROJ ? nullptr : B.dout + img_o, q);
+  bn_bwd_table(a.bns[B.bn1], x.bnr, GI::C, (float)a.N * GI::R * GI::R, x.m.tbl2);
+  if constexpr (PROJ) bwd_apply<SI, P, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  else bwd_apply<SI, P, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  if (Bn) load_regs<SI, P>(hs, Bn->h1 + img_i, x.kslice, wave, lane);   // previous block's BN2 input
+  // the halo of dx for the previous block's conv2 dgrad (its neighbour rows: this block's
+  // published da1, the saved block input, and -- identity blocks -- the published dout)
+  bwd_halo<SI, P>(x, x.m.hb, dout, nb, q, nullptr, !PROJ, x.m.tbl2, wave, lane);
   w_store(next_w2, w2r, x.m.w1);   // visible after the next block's first __syncthreads
   return true;
 }
@@ -1148,29 +1365,34 @@ __device__ __forceinline__ void run_item(const PrnItem& it, char* smem, int wave
   }
 }
 
+
 }  // namespace
 
+template <int P>
 __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  if ((int)blockIdx.x >= a.N) {
+  const int nsl = a.N * P;
+  if ((int)blockIdx.x >= nsl) {
     // ---- weight-gradient role: items w, w + W, ... in readiness order ----
-    const int w = blockIdx.x - a.N, W = gridDim.x - a.N;
+    const int w = blockIdx.x - nsl, W = gridDim.x - nsl;
     int* flag = reinterpret_cast<int*>(smem + OFF_MISC);
     for (int i = w; i < a.nitems; i += W) {
       const PrnItem& it = a.items[i];
-      if (!grid_wait(a.bar + 1, (unsigned)it.ready * (unsigned)a.N, a.err, flag)) return;
+      if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
       run_item(it, smem, wave, lane);
     }
     return;
   }
-  BwdCtx x;
+  Ctx x;
   x.a = &a;
   x.m = carve(smem);
-  x.img = blockIdx.x;
+  x.img = blockIdx.x / P;
+  x.kslice = blockIdx.x % P;
   x.wave = wave;
   x.lane = lane;
   x.nbar = 0;
+  x.slices = (unsigned)nsl;
   x.pc = 0;
   probe(x, 0);
   const int nb = a.nblocks;
@@ -1181,26 +1403,39 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     w_prefetch(L, r);
     w_store(L, r, x.m.w1);
   }
-  // ---- final BN backward: dXL = a g - b - c xhat, g = dpool * relu'(bn(XL)) ----
-  using G2 = Stg<2>;
-  bf16x4 dout[8];
+  // ---- final BN backward: sums of g = dpool * relu'(bn(XL)), one barrier, then
+  //      dXL = a g - b - c xhat and its halo ----
+  using G2 = Stg<2, P>;
+  bf16x4 dout[8], hs[8];
   {
     const int fb = 2 * nb;
+    const long img_o = (long)x.img * 64 * 64;
     bf16x4 xs[8];
-    load_regs<2>(xs, BL.out + (long)x.img * 64 * 64, wave, lane);
-    bf16x4 dp[8];
-    float* dps = x.m.tbl;   // dpool row
+    load_regs<2, P>(xs, BL.out + img_o, x.kslice, wave, lane);
+    float* dps = x.m.tbl + 256;   // this image's dpool row
+    bn_load_table(a.bns[fb], 64, x.m.tbl);
     if (tid < 64) dps[tid] = a.dpool[(long)x.img * 64 + tid];
     __syncthreads();
+    bf16x4 dp[8];
 #pragma unroll
     for (int t = 0; t < G2::TPW; ++t) {
       int pb, cb;
-      tile_of<2>(wave, t, pb, cb);
+      tile_of<2, P>(wave, t, pb, cb);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dp[t][r] = (bf16)dps[cb * 16 + 4 * (lane >> 4) + r];
+      for (int r = 0; r < 4; ++r) dp[t][r] = (bf16)dps[(cb * 16 + 4 * (lane >> 4) + r) & 63];
     }
-    bwd_combine(x, fb, 64, (float)a.N * 64);
-    bwd_apply<2, false>(dout, dp, xs, dout, x.m.tbl2, wave, lane);
+    bwd_sums<2, P>(x, dp, xs, x.m.tbl, fb, wave, lane);
+    grid_arrive(a.bar + 1);
+    bn_prefetch_bwd(a.bns[fb], 64, x.bnr);
+    bn_prefetch_tab(a.bns[BL.bn2], 64, x.ftr);
+    if (!wait_bwd(x)) return;
+    const Nbr<2, P> nb(x.kslice);
+    NbrBwd q;
+    bwd_nbr_issue<2, P>(nb, nullptr, BL.out + img_o, nullptr, q);
+    bn_bwd_table(a.bns[fb], x.bnr, 64, (float)a.N * 64, x.m.tbl2);
+    bwd_apply<2, P, false>(dout, dp, xs, dout, x.m.tbl2, wave, lane);
+    load_regs<2, P>(hs, BL.h1 + img_o, x.kslice, wave, lane);
+    bwd_halo<2, P>(x, x.m.hb, dout, nb, q, dps, false, x.m.tbl2, wave, lane);
   }
   // ---- blocks, last to first (straight-line stages, as in the forward) ----
   const int nps = nb / 3;
@@ -1208,11 +1443,9 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     constexpr int S = decltype(tag)::S, STR = decltype(tag)::STR;
     constexpr bool PROJ = decltype(tag)::PROJ;
     WLoad n2{};
-    if (bi > 0) {
-      const PrnBlock& Bp = a.blocks[bi - 1];
-      n2 = wl_dgrad(Bp.w2b, 16 << Bp.stage, 16 << Bp.stage, 3);
-    }
-    return block_bwd<S, STR, PROJ>(x, dout, n2, a.blocks[bi]);
+    const PrnBlock* Bp = bi > 0 ? &a.blocks[bi - 1] : nullptr;
+    if (Bp) n2 = wl_dgrad(Bp->w2b, 16 << Bp->stage, 16 << Bp->stage, 3);
+    return block_bwd<S, STR, PROJ, P>(x, dout, hs, n2, Bp, a.blocks[bi]);
   };
   for (int bi = nb - 1; bi > 2 * nps; --bi)
     if (!run(BlkTag<2, 1, false>{}, bi)) return;
@@ -1225,10 +1458,9 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   if (!run(BlkTag<0, 1, true>{}, 0)) return;
   probe(x, 200);
   // ---- the stem output's gradient: published for the stem's weight gradient ----
-  store_regs<0>(dout, a.dx0 + (long)x.img * 1024 * 16, wave, lane, true);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(a.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  publish<0, P>(dout, a.dx0 + (long)x.img * 1024 * 16, x.kslice, wave, lane);
+  grid_arrive(a.bar + 1);
+  if (blockIdx.x == 0) wait_bwd(x);   // publishes the stem item's readiness
 }
 
 // ---- host ------------------------------------------------------------------------------
@@ -1237,9 +1469,9 @@ void prn_set_probe(long long* p) { g_prn_probe = p; }
 
 size_t prn_lds_bytes() { return LDS_TOTAL; }
 
-bool prn_supported(int N, int nblocks, int classes, int kpad) {
-  return N >= 1 && N <= 128 && nblocks >= 3 && nblocks % 3 == 0 && classes >= 1 &&
-         classes <= kpad && kpad <= 64 && kpad % 16 == 0;
+bool prn_supported(int N, int P, int nblocks, int classes, int kpad) {
+  return N >= 1 && (P == 2 || P == 4) && N * P <= 192 && nblocks >= 3 && nblocks % 3 == 0 &&
+         classes >= 1 && classes <= kpad && kpad <= 64 && kpad % 16 == 0;
 }
 
 int prn_item_kind(int cin, int cout, int ksize, int stride) {
@@ -1256,23 +1488,25 @@ static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS
               "weight-gradient LDS");
 
 void prn_forward(const PrnArgs& a, hipStream_t s) {
-  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad) || a.N > cu_count())
-    throw std::invalid_argument("prn_forward: unsupported shape (N <= CUs, 3n blocks, <= 64 classes)");
+  if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad) || a.N * a.P > cu_count())
+    throw std::invalid_argument("prn_forward: unsupported shape (N x P <= CUs, 3n blocks, <= 64 classes)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  hipLaunchKernelGGL(prn_fwd_kernel, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
+  if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
+  else hipLaunchKernelGGL(prn_fwd_kernel<4>, dim3(a.N * 4), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }
 
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
-  if (!prn_supported(a.N, a.nblocks, a.classes, a.kpad))
+  if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad))
     throw std::invalid_argument("prn_backward: unsupported shape");
-  const int grid = a.N + std::max(1, wgrad_wgs);
+  const int grid = a.N * a.P + std::max(1, wgrad_wgs);
   if (grid > cu_count())
     throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  hipLaunchKernelGGL(prn_bwd_kernel, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
+  if (a.P == 2) hipLaunchKernelGGL(prn_bwd_kernel<2>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
+  else hipLaunchKernelGGL(prn_bwd_kernel<4>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }
 

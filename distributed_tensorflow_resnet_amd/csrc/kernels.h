@@ -205,26 +205,30 @@ int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() pi
 // ---- Persistent small-batch CIFAR step (cifar_persist.hip) ----
 // The whole CIFAR ResNet v2 (6n+2, building blocks, 16/32/64 channels on 32/16/8 maps;
 // resnet_model_official.py:217-278) forward in ONE launch and its backward in ONE
-// launch: one 512-thread workgroup per image keeps the image's activations on-chip
-// (registers + LDS halos) across layers; grid barriers only where BatchNorm batch
-// statistics need the whole batch.  In the backward launch the remaining CUs compute
-// the weight gradients (per image group, fp32 slabs for the grouped reduce) as soon
-// as the image workgroups have published each layer's output gradient.
+// launch.  Each image is split into P row slices, one 512-thread workgroup per slice,
+// that keep their activations on-chip across layers; the two halo rows a 3x3 conv needs
+// from the neighbouring slices come from tensors the neighbours publish anyway (the
+// saved activations, the backward's gradients); grid barriers only where BatchNorm
+// needs batch statistics (exact fp64 atomic sums).  In the backward launch the
+// remaining CUs compute the weight gradients (per image group, fp32 slabs for the
+// grouped reduce) as soon as the slices have published each layer's output gradient.
 struct PrnBn {               // one BatchNorm (all device pointers)
   const float* gamma;
   const float* beta;
-  float* mmean;              // moving statistics (updated by image 0)
+  float* mmean;              // moving statistics (updated by workgroup 0)
   float* mvar;
-  float* mean;               // batch statistics (written by image 0)
+  float* mean;               // batch statistics (written by workgroup 0)
   float* rstd;
   float* scale;
   float* shift;
-  float* dgamma;             // gradients in the flat fp32 gradient buffer (image 0)
+  float* dgamma;             // gradients in the flat fp32 gradient buffer (workgroup 0)
   float* dbeta;
+  double* acc;               // [BN_ACC_REP][2][C] forward sums (sum y, sum y^2), zeroed per step
+  double* bacc;              // [BN_ACC_REP][2][C] backward sums (sum g, sum g xhat)
 };
 struct PrnBlock {            // one building block (resnet_model_official.py:94-130)
-  bf16* x;                   // block input [N][R_in][R_in][C_in], NHWC (saved)
-  bf16* h1;                  // conv1 output [N][R][R][C] (saved)
+  bf16* x;                   // block input [N][R_in][R_in][C_in], NHWC (saved, published)
+  bf16* h1;                  // conv1 output [N][R][R][C] (saved, published)
   bf16* out;                 // block output (the next block's x)
   const bf16* w1f;           // forward weights, OHWI [co][kh][kw][ci]
   const bf16* w2f;
@@ -232,31 +236,33 @@ struct PrnBlock {            // one building block (resnet_model_official.py:94-
   const bf16* w1b;           // dgrad weights, HWIO [kh][kw][ci][co]
   const bf16* w2b;
   const bf16* wpb;
-  bf16* dout;                // backward: gradient of `out` (published for the weight gradients)
-  bf16* dh1;                 // backward: gradient of h1 (after BN2's backward)
+  bf16* dout;                // backward: gradient of `out` (published)
+  bf16* dh1;                 // backward: gradient of h1 after BN2's backward (published)
+  bf16* da2;                 // backward: conv2's dgrad output, before BN2's backward (published)
+  bf16* da1;                 // backward: conv1's (+ projection's) dgrad output (published)
   int stage;                 // output stage 0..2 (32x32x16, 16x16x32, 8x8x64)
   int stride;                // 1 or 2 (the first block of stages 1 and 2)
   int bn1, bn2;              // PrnBn indices of the block's two BatchNorms
 };
 struct PrnItem {             // backward weight-gradient work item: one conv x one image group
-  const bf16* dy;            // [N][Ro][Ro][CO] output gradient (published by the image workgroups)
+  const bf16* dy;            // [N][Ro][Ro][CO] output gradient (published by the slices)
   const bf16* x;             // [N][Ri][Ri][CI] conv input before its BatchNorm (stem: the image)
   const float* scale;        // BN+ReLU of x (nullptr: none -- the stem)
   const float* shift;
   float* part;               // [CO][taps*CI] fp32 slab of this image group
   int kind;                  // conv shape class (prn_item_kind)
   int img0, nimg;
-  int ready;                 // backward barrier arrivals (x images) after which dy is complete
+  int ready;                 // backward barrier arrivals (x slices) after which dy is complete
 };
 struct PrnArgs {
   const PrnBlock* blocks;
   int nblocks;
-  const PrnBn* bns;          // [2 * nblocks + 1]: block i's BNs at 2i, 2i+1; the final BN last
+  const PrnBn* bns;          // [2 * nblocks + 1]: block i's BNs at 2i, 2i + 1; the final BN last
   const bf16* x_in;          // [N][32][32][8] input images (channels 3..7 zero)
   const bf16* stem_w;        // OHWI [16][3][3][8]
-  float* fslot;              // [2 * nblocks + 1][N][128] forward BN partial sums (sum, sum sq)
-  float* bslot;              // [2 * nblocks + 1][N][128] backward BN partial sums (sum g, sum g xhat)
-  unsigned* bar;             // [2] barrier counters (forward, backward), zeroed every step
+  double* pool_acc;          // [N][64] fp64 average-pool sums (zeroed every step)
+  unsigned* bar;             // [128]: barrier counters (forward, backward) at 0, 1; the backward
+                             // readiness count at 64 -- zeroed every step
   int* err;                  // set when a barrier wait times out
   const bf16* dense_w;       // [64][kpad] bf16 HWIO
   const float* dense_b;
@@ -268,15 +274,15 @@ struct PrnArgs {
   bf16* dx0;                 // backward: gradient of the stem output [N][32][32][16]
   const PrnItem* items;      // backward weight-gradient items, in readiness order
   int nitems;
-  int N, classes, kpad;
+  int N, P, classes, kpad;   // P: row slices (workgroups) per image
   float grad_scale;          // 1 / global batch
   float momentum, eps;
   int update_moving;
-  long long* probe = nullptr;   // diagnostics: image 0's (tag, wall clock) phase stamps
+  long long* probe = nullptr;   // diagnostics: workgroup 0's (tag, wall clock) phase stamps
 };
-enum { PRN_THREADS = 512, PRN_SLOT = 128 };
+enum { PRN_THREADS = 512 };
 void prn_set_probe(long long* p);   // diagnostics (scripts/prn_probe.py); nullptr = off
-bool prn_supported(int N, int nblocks, int classes, int kpad);
+bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
 void prn_forward(const PrnArgs& a, hipStream_t s);
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);

@@ -255,6 +255,7 @@ class Engine:
         # batch <= 32 on a supported CIFAR network, 0 off, 1 whenever supported)
         from . import persist as _persist
         pm = tune.get("persist")
+        self.persist_slices = tune.get("persist_slices")
         ok = pm != 0 and _persist.supported(self)
         self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
         self.prn = _persist.PersistStep(self) if self.persist else None
@@ -474,10 +475,13 @@ class Engine:
         self.bn_acc_on = self.bn_bacc_on = bool(tune.get("bn_acc"))
         rep = self.nat.bn_acc_rep()
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
-        # (+ 2 doubles: the persistent step's two barrier counters, zeroed with the
-        # accumulators at the start of every step -- train/persist.py)
-        self.bn_acc = torch.zeros(max(_ceil(tot, 2) * 2, 2) + 2, dtype=torch.float64, device=dev)
-        self.prn_bar = self.bn_acc.data_ptr() + 8 * (self.bn_acc.numel() - 2)
+        # (+ N x 64 doubles and 64 more: the persistent step's average-pool sums and its
+        # barrier counters / readiness line, zeroed with the accumulators at the start of
+        # every step -- train/persist.py)
+        base = max(_ceil(tot, 2) * 2, 2)
+        self.bn_acc = torch.zeros(base + 64 * N + 64, dtype=torch.float64, device=dev)
+        self.prn_pool = self.bn_acc.data_ptr() + 8 * base
+        self.prn_bar = self.bn_acc.data_ptr() + 8 * (base + 64 * N)
         off = 0
         for b in self.bns.values():
             n = 2 * rep * b.spec.channels
@@ -1286,7 +1290,7 @@ class Engine:
         self._head_fused = False
         b0 = plan.size()
         self._t_fwd0 = plan.timing_point("fwd_begin")
-        # BN accumulators + the two barrier counters start every step at zero
+        # BN accumulators, the pool sums and the two barrier counters start every step at zero
         zero = (self.bn_acc.data_ptr(), self.bn_acc.numel() * 8)
         if self.input_mode == "cifar_u8":
             plan.cifar_augment(self.img_u8.data_ptr(), self.x_in.data_ptr(), N, spec.image_h,
@@ -1294,7 +1298,7 @@ class Engine:
                                self.gstep.data_ptr(), 1, 0, *zero)
         else:
             plan.memset(*zero)
-        ptrs, ints, floats = self.prn.args(self.prn_bar, BN_DECAY, BN_EPS)
+        ptrs, ints, floats = self.prn.args(self.prn_pool, self.prn_bar, BN_DECAY, BN_EPS)
         plan.prn(0, ptrs, ints, floats)
         self.seg["fwd"] = (b0, plan.size())
 

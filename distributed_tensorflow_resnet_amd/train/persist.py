@@ -4,9 +4,11 @@ At the per-rank batches of the strong-scaling headline config (global batch 128 
 4-8 GPUs = 16-32 images per rank; reference README.md:16-22, resnet_cifar_main.py:326-340)
 the launch-per-layer step is a chain of ~110 dependent kernel boundaries.  This path
 runs the CIFAR ResNet v2 (resnet_model_official.py:217-278) forward as ONE launch and
-its backward as ONE launch: one 512-thread workgroup per image keeps the image's
-activations on-chip across layers, grid barriers only where BatchNorm needs batch
-statistics, and the CUs beyond the images compute the weight gradients (fp32 slabs per
+its backward as ONE launch: each image is cut into P row slices and one 512-thread
+workgroup per slice keeps the slice's activations on-chip across layers (the one halo row
+a 3x3 conv needs from each neighbouring slice comes from the tensors the neighbour
+publishes anyway), grid barriers only where BatchNorm needs batch statistics (exact fp64
+atomic sums), and the CUs beyond the slices compute the weight gradients (fp32 slabs per
 image group) while the backward's dgrad chain continues.  The step is then:
 
     [augment] -> prn forward -> (side: softmax-xent batch folds, dense wgrad)
@@ -23,14 +25,23 @@ import numpy as np
 import torch
 
 PRN_BN = np.dtype([(k, "<u8") for k in ("gamma", "beta", "mmean", "mvar", "mean", "rstd",
-                                        "scale", "shift", "dgamma", "dbeta")])
+                                        "scale", "shift", "dgamma", "dbeta", "acc", "bacc")])
 PRN_BLOCK = np.dtype([(k, "<u8") for k in ("x", "h1", "out", "w1f", "w2f", "wpf", "w1b", "w2b",
-                                           "wpb", "dout", "dh1")] +
+                                           "wpb", "dout", "dh1", "da2", "da1")] +
                      [(k, "<i4") for k in ("stage", "stride", "bn1", "bn2")])
 PRN_ITEM = np.dtype([(k, "<u8") for k in ("dy", "x", "scale", "shift", "part")] +
                     [(k, "<i4") for k in ("kind", "img0", "nimg", "ready")])
-SLOT = 128          # floats per (BatchNorm, image) partial-sum slot
 AUTO_MAX_BATCH = 32
+
+
+def slices_for(N: int, cus: int, override: int = -1) -> int:
+    """Row slices (workgroups) per image: 4 up to 16 images, else 2 (MI355X, CIFAR RN50:
+    bs16 0.815 ms at 4 vs 0.840 at 2; bs32 0.993 at 4 vs 0.977 at 2 -- the barrier
+    latency grows with the number of arrivals).  The engine's tune persist_slices
+    overrides."""
+    if override in (2, 4):
+        return override
+    return 4 if N <= 16 and 4 * N + 32 <= cus else 2
 
 
 def supported(eng) -> bool:
@@ -55,7 +66,8 @@ def supported(eng) -> bool:
         if (b.proj is not None) != first or b.stride != (2 if first and stage else 1):
             return False
     cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
-    return eng.N < cus and bool(nat.prn_supported(eng.N, nb, spec.num_classes, eng.kpad))
+    P = slices_for(eng.N, cus, eng.persist_slices)
+    return eng.N * P < cus and bool(nat.prn_supported(eng.N, P, nb, spec.num_classes, eng.kpad))
 
 
 def _stage(b) -> int:
@@ -82,16 +94,20 @@ class PersistStep:
             r["mean"], r["rstd"] = e.mean.data_ptr(), e.rstd.data_ptr()
             r["scale"], r["shift"] = e.scale.data_ptr(), e.shift.data_ptr()
             r["dgamma"], r["dbeta"] = e.dgamma, e.dbeta
+            r["acc"], r["bacc"] = e.acc.data_ptr(), e.bacc.data_ptr()
         self.bn_dev = self._dev(bn_rows)
-        nbn = len(order)
-        self.fslot = torch.zeros(nbn * N * SLOT, device=dev)
-        self.bslot = torch.zeros(nbn * N * SLOT, device=dev)
+        self.cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.P = slices_for(N, self.cus, eng.persist_slices)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.dpool = torch.zeros((N, 64), device=dev)
         self.dx0 = torch.empty_like(eng.X[0])
         # per-block backward gradients published to the weight-gradient workgroups
         self.dout = [torch.empty_like(eng.X[i + 1]) for i in range(nb)]
         self.dh1 = [torch.empty_like(eng.H1[i]) for i in range(nb)]
+        # dgrad outputs before their BN backward: the neighbouring slices recompute their
+        # halo rows of the BN-backward output from these
+        self.da2 = [torch.empty_like(eng.H1[i]) for i in range(nb)]
+        self.da1 = [torch.empty_like(eng.X[i]) for i in range(nb)]
         rows = np.zeros(nb, dtype=PRN_BLOCK)
         for i, (r, b) in enumerate(zip(rows, blocks)):
             c1, c2 = eng.convs[b.convs[0].name], eng.convs[b.convs[1].name]
@@ -102,6 +118,7 @@ class PersistStep:
                 cp = eng.convs[b.proj.name]
                 r["wpf"], r["wpb"] = cp.ohwi, cp.hwio
             r["dout"], r["dh1"] = self.dout[i].data_ptr(), self.dh1[i].data_ptr()
+            r["da2"], r["da1"] = self.da2[i].data_ptr(), self.da1[i].data_ptr()
             r["stage"], r["stride"] = _stage(b), b.stride
             r["bn1"], r["bn2"] = 2 * i, 2 * i + 1
         self.block_dev = self._dev(rows)
@@ -111,15 +128,18 @@ class PersistStep:
         return torch.from_numpy(arr.view(np.uint8).copy()).to(self.eng.device)
 
     def _build_items(self):
-        """Weight-gradient work items in the order the backward publishes their dy:
-        per block (last first) conv2 and the projection after the block's first
-        backward barrier, conv1 after its second; the stem after the final arrive.
-        Images are grouped (<= 16 groups: the grouped reduce reads one slab per group)."""
+        """Weight-gradient work items in the order the backward publishes their dy
+        (`ready` = backward barrier count after which it is visible; barrier 1 is the
+        final BN): per block j (last block first) conv2 and the projection with the
+        block's dout at 2j + 2, conv1 with dh1 at 2j + 3; the stem after the final arrive.
+        Images are grouped 4 ways (the grouped reduce reads one slab per group): the items
+        of the first blocks only become ready at the end of the backward, and a quarter of
+        the batch per workgroup shortens that tail 4x for a 4-slab reduce."""
         eng, spec, N = self.eng, self.eng.spec, self.eng.N
         nat = eng.nat
         blocks = spec.blocks
         nb = len(blocks)
-        self.group = max(1, math.ceil(N / 16))
+        self.group = max(1, math.ceil(N / 4))
         groups = [(g0, min(self.group, N - g0)) for g0 in range(0, N, self.group)]
         self.splits = len(groups)
         convs = []   # (name, dy, x, bn scale, bn shift, ready)
@@ -127,11 +147,11 @@ class PersistStep:
             b = blocks[i]
             bn1, bn2 = eng.bns[b.bns[0].name], eng.bns[b.bns[1].name]
             d_out, d_h1 = self.dout[i].data_ptr(), self.dh1[i].data_ptr()
-            convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 1))
+            convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 2))
             if b.proj is not None:
-                convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 1))
-            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 2))
-        convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 1))
+                convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 2))
+            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 3))
+        convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 2))
         tot = 0
         self.part_off = {}
         for name, *_ in convs:
@@ -157,8 +177,7 @@ class PersistStep:
                 items.append(r)
         self.items = np.array(items, dtype=PRN_ITEM)
         self.item_dev = self._dev(self.items)
-        cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
-        self.wgrad_wgs = max(1, min(cus - N, len(items)))
+        self.wgrad_wgs = max(1, min(self.cus - N * self.P, len(items)))
         self.convs = [c[0] for c in convs]
 
     def pending(self):
@@ -172,15 +191,15 @@ class PersistStep:
                            s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         return out
 
-    def args(self, bar_ptr: int, bn_decay: float, bn_eps: float):
+    def args(self, pool_ptr: int, bar_ptr: int, bn_decay: float, bn_eps: float):
         eng, spec = self.eng, self.eng.spec
         ptrs = [self.block_dev.data_ptr(), self.bn_dev.data_ptr(), eng.x_in.data_ptr(),
-                eng.convs[spec.stem.name].ohwi, self.fslot.data_ptr(), self.bslot.data_ptr(),
+                eng.convs[spec.stem.name].ohwi, pool_ptr,
                 bar_ptr, self.err.data_ptr(), eng.dense_hwio, eng.dense_bias,
                 eng.labels.data_ptr(), eng.pooled.data_ptr(), eng.dlogits.data_ptr(),
                 eng.xent_ws.data_ptr(), self.dpool.data_ptr(), self.dx0.data_ptr(),
                 self.item_dev.data_ptr()]
-        ints = [self.nblocks, len(self.items), eng.N, spec.num_classes, eng.kpad, 1,
+        ints = [self.nblocks, len(self.items), eng.N, self.P, spec.num_classes, eng.kpad, 1,
                 self.wgrad_wgs]
         floats = [1.0 / eng.global_batch, bn_decay, bn_eps]
         return ptrs, ints, floats
