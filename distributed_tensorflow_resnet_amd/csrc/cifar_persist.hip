@@ -111,19 +111,79 @@ __device__ __forceinline__ int haddr(int pix, int lc, int c) {
   return (pix * U + ((c >> 3) ^ (lc & (U - 1)))) * 8 + (c & 7);
 }
 
+// Descriptor tables (blocks, BatchNorms, weight-gradient items) are read-only for the
+// whole launch: read them through the constant address space, i.e. scalar loads into
+// SGPRs via the scalar cache.  Through a generic pointer the compiler issues vector
+// loads, waits a full memory round trip for each pointer it needs and then builds
+// buffer descriptors from VGPRs in readfirstlane loops.
+#define DTR_CONST_AS __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ T ld_const(const T* p) {
+#if __HIP_DEVICE_COMPILE__
+  return *(const DTR_CONST_AS T*)p;
+#else
+  return *p;   // (host pass: never called)
+#endif
+}
+
+// Global loads / stores through pointers read from the descriptor tables: the compiler
+// cannot infer their address space and emits flat instructions, which also count in
+// lgkmcnt -- every LDS barrier (s_waitcnt lgkmcnt(0)) after one then waits for a memory
+// round trip.  These casts make them global_load / global_store.
+template <typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+#if __HIP_DEVICE_COMPILE__
+  return *(const __attribute__((address_space(1))) T*)p;
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void stg(T* p, T v) {
+#if __HIP_DEVICE_COMPILE__
+  *(__attribute__((address_space(1))) T*)p = v;
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ bf16x8 lds16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 __device__ __forceinline__ double ld_sc1_d(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if __HIP_DEVICE_COMPILE__
+  return __hip_atomic_load((const __attribute__((address_space(1))) double*)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return *p;
+#endif
 }
-// 8-byte write-through store of 4 bf16 / 16-byte sc1 load (buffer ops with the sc1 bit)
+// memory-side fp64 add (global_atomic_add_f64, no return)
+__device__ __forceinline__ void atomic_add_g(double* p, double v) {
+#if __HIP_DEVICE_COMPILE__
+  __builtin_amdgcn_global_atomic_fadd_f64((__attribute__((address_space(1))) double*)p, v);
+#else
+  *p += v;
+#endif
+}
+// a wave-uniform pointer, stated as such (SGPRs): a buffer descriptor built from VGPRs
+// costs a readfirstlane waterfall loop around every buffer instruction
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
+
+// 8-byte write-through store of 4 bf16 / 16-byte sc1 load (buffer ops with the sc1 bit);
+// `base` is wave-uniform
 __device__ __forceinline__ void st_sc1_b64(bf16* base, long elem, bf16x4 v) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 16);
 }
 __device__ __forceinline__ bf16x8 ld_sc1_b128(const bf16* base, long elem) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(base), 0, 0x7fffffff,
-                                                    0x00020000);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(const_cast<bf16*>(base)), 0,
+                                                    0x7fffffff, 0x00020000);
   return __builtin_bit_cast(bf16x8, (u32x4)__builtin_amdgcn_raw_buffer_load_b128(rs, (int)(elem * 2), 0, 16));
 }
 
@@ -168,7 +228,7 @@ __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* e
     *flag = ok;
   }
   __syncthreads();
-  return *flag != 0;
+  return __builtin_amdgcn_readfirstlane(*flag) != 0;   // uniform: no divergent region after
 }
 
 // ---- weights: global -> registers (waves 1-7) -> LDS -----------------------------------
@@ -195,7 +255,7 @@ __device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
       } else {
         off = (long)row * L.K + j * 8;
       }
-      r[i] = *reinterpret_cast<const bf16x8*>(L.src + off);
+      r[i] = ldg(reinterpret_cast<const bf16x8*>(L.src + off));
     }
   }
 }
@@ -365,7 +425,7 @@ __device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, 
   if (!wave_active<S, P>(wave)) return;
 #pragma unroll
   for (int t = 0; t < Stg<S, P>::TPW; ++t)
-    v[t] = *reinterpret_cast<const bf16x4*>(img_base + gofs<S, P>(kslice, wave, lane, t));
+    v[t] = ldg(reinterpret_cast<const bf16x4*>(img_base + gofs<S, P>(kslice, wave, lane, t)));
 }
 
 // write-through (sc1) stores: these tensors are read by other workgroups in the launch
@@ -511,8 +571,8 @@ __device__ __forceinline__ void bn_sums(F f, float* red, double* acc, int wave, 
         v2 += red[w * 128 + 64 + c];
       }
     double* p = acc + (long)(blockIdx.x % BN_ACC_REP) * 2 * G::C + c;
-    unsafeAtomicAdd(p, (double)v1);
-    unsafeAtomicAdd(p + G::C, (double)v2);
+    atomic_add_g(p, (double)v1);
+    atomic_add_g(p + G::C, (double)v2);
   }
 }
 
@@ -540,18 +600,18 @@ struct BnRegs {
 __device__ __forceinline__ void bn_prefetch_fwd(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
-    r.g = bn.gamma[c];
-    r.b = bn.beta[c];
+    r.g = ldg(bn.gamma + c);
+    r.b = ldg(bn.beta + c);
   }
 }
 __device__ __forceinline__ void bn_prefetch_bwd(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
-    r.g = bn.gamma[c];
-    r.mean = bn.mean[c];
-    r.rstd = bn.rstd[c];
-    r.scale = bn.scale[c];
-    r.shift = bn.shift[c];
+    r.g = ldg(bn.gamma + c);
+    r.mean = ldg(bn.mean + c);
+    r.rstd = ldg(bn.rstd + c);
+    r.scale = ldg(bn.scale + c);
+    r.shift = ldg(bn.shift + c);
   }
 }
 
@@ -560,10 +620,10 @@ __device__ __forceinline__ void bn_prefetch_bwd(const PrnBn& bn, int C, BnRegs& 
 __device__ __forceinline__ void bn_prefetch_tab(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
-    r.scale = bn.scale[c];
-    r.shift = bn.shift[c];
-    r.mean = bn.mean[c];
-    r.rstd = bn.rstd[c];
+    r.scale = ldg(bn.scale + c);
+    r.shift = ldg(bn.shift + c);
+    r.mean = ldg(bn.mean + c);
+    r.rstd = ldg(bn.rstd + c);
   }
 }
 __device__ __forceinline__ void tab_store(const BnRegs& r, int C, float* tbl) {
@@ -597,15 +657,15 @@ __device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const BnRegs& pr, 
     tbl[128 + c] = fmu;
     tbl[192 + c] = rs;
     if (blockIdx.x == 0) {
-      bn.mean[c] = fmu;
-      bn.rstd[c] = rs;
-      bn.scale[c] = sc;
-      bn.shift[c] = sh;
+      stg(bn.mean + c, fmu);
+      stg(bn.rstd + c, rs);
+      stg(bn.scale + c, sc);
+      stg(bn.shift + c, sh);
       if (update_moving) {
         const float uvar = M > 1.0 ? (float)(var * M / (M - 1.0)) : fvar;
-        const float mm = bn.mmean[c], mv = bn.mvar[c];
-        bn.mmean[c] = mm - (1.f - momentum) * (mm - fmu);
-        bn.mvar[c] = mv - (1.f - momentum) * (mv - uvar);
+        const float mm = ldg(bn.mmean + c), mv = ldg(bn.mvar + c);
+        stg(bn.mmean + c, mm - (1.f - momentum) * (mm - fmu));
+        stg(bn.mvar + c, mv - (1.f - momentum) * (mv - uvar));
       }
     }
   }
@@ -631,8 +691,8 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, 
     tbl[320 + c] = pr.scale;
     tbl[384 + c] = pr.shift;
     if (blockIdx.x == 0) {
-      bn.dbeta[c] = sg;
-      bn.dgamma[c] = sgx;
+      stg(bn.dbeta + c, sg);
+      stg(bn.dgamma + c, sgx);
     }
   }
   __syncthreads();
@@ -642,10 +702,10 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, 
 __device__ __forceinline__ void bn_load_table(const PrnBn& bn, int C, float* tbl) {
   const int c = threadIdx.x;
   if (c < C) {
-    tbl[c] = bn.scale[c];
-    tbl[64 + c] = bn.shift[c];
-    tbl[128 + c] = bn.mean[c];
-    tbl[192 + c] = bn.rstd[c];
+    tbl[c] = ldg(bn.scale + c);
+    tbl[64 + c] = ldg(bn.shift + c);
+    tbl[128 + c] = ldg(bn.mean + c);
+    tbl[192 + c] = ldg(bn.rstd + c);
   }
 }
 
@@ -759,7 +819,7 @@ __device__ __forceinline__ void fwd_sums(Ctx& x, const bf16x4 (&v)[8], int bi, i
     const float f = (float)v[t][r];
     s1 = f;
     s2 = f * f;
-  }, x.m.red, x.a->bns[bi].acc, wave, lane);
+  }, x.m.red, ld_const(x.a->bns + (bi)).acc, wave, lane);
 }
 
 // prefetch registers for the next block's conv1 after a stage-S block (stage S or S+1)
@@ -780,7 +840,7 @@ __device__ __forceinline__ void fwd_bn_halo(Ctx& x, bf16* hal, const bf16x4 (&v)
   const Nbr<S, P> nb(x.kslice);
   bf16x8 nv = {};
   if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok) nv = ld_sc1_b128(src, nb.gofs);
-  bn_fwd_table(a.bns[bi], x.bnr, G::C, (double)a.N * G::R * G::R, a.eps, a.momentum,
+  bn_fwd_table(ld_const(a.bns + (bi)), x.bnr, G::C, (double)a.N * G::R * G::R, a.eps, a.momentum,
                a.update_moving, x.m.tbl);
   if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok)
     nv = affine_relu8(nv, x.m.tbl + nb.u * 8, x.m.tbl + 64 + nb.u * 8);
@@ -827,7 +887,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
     const WLoad L2 = wl_fwd(B.w2f, G::C, G::C, 3);
     w_prefetch(L2, w2r);
-    bn_prefetch_fwd(a.bns[B.bn2], G::C, x.bnr);
+    bn_prefetch_fwd(ld_const(a.bns + (B.bn2)), G::C, x.bnr);
     if (!wait_fwd(x)) return false;
     probe(x, 6);
     // BN2 + ReLU -> halo A, conv2 (+ residual)
@@ -849,7 +909,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
   w_prefetch(next_wp, wpr);
-  bn_prefetch_fwd(a.bns[bi_next], G::C, x.bnr);   // the next BN normalizes this output
+  bn_prefetch_fwd(ld_const(a.bns + (bi_next)), G::C, x.bnr);   // the next BN normalizes this output
   if (!wait_fwd(x)) return false;
   probe(x, 12);
   w_store(next_w1, w1r, x.m.w1);   // visible after the next block's first __syncthreads
@@ -894,7 +954,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     }
     __syncthreads();
   }
-  const PrnBlock& B0 = a.blocks[0];
+  const PrnBlock& B0 = ld_const(a.blocks + (0));
   bf16x4 xr[8];
   {
     f32x4 acc[8];
@@ -910,7 +970,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     bf16x8 w1r[nreg(conv_units(16, 16, 3))], wpr[1];
     w_prefetch(L1, w1r);
     w_prefetch(LP, wpr);
-    bn_prefetch_fwd(a.bns[B0.bn1], 16, x.bnr);
+    bn_prefetch_fwd(ld_const(a.bns + (B0.bn1)), 16, x.bnr);
     if (!wait_fwd(x)) return;
     w_store(L1, w1r, x.m.w1);
     w_store(LP, wpr, x.m.w2);
@@ -922,12 +982,12 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
   auto run = [&](auto tag, int bi) -> bool {
     constexpr int S = decltype(tag)::S, STR = decltype(tag)::STR;
     constexpr bool PROJ = decltype(tag)::PROJ;
-    const PrnBlock& B = a.blocks[bi];
+    const PrnBlock& B = ld_const(a.blocks + (bi));
     const bool last = bi + 1 == a.nblocks;
-    const int bnx = last ? 2 * a.nblocks : a.blocks[bi + 1].bn1;
+    const int bnx = last ? 2 * a.nblocks : ld_const(a.blocks + (bi + 1)).bn1;
     WLoad n1{}, np{};
     if (!last) {
-      const PrnBlock& Bn = a.blocks[bi + 1];
+      const PrnBlock& Bn = ld_const(a.blocks + (bi + 1));
       const int so = Bn.stage, si = Bn.stride == 2 ? so - 1 : so;
       n1 = wl_fwd(Bn.w1f, 16 << so, 16 << si, 3);
       if (Bn.wpf) np = wl_fwd(Bn.wpf, 16 << so, 16 << si, 1);
@@ -953,7 +1013,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
   const int dunits = 64 * a.kpad / 8;
   bf16x8 dwv = {};
   if (x.kslice == 0 && tid < dunits) dwv = *reinterpret_cast<const bf16x8*>(a.dense_w + tid * 8);
-  bn_fwd_table(a.bns[fb], x.bnr, 64, (double)a.N * 64, a.eps, a.momentum, a.update_moving, x.m.tbl);
+  bn_fwd_table(ld_const(a.bns + (fb)), x.bnr, 64, (double)a.N * 64, a.eps, a.momentum, a.update_moving, x.m.tbl);
   const float* tbl = x.m.tbl;
   {
     const int wave = opaque_s(x.wave), lane = opaque_v(x.lane);
@@ -993,7 +1053,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
 #pragma unroll
       for (int w = 0; w < NW; ++w)
         if (w % G2::WPB == grp) v += x.m.red[w * 128 + tid];
-      unsafeAtomicAdd(a.pool_acc + (long)x.img * 64 + tid, (double)v);
+      atomic_add_g(a.pool_acc + (long)x.img * 64 + tid, (double)v);
     }
   }
   grid_arrive(a.bar);
@@ -1083,7 +1143,7 @@ __device__ __forceinline__ void bwd_sums(Ctx& x, const bf16x4 (&da)[8], const bf
     const float gg = (xf * tb[c] + tb[64 + c] > 0.f) ? (float)da[t][r] : 0.f;
     s1 = gg;
     s2 = gg * (xf - tb[128 + c]) * tb[192 + c];
-  }, x.m.red, x.a->bns[bi].bacc, wave, lane);
+  }, x.m.red, ld_const(x.a->bns + (bi)).bacc, wave, lane);
 }
 
 // dh = a g - b - c xhat (+ add) with the backward coefficient table cf
@@ -1125,7 +1185,7 @@ __device__ __forceinline__ void bwd_nbr_issue(const Nbr<S, P>& nb, const bf16* d
                                               const bf16* xsrc, const bf16* add, NbrBwd& q) {
   if ((int)threadIdx.x < Nbr<S, P>::UNITS && nb.ok) {
     q.dv = da ? ld_sc1_b128(da, nb.gofs) : bf16x8{};
-    q.xv = *reinterpret_cast<const bf16x8*>(xsrc + nb.gofs);
+    q.xv = ldg(reinterpret_cast<const bf16x8*>(xsrc + nb.gofs));
     q.av = add ? ld_sc1_b128(add, nb.gofs) : bf16x8{};
   }
 }
@@ -1147,13 +1207,13 @@ __device__ __forceinline__ void bwd_halo(Ctx& x, bf16* hal, const bf16x4 (&own)[
 // One block's backward: dout (stage S) in registers and its halo in HB, the saved BN2
 // input `hs` in registers, conv2's dgrad weights in W1, BN2's forward table in x.ftr;
 // out: dx (input stage) in `dout`, its halo in HB, and for the previous block `Bn`
-// (nullptr: none) its conv2 dgrad weights (`next_w2`) in W1, its BN2 input in `hs`, its
+// (has_prev false: none) its conv2 dgrad weights (`next_w2`) in W1, its BN2 input in `hs`, its
 // BN2 forward table in x.ftr.  Every global load on the critical path is issued a phase
 // ahead (before a barrier wait, or before the halo work).
 template <int S, int STR, bool PROJ, int P>
 __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs)[8],
-                                          const WLoad& next_w2, const PrnBlock* Bn,
-                                          const PrnBlock& B) {
+                                          const WLoad& next_w2, bool has_prev,
+                                          const PrnBlock& Bn, const PrnBlock& B) {
   constexpr int SI = STR == 2 ? S - 1 : S;
   using GI = Stg<SI, P>;
   using G = Stg<S, P>;
@@ -1186,14 +1246,14 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     bf16x8 w1r[nreg(conv_units(G::C, GI::C, 3))], wpr[1];
     w_prefetch(L1, w1r);
     w_prefetch(LP, wpr);
-    bn_prefetch_bwd(a.bns[B.bn2], G::C, x.bnr);
-    bn_prefetch_tab(a.bns[B.bn1], GI::C, x.ftr);
+    bn_prefetch_bwd(ld_const(a.bns + (B.bn2)), G::C, x.bnr);
+    bn_prefetch_tab(ld_const(a.bns + (B.bn1)), GI::C, x.ftr);
     if (!wait_bwd(x)) return false;
     probe(x, 6);
     const Nbr<S, P> nb(x.kslice);
     NbrBwd q;
     bwd_nbr_issue<S, P>(nb, B.da2 + img_o, B.h1 + img_o, nullptr, q);
-    bn_bwd_table(a.bns[B.bn2], x.bnr, G::C, (float)a.N * G::R * G::R, x.m.tbl2);
+    bn_bwd_table(ld_const(a.bns + (B.bn2)), x.bnr, G::C, (float)a.N * G::R * G::R, x.m.tbl2);
     bf16x4 dh[8];
     bwd_apply<S, P, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
     publish<S, P>(dh, B.dh1 + img_o, x.kslice, wave, lane);    // conv1 weight gradient
@@ -1221,17 +1281,17 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   probe(x, 11);
   bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
   w_prefetch(next_w2, w2r);
-  bn_prefetch_bwd(a.bns[B.bn1], GI::C, x.bnr);
-  if (Bn) bn_prefetch_tab(a.bns[Bn->bn2], GI::C, x.ftr);
+  bn_prefetch_bwd(ld_const(a.bns + (B.bn1)), GI::C, x.bnr);
+  if (has_prev) bn_prefetch_tab(ld_const(a.bns + (Bn.bn2)), GI::C, x.ftr);
   if (!wait_bwd(x)) return false;
   probe(x, 12);
   const Nbr<SI, P> nb(x.kslice);
   NbrBwd q;
   bwd_nbr_issue<SI, P>(nb, B.da1 + img_i, B.x + img_i, PROJ ? nullptr : B.dout + img_o, q);
-  bn_bwd_table(a.bns[B.bn1], x.bnr, GI::C, (float)a.N * GI::R * GI::R, x.m.tbl2);
+  bn_bwd_table(ld_const(a.bns + (B.bn1)), x.bnr, GI::C, (float)a.N * GI::R * GI::R, x.m.tbl2);
   if constexpr (PROJ) bwd_apply<SI, P, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   else bwd_apply<SI, P, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
-  if (Bn) load_regs<SI, P>(hs, Bn->h1 + img_i, x.kslice, wave, lane);   // previous block's BN2 input
+  if (has_prev) load_regs<SI, P>(hs, Bn.h1 + img_i, x.kslice, wave, lane);   // previous block's BN2 input
   // the halo of dx for the previous block's conv2 dgrad (its neighbour rows: this block's
   // published da1, the saved block input, and -- identity blocks -- the published dout)
   bwd_halo<SI, P>(x, x.m.hb, dout, nb, q, nullptr, !PROJ, x.m.tbl2, wave, lane);
@@ -1261,8 +1321,8 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
   const int tg = wave % WT, kq = wave / WT;
   const int gq = lane >> 4, li = lane & 15, qr = li >> 2, pc = li & 3;
   if (it.scale != nullptr && tid < CI) {
-    tb[tid] = it.scale[tid];
-    tb[64 + tid] = it.shift[tid];
+    tb[tid] = ldg(it.scale + tid);
+    tb[64 + tid] = ldg(it.shift + tid);
   }
   f32x4 acc[TPW];
 #pragma unroll
@@ -1278,7 +1338,7 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
       const int hr = pix / W2, hc = pix - hr * W2;
       bf16x8 v = {};
       if (hr >= 1 && hr <= RI && hc >= 1 && hc <= RI) {
-        v = *reinterpret_cast<const bf16x8*>(it.x + (((long)n * RI + hr - 1) * RI + hc - 1) * CI + u * 8);
+        v = ldg(reinterpret_cast<const bf16x8*>(it.x + (((long)n * RI + hr - 1) * RI + hc - 1) * CI + u * 8));
         if (it.scale != nullptr) v = affine_relu8(v, tb + u * 8, tb + 64 + u * 8);
       }
       *reinterpret_cast<bf16x8*>(hal + pix * CI + u * 8) = v;
@@ -1338,7 +1398,7 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
       const int n = nb * 16 + li;
       if (n < KN)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) it.part[(long)(mb * 16 + 4 * gq + i) * KN + n] = acc[t][i];
+        for (int i = 0; i < 4; ++i) stg(it.part + (long)(mb * 16 + 4 * gq + i) * KN + n, acc[t][i]);
     }
   }
   __syncthreads();
@@ -1378,7 +1438,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     const int w = blockIdx.x - nsl, W = gridDim.x - nsl;
     int* flag = reinterpret_cast<int*>(smem + OFF_MISC);
     for (int i = w; i < a.nitems; i += W) {
-      const PrnItem& it = a.items[i];
+      const PrnItem& it = ld_const(a.items + i);
       if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
       run_item(it, smem, wave, lane);
     }
@@ -1396,7 +1456,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   x.pc = 0;
   probe(x, 0);
   const int nb = a.nblocks;
-  const PrnBlock& BL = a.blocks[nb - 1];
+  const PrnBlock& BL = ld_const(a.blocks + (nb - 1));
   {   // the last block's conv2 dgrad weights (stage 2: 64 x 576)
     const WLoad L = wl_dgrad(BL.w2b, 64, 64, 3);
     bf16x8 r[nreg(conv_units(64, 64, 3))];
@@ -1413,7 +1473,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     bf16x4 xs[8];
     load_regs<2, P>(xs, BL.out + img_o, x.kslice, wave, lane);
     float* dps = x.m.tbl + 256;   // this image's dpool row
-    bn_load_table(a.bns[fb], 64, x.m.tbl);
+    bn_load_table(ld_const(a.bns + (fb)), 64, x.m.tbl);
     if (tid < 64) dps[tid] = a.dpool[(long)x.img * 64 + tid];
     __syncthreads();
     bf16x4 dp[8];
@@ -1426,13 +1486,13 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     }
     bwd_sums<2, P>(x, dp, xs, x.m.tbl, fb, wave, lane);
     grid_arrive(a.bar + 1);
-    bn_prefetch_bwd(a.bns[fb], 64, x.bnr);
-    bn_prefetch_tab(a.bns[BL.bn2], 64, x.ftr);
+    bn_prefetch_bwd(ld_const(a.bns + (fb)), 64, x.bnr);
+    bn_prefetch_tab(ld_const(a.bns + (BL.bn2)), 64, x.ftr);
     if (!wait_bwd(x)) return;
     const Nbr<2, P> nb(x.kslice);
     NbrBwd q;
     bwd_nbr_issue<2, P>(nb, nullptr, BL.out + img_o, nullptr, q);
-    bn_bwd_table(a.bns[fb], x.bnr, 64, (float)a.N * 64, x.m.tbl2);
+    bn_bwd_table(ld_const(a.bns + (fb)), x.bnr, 64, (float)a.N * 64, x.m.tbl2);
     bwd_apply<2, P, false>(dout, dp, xs, dout, x.m.tbl2, wave, lane);
     load_regs<2, P>(hs, BL.h1 + img_o, x.kslice, wave, lane);
     bwd_halo<2, P>(x, x.m.hb, dout, nb, q, dps, false, x.m.tbl2, wave, lane);
@@ -1443,9 +1503,10 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     constexpr int S = decltype(tag)::S, STR = decltype(tag)::STR;
     constexpr bool PROJ = decltype(tag)::PROJ;
     WLoad n2{};
-    const PrnBlock* Bp = bi > 0 ? &a.blocks[bi - 1] : nullptr;
-    if (Bp) n2 = wl_dgrad(Bp->w2b, 16 << Bp->stage, 16 << Bp->stage, 3);
-    return block_bwd<S, STR, PROJ, P>(x, dout, hs, n2, Bp, a.blocks[bi]);
+    const bool hp = bi > 0;
+    const PrnBlock Bp = ld_const(a.blocks + (hp ? bi - 1 : bi));
+    if (hp) n2 = wl_dgrad(Bp.w2b, 16 << Bp.stage, 16 << Bp.stage, 3);
+    return block_bwd<S, STR, PROJ, P>(x, dout, hs, n2, hp, Bp, ld_const(a.blocks + (bi)));
   };
   for (int bi = nb - 1; bi > 2 * nps; --bi)
     if (!run(BlkTag<2, 1, false>{}, bi)) return;

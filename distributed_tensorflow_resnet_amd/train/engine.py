@@ -1336,14 +1336,18 @@ class Engine:
             plan.record(ev)
             plan.use_stream(0)
             plan.wait(ev)
-        # per bucket: its slab reduces, then (world > 1) its all-reduce on the comm stream
+        # every slab is complete when the backward launch ends, and that launch holds
+        # every CU (nothing can overlap it): ONE grouped reduce of all the slabs, then
+        # (world > 1) ONE all-reduce of the whole gradient -- the per-bucket launches of
+        # the per-layer plan only pay off when they overlap a backward (bs16: 6 reduce
+        # launches 32 us vs 1)
+        self._emit_reduce(plan, [n for (_, _, names) in self.buckets for n in names])
         for bi, (lo, hi, names) in enumerate(self.buckets):
-            for gnames in self.reduce_groups[bi]:
-                self._emit_reduce(plan, gnames)
             self._mark(plan, *names)
             self._flushed.add(bi)
-            if self.comm is not None:
-                self._emit_allreduce(plan, lo, hi, side_dep=False)
+        if self.comm is not None:
+            self._emit_allreduce(plan, min(b[0] for b in self.buckets),
+                                 max(b[1] for b in self.buckets), side_dep=False)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
         self._join_comm(plan)
         self._t_joined = plan.timing_point("allreduce_joined")
