@@ -727,7 +727,7 @@ __device__ __forceinline__ bf16x8 bwd8(bf16x8 da, bf16x8 x, bf16x8 add, bool has
 }
 
 // ---- LDS carve-up (bytes) ------------------------------------------------------------
-constexpr int HALO_B = (16 + 2) * 34 * 16 * 2;            // P = 2 slice of the 32x32x16 map
+constexpr int HALO_B = (32 + 2) * 34 * 16 * 2;            // P = 1: the whole 32x32x16 map
 constexpr int W1_B = 64 * kpad_of(576) * 2;               // 64 rows x 9*64 (+pad)
 constexpr int W2_B = 64 * kpad_of(32) * 2;                // projection (64 x 32 fwd / 32 x 64 dgrad)
 constexpr int TBL_B = 7 * 64 * 4;
@@ -1531,7 +1531,7 @@ void prn_set_probe(long long* p) { g_prn_probe = p; }
 size_t prn_lds_bytes() { return LDS_TOTAL; }
 
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad) {
-  return N >= 1 && (P == 2 || P == 4) && N * P <= 192 && nblocks >= 3 && nblocks % 3 == 0 &&
+  return N >= 1 && (P == 1 || P == 2 || P == 4) && N * P <= 224 && nblocks >= 3 && nblocks % 3 == 0 &&
          classes >= 1 && classes <= kpad && kpad <= 64 && kpad % 16 == 0;
 }
 
@@ -1553,7 +1553,8 @@ void prn_forward(const PrnArgs& a, hipStream_t s) {
     throw std::invalid_argument("prn_forward: unsupported shape (N x P <= CUs, 3n blocks, <= 64 classes)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
+  if (a.P == 1) hipLaunchKernelGGL(prn_fwd_kernel<1>, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
+  else if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_fwd_kernel<4>, dim3(a.N * 4), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }
@@ -1566,7 +1567,8 @@ void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
     throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  if (a.P == 2) hipLaunchKernelGGL(prn_bwd_kernel<2>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
+  if (a.P == 1) hipLaunchKernelGGL(prn_bwd_kernel<1>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
+  else if (a.P == 2) hipLaunchKernelGGL(prn_bwd_kernel<2>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_bwd_kernel<4>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   DTR_CHECK_LAUNCH();
 }

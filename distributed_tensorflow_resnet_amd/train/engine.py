@@ -252,7 +252,7 @@ class Engine:
         self._alloc_activations()
         # Persistent small-batch CIFAR step (train/persist.py, csrc/cifar_persist.hip): the
         # forward and the backward each as ONE launch (tune persist: -1 auto = per-rank
-        # batch <= 32 on a supported CIFAR network, 0 off, 1 whenever supported)
+        # batch <= AUTO_MAX_BATCH on a supported CIFAR network, 0 off, 1 whenever supported)
         from . import persist as _persist
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")

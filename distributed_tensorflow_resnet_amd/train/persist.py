@@ -14,7 +14,7 @@ image group) while the backward's dgrad chain continues.  The step is then:
     [augment] -> prn forward -> (side: softmax-xent batch folds, dense wgrad)
               -> prn backward -> grouped slab reduces (+ bucket all-reduces) -> optimizer
 
-Selected by the engine (tune ``persist``: -1 auto = per-rank batch <= 32 on a supported
+Selected by the engine (tune ``persist``: -1 auto = per-rank batch <= AUTO_MAX_BATCH on a supported
 CIFAR spec, 0 off, 1 on when supported).
 """
 from __future__ import annotations
@@ -31,17 +31,22 @@ PRN_BLOCK = np.dtype([(k, "<u8") for k in ("x", "h1", "out", "w1f", "w2f", "wpf"
                      [(k, "<i4") for k in ("stage", "stride", "bn1", "bn2")])
 PRN_ITEM = np.dtype([(k, "<u8") for k in ("dy", "x", "scale", "shift", "part")] +
                     [(k, "<i4") for k in ("kind", "img0", "nimg", "ready")])
-AUTO_MAX_BATCH = 32
+# every supported per-rank batch (MI355X, CIFAR RN50 step vs the per-layer engine: bs16
+# 0.660 vs 0.915 ms, bs32 0.722 vs 0.962, bs64 0.837 vs 1.085, bs96 1.034 vs 1.272, bs128
+# (1 slice) 1.101 vs 1.261)
+AUTO_MAX_BATCH = 240
 
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
-    """Row slices (workgroups) per image: 4 up to 16 images, else 2 (MI355X, CIFAR RN50:
-    bs16 0.815 ms at 4 vs 0.840 at 2; bs32 0.993 at 4 vs 0.977 at 2 -- the barrier
-    latency grows with the number of arrivals).  The engine's tune persist_slices
-    overrides."""
-    if override in (2, 4):
+    """Row slices (workgroups) per image: 4 up to 16 images, 2 while 2N slices leave 32
+    CUs for the weight gradients, else 1 (MI355X, CIFAR RN50: bs16 0.815 ms at 4 vs
+    0.840 at 2; bs32 0.993 at 4 vs 0.977 at 2 -- the barrier latency grows with the
+    number of arrivals).  The engine's tune persist_slices overrides."""
+    if override in (1, 2, 4):
         return override
-    return 4 if N <= 16 and 4 * N + 32 <= cus else 2
+    if N <= 16 and 4 * N + 32 <= cus:
+        return 4
+    return 2 if 2 * N + 32 <= cus else 1
 
 
 def supported(eng) -> bool:
@@ -67,7 +72,8 @@ def supported(eng) -> bool:
             return False
     cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
     P = slices_for(eng.N, cus, eng.persist_slices)
-    return eng.N * P < cus and bool(nat.prn_supported(eng.N, P, nb, spec.num_classes, eng.kpad))
+    # (at least 16 CUs left for the weight-gradient workgroups)
+    return eng.N * P + 16 <= cus and bool(nat.prn_supported(eng.N, P, nb, spec.num_classes, eng.kpad))
 
 
 def _stage(b) -> int:

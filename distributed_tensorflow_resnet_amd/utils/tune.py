@@ -52,9 +52,9 @@ ENGINE = {
                            "stage 3) on the streaming kernel bn_dgrad1x1 (store + sums)"),
     "persist": (-1, "persistent small-batch CIFAR step (forward and backward each ONE launch, "
                     "one workgroup per image row slice; train/persist.py): -1 auto = per-rank "
-                    "batch <= 32, 0 off, 1 whenever the network is supported"),
-    "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (4 up to "
-                           "16 images, else 2), 2 or 4"),
+                    "batch <= 240, 0 off, 1 whenever the network is supported"),
+    "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (4 up to 16 "
+                           "images, 2 while 2N + 32 <= CUs, else 1), 1, 2 or 4"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 

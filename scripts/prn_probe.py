@@ -73,13 +73,20 @@ def main():
             xs = acc[t]
             print(f"  {str(NAMES[seg].get(t, t)):34s} n={len(xs):3d} mean {sum(xs)/len(xs):7.2f} us  total {sum(xs):8.1f} us")
         stage_t = defaultdict(float)
+        per = defaultdict(lambda: defaultdict(list))   # phase -> stage -> [us]
         cur = None
         for (t0, c0), (t1, c1) in zip(stamps, stamps[1:]):
             if t0 >= 100 and t0 < 200:
                 cur = t0 - 100
             if cur is not None:
                 stage_t[cur] += (c1 - c0) / 100.0
+                if not (100 <= t1 < 200):
+                    per[t1][cur].append((c1 - c0) / 100.0)
         print("  per stage:", {k: round(v, 1) for k, v in sorted(stage_t.items())})
+        print("  mean us per phase and stage:")
+        for t in sorted(per):
+            row = "  ".join(f"s{k}: {sum(v) / len(v):5.2f}" for k, v in sorted(per[t].items()))
+            print(f"    {str(NAMES[seg].get(t, t)):34s} {row}")
     step = eng.step_timed()
     print("step_timed:", {k: round(v, 4) for k, v in step.items()})
 

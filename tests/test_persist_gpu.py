@@ -15,8 +15,8 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-def _engine(monkeypatch, spec, N, gpu, persist, input_mode="nhwc"):
-    monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
+def _engine(monkeypatch, spec, N, gpu, persist, input_mode="nhwc", slices=-1):
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist},persist_slices={slices}")
     eng = Engine(spec, N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu,
                  input_mode=input_mode, use_graph=False)
     assert eng.persist == (persist == 1)
@@ -30,8 +30,8 @@ def _batch(spec, N, gpu, seed=0):
     return imgs.to(gpu), labels.to(gpu)
 
 
-def _pair(monkeypatch, spec, N, gpu):
-    ep = _engine(monkeypatch, spec, N, gpu, 1)
+def _pair(monkeypatch, spec, N, gpu, slices=-1):
+    ep = _engine(monkeypatch, spec, N, gpu, 1, slices=slices)
     er = _engine(monkeypatch, spec, N, gpu, 0)
     er.params.master.copy_(ep.params.master)
     er.params.stats.copy_(ep.params.stats)
@@ -42,12 +42,15 @@ def _pair(monkeypatch, spec, N, gpu):
     return ep, er, imgs, labels
 
 
-@pytest.mark.parametrize("size,N", [(8, 16), (20, 32), (50, 16)])
-def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N):
+@pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (20, 32, 2), (50, 16, 4), (20, 16, 1),
+                                           (8, 64, 2)])
+def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N, slices):
     """Saved activations, batch statistics and head outputs of the one-launch forward
-    vs the per-layer forward (same weights, same batch): bf16-rounding agreement."""
+    vs the per-layer forward (same weights, same batch): bf16-rounding agreement, for
+    4, 2 and 1 row slices per image."""
     spec = cifar_spec(size)
-    ep, er, _, _ = _pair(monkeypatch, spec, N, gpu)
+    ep, er, _, _ = _pair(monkeypatch, spec, N, gpu, slices)
+    assert ep.prn.P == slices
     st = torch.cuda.current_stream().cuda_stream
     for e in (ep, er):
         e._run("fwd", st)
@@ -68,12 +71,13 @@ def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N):
     assert _rel(ep.params.stats, er.params.stats) < 1e-3   # moving averages
 
 
-@pytest.mark.parametrize("size,N", [(8, 16), (8, 32)])
-def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N):
+@pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (8, 32, 2), (8, 16, 1), (8, 48, 2)])
+def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N, slices):
     """Whole training step (forward + backward + slab reduces): per-tensor gradients
     vs the bf16-emulating fp32 oracle, like test_engine_step_matches_autograd_shallow."""
     spec = cifar_spec(size)
-    ep = _engine(monkeypatch, spec, N, gpu, 1)
+    ep = _engine(monkeypatch, spec, N, gpu, 1, slices=slices)
+    assert ep.prn.P == slices
     imgs, labels = _batch(spec, N, gpu)
     ep.set_batch(imgs, labels)
     store = ParamStore(spec, device=gpu)
@@ -172,12 +176,14 @@ def test_persistent_training_tracks_per_layer(gpu, monkeypatch):
 
 
 def test_persistent_auto_selection(gpu, monkeypatch):
-    """tune persist -1: on at per-rank batch <= 32, off above; never for ImageNet."""
+    """tune persist -1: on for every supported per-rank batch (4 slices up to 16 images,
+    then 2, then 1); never for ImageNet."""
     from distributed_tensorflow_resnet_amd.models.spec import imagenet_spec
 
     monkeypatch.setenv("DTR_TUNE", "persist=-1")
     mk = lambda spec, N: Engine(spec, N, weight_decay=2e-4,  # noqa: E731
                                 lr_schedule=cifar_lr_schedule(), device=gpu)
-    assert mk(cifar_spec(8), 32).persist
-    assert not mk(cifar_spec(8), 64).persist
+    assert mk(cifar_spec(8), 16).prn.P == 4
+    assert mk(cifar_spec(8), 64).prn.P == 2
+    assert mk(cifar_spec(8), 128).prn.P == 1
     assert not mk(imagenet_spec(18, image_hw=64), 8).persist
