@@ -1234,7 +1234,8 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   bf16x4 da[8];
   round_acc<S, P, false>(da, acc, da);
   probe(x, 3);
-  publish<S, P>(da, B.da2 + img_o, x.kslice, wave, lane);
+  if constexpr (P > 1)   // only the neighbouring slices read it
+    publish<S, P>(da, B.da2 + img_o, x.kslice, wave, lane);
   bwd_sums<S, P>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
   probe(x, 4);
   grid_arrive(a.bar + 1);
@@ -1274,7 +1275,8 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   }
   round_acc<SI, P, false>(da, acc, da);
   probe(x, 9);
-  publish<SI, P>(da, B.da1 + img_i, x.kslice, wave, lane);
+  if constexpr (P > 1)   // only the neighbouring slices read it
+    publish<SI, P>(da, B.da1 + img_i, x.kslice, wave, lane);
   bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar + 1);

@@ -38,15 +38,16 @@ AUTO_MAX_BATCH = 240
 
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
-    """Row slices (workgroups) per image: 4 up to 16 images, 2 while 2N slices leave 32
-    CUs for the weight gradients, else 1 (MI355X, CIFAR RN50: bs16 0.815 ms at 4 vs
-    0.840 at 2; bs32 0.993 at 4 vs 0.977 at 2 -- the barrier latency grows with the
-    number of arrivals).  The engine's tune persist_slices overrides."""
+    """Row slices (workgroups) per image: 4 up to 16 images, 2 up to 64, else 1
+    (MI355X, CIFAR RN50 step ms: bs16 0.667 at 4 / 0.684 at 2; bs32 0.722 at 2 / 0.826
+    at 1; bs64 0.836 / 0.893; bs96 1.025 at 2 / 0.998 at 1 -- more slices shorten each
+    layer, more arrivals lengthen each barrier and leave fewer CUs for the weight
+    gradients).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
     if N <= 16 and 4 * N + 32 <= cus:
         return 4
-    return 2 if 2 * N + 32 <= cus else 1
+    return 2 if N <= 64 and 2 * N + 32 <= cus else 1
 
 
 def supported(eng) -> bool:
@@ -111,9 +112,10 @@ class PersistStep:
         self.dout = [torch.empty_like(eng.X[i + 1]) for i in range(nb)]
         self.dh1 = [torch.empty_like(eng.H1[i]) for i in range(nb)]
         # dgrad outputs before their BN backward: the neighbouring slices recompute their
-        # halo rows of the BN-backward output from these
-        self.da2 = [torch.empty_like(eng.H1[i]) for i in range(nb)]
-        self.da1 = [torch.empty_like(eng.X[i]) for i in range(nb)]
+        # halo rows of the BN-backward output from these (no neighbours at 1 slice)
+        none = torch.empty(0, dtype=eng.X[0].dtype, device=dev)
+        self.da2 = [torch.empty_like(eng.H1[i]) if self.P > 1 else none for i in range(nb)]
+        self.da1 = [torch.empty_like(eng.X[i]) if self.P > 1 else none for i in range(nb)]
         rows = np.zeros(nb, dtype=PRN_BLOCK)
         for i, (r, b) in enumerate(zip(rows, blocks)):
             c1, c2 = eng.convs[b.convs[0].name], eng.convs[b.convs[1].name]
