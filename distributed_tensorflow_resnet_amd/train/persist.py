@@ -140,16 +140,20 @@ class PersistStep:
         (`ready` = backward barrier count after which it is visible; barrier 1 is the
         final BN): per block j (last block first) conv2 and the projection with the
         block's dout at 2j + 2, conv1 with dh1 at 2j + 3; the stem after the final arrive.
-        Images are grouped 4 ways (the grouped reduce reads one slab per group): the items
-        of the first blocks only become ready at the end of the backward, and a quarter of
-        the batch per workgroup shortens that tail 4x for a 4-slab reduce."""
+        Images are grouped per item (the grouped reduce sums one slab per group): a
+        quarter of the batch for stages 2-3, whose items have the rest of the backward
+        to run in; 4 images for stage 1 and the stem, whose items only become ready at
+        the end of the backward -- their duration is the launch's tail (bs128: 32-image
+        items left ~140 us of tail after the last slice finished)."""
         eng, spec, N = self.eng, self.eng.spec, self.eng.N
         nat = eng.nat
         blocks = spec.blocks
         nb = len(blocks)
-        self.group = max(1, math.ceil(N / 4))
-        groups = [(g0, min(self.group, N - g0)) for g0 in range(0, N, self.group)]
-        self.splits = len(groups)
+
+        def groups_of(name):
+            c = eng.convs[name]
+            size = 4 if c.spec.cout == 16 else max(1, math.ceil(N / 4))
+            return [(g0, min(size, N - g0)) for g0 in range(0, N, size)]
         convs = []   # (name, dy, x, bn scale, bn shift, ready)
         for j, i in enumerate(range(nb - 1, -1, -1)):
             b = blocks[i]
@@ -161,12 +165,13 @@ class PersistStep:
             convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 3))
         convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 2))
         tot = 0
-        self.part_off = {}
+        self.part_off, self.splits = {}, {}
         for name, *_ in convs:
             c = eng.convs[name]
             s = c.spec
             self.part_off[name] = tot
-            tot += self.splits * s.cout * s.kh * s.kw * c.cin
+            self.splits[name] = len(groups_of(name))
+            tot += self.splits[name] * s.cout * s.kh * s.kw * c.cin
         self.part = torch.empty(max(tot, 1), device=eng.device)
         items = []
         for name, dy, x, bn, ready in convs:
@@ -175,7 +180,7 @@ class PersistStep:
             kind = nat.prn_item_kind(c.cin, s.cout, s.kh, s.stride)
             assert kind >= 0, (name, c.cin, s.cout, s.kh, s.stride)
             slab = s.cout * s.kh * s.kw * c.cin
-            for gi, (g0, gn) in enumerate(groups):
+            for gi, (g0, gn) in enumerate(groups_of(name)):
                 r = np.zeros(1, dtype=PRN_ITEM)[0]
                 r["dy"], r["x"] = dy, x
                 if bn is not None:
@@ -195,7 +200,7 @@ class PersistStep:
         for name in self.convs:
             c = eng.convs[name]
             s = c.spec
-            out[c.name] = (self.part.data_ptr() + 4 * self.part_off[name], c.grad, self.splits,
+            out[c.name] = (self.part.data_ptr() + 4 * self.part_off[name], c.grad, self.splits[name],
                            s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         return out
 
