@@ -89,6 +89,16 @@ def local_device_index() -> int:
     return local % n if n > 0 else local
 
 
+def gpu_shared_by_ranks() -> bool:
+    """Whether this node's ranks are folded onto fewer GPUs than ranks (the one-GPU
+    rehearsals).  Kernels that need every workgroup co-resident (the persistent CIFAR
+    step) must not run then: two processes' grids interleaved on one device could each
+    hold part of the CUs and wait for the rest forever."""
+    n = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return n > 0 and local_world > n
+
+
 class DistContext:
     """Thin, explicit wrapper so the engine never touches global state."""
 

@@ -254,9 +254,11 @@ class Engine:
         # forward and the backward each as ONE launch (tune persist: -1 auto = per-rank
         # batch <= AUTO_MAX_BATCH on a supported CIFAR network, 0 off, 1 whenever supported)
         from . import persist as _persist
+        from ..parallel.dist import gpu_shared_by_ranks
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")
-        ok = pm != 0 and _persist.supported(self)
+        # (never on a GPU shared by several ranks: its grids need every CU to themselves)
+        ok = pm != 0 and not gpu_shared_by_ranks() and _persist.supported(self)
         self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
         self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()

@@ -37,10 +37,16 @@ def _engines(gpu, **kw):
 
 
 @pytest.mark.gpu
-def test_native_comm_single_rank_is_identity(gpu):
+@pytest.mark.parametrize("persist", ["0", "1"])
+def test_native_comm_single_rank_is_identity(gpu, monkeypatch, persist):
+    """Per-layer plan: one all-reduce per bucket, overlapping the backward; persistent
+    step: ONE all-reduce of the whole gradient after the backward launch."""
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
     ref, eng = _engines(gpu)
+    assert eng.persist == (persist == "1")
     info = eng.comm_info()
-    assert info["native_rccl"] and info["allreduce_ops"] >= 2, info
+    assert info["native_rccl"], info
+    assert info["allreduce_ops"] >= 2 if persist == "0" else info["allreduce_ops"] == 1, info
     assert "librccl" in info["rccl_library"]
     names = eng.plan.names()
     assert names.count("all_reduce") == info["allreduce_ops"]
@@ -125,12 +131,16 @@ def _loopback_engines(gpu, dtype, seed_eng=3):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_loopback_doubling_standin_orders_every_bucket(gpu, dtype):
-    """grad == 2 x the no-comm engine's grad, bitwise, plain and under jitter."""
+@pytest.mark.parametrize("persist", ["0", "1"])
+def test_loopback_doubling_standin_orders_every_bucket(gpu, monkeypatch, dtype, persist):
+    """grad == 2 x the no-comm engine's grad, bitwise, plain and under jitter (per-layer
+    plan: >= 4 bucket all-reduces; persistent step: one)."""
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
     for trial in range(4):
         ref, eng = _loopback_engines(gpu, dtype)
         info = eng.comm_info()
-        assert info["transport"] == "loopback" and info["allreduce_ops"] >= 4, info
+        assert info["transport"] == "loopback", info
+        assert info["allreduce_ops"] >= 4 if persist == "0" else info["allreduce_ops"] == 1, info
         if trial:   # schedule perturbation: random delays in front of launches, every stream
             eng.plan.set_perturb(2, 1000 + trial, 0.35, 25.0)
         ref.step()

@@ -13,6 +13,13 @@ from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_sche
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _per_layer_engine(monkeypatch):
+    """These tests pin the launch-per-layer engine and its knobs (the persistent CIFAR
+    step, the default for CIFAR batches <= 240, is covered by test_persist_gpu.py)."""
+    monkeypatch.setenv("DTR_TUNE", "persist=0")
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
@@ -177,7 +184,7 @@ def test_bn_accumulator_mode_matches_partials(gpu, monkeypatch):
     spec = cifar_spec(8)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DTR_TUNE", f"bn_acc={mode}")
+        monkeypatch.setenv("DTR_TUNE", f"bn_acc={mode},persist=0")
         eng, _, _, _ = _make(spec, 64, gpu)
         st = torch.cuda.current_stream().cuda_stream
         eng._run("fwd", st)
@@ -196,7 +203,7 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
     spec = cifar_spec(8)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DTR_TUNE", f"fused_head={mode}")
+        monkeypatch.setenv("DTR_TUNE", f"fused_head={mode},persist=0")
         eng, _, _, _ = _make(spec, 64, gpu)
         assert eng._head_fused == (mode == "1")
         st = torch.cuda.current_stream().cuda_stream
@@ -220,7 +227,7 @@ def test_bn_backward_apply_recompute_matches_separate_apply(gpu, monkeypatch):
     spec = imagenet_spec(50, image_hw=64)
     res = {}
     for mode in ("0", "2048"):
-        monkeypatch.setenv("DTR_TUNE", f"bap_maxc={mode}")
+        monkeypatch.setenv("DTR_TUNE", f"bap_maxc={mode},persist=0")
         eng, _, _, _ = _make(spec, 8, gpu)
         st = torch.cuda.current_stream().cuda_stream
         eng._run("fwd", st)
@@ -246,7 +253,7 @@ def test_streaming_fwd1x1_matches_implicit_gemm(gpu, monkeypatch):
     spec = imagenet_spec(0, image_hw=64, block="bottleneck", layers=[2, 2, 2, 2])
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DTR_TUNE", f"fwd1x1_stream={mode}")
+        monkeypatch.setenv("DTR_TUNE", f"fwd1x1_stream={mode},persist=0")
         eng, _, _, _ = _make(spec, 8, gpu)
         st = torch.cuda.current_stream().cuda_stream
         eng._run("fwd", st)
@@ -272,7 +279,7 @@ def test_built_plans_pass_stream_order_check(gpu, monkeypatch, spec_fn, N, fork_
     check sees side-stream work at all (otherwise it would pass vacuously)."""
     from distributed_tensorflow_resnet_amd.utils.streamcheck import check_plan
 
-    monkeypatch.setenv("DTR_TUNE", f"fork_every={fork_every}")
+    monkeypatch.setenv("DTR_TUNE", f"fork_every={fork_every},persist=0")
     eng = Engine(spec_fn(), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
                  device=gpu, use_graph=False)
     assert eng.fork_wgrad

@@ -56,3 +56,25 @@ def test_start_and_stop_background_run(tmp_path):
             alive = False
         assert not alive
     assert not glob.glob(str(tmp_path / "*.pid"))
+
+
+def test_gpu_shared_by_ranks(monkeypatch):
+    """Ranks folded onto fewer GPUs than ranks (one-GPU rehearsals) must switch the
+    persistent CIFAR step off: its grids need every CU of the device to themselves."""
+    import torch
+
+    from distributed_tensorflow_resnet_amd.parallel.dist import gpu_shared_by_ranks
+
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert gpu_shared_by_ranks()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert not gpu_shared_by_ranks()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert not gpu_shared_by_ranks()
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    assert gpu_shared_by_ranks()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert not gpu_shared_by_ranks()

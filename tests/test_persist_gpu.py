@@ -187,3 +187,34 @@ def test_persistent_auto_selection(gpu, monkeypatch):
     assert mk(cifar_spec(8), 64).prn.P == 2
     assert mk(cifar_spec(8), 128).prn.P == 1
     assert not mk(imagenet_spec(18, image_hw=64), 8).persist
+
+
+@pytest.mark.parametrize("slices", [4, 2])
+def test_persistent_step_bitwise_under_concurrent_load(gpu, monkeypatch, slices):
+    """Race stress for the hand-off protocol (write-through publishes, drained arrives,
+    sc1 reads, the weight-gradient readiness line): while the persistent launches run,
+    another stream keeps a CU busy (so one slice workgroup starts late and every other
+    waits at the barriers) and streams memory-heavy kernels through the L2s.  Every run
+    must reproduce the quiet run's gradient bit for bit and never time out."""
+    spec = cifar_spec(20)
+    N = 16 if slices == 4 else 32
+    eng = _engine(monkeypatch, spec, N, gpu, 1, slices=slices)
+    imgs, labels = _batch(spec, N, gpu)
+    eng.set_batch(imgs, labels)
+    st = torch.cuda.current_stream()
+    eng._run("fwd", st.cuda_stream)
+    eng._run_bwd(st.cuda_stream)
+    torch.cuda.synchronize()
+    ref = eng.grad.clone()
+    noise = torch.cuda.Stream(device=gpu)
+    big = torch.zeros(64 << 20, device=gpu)   # 256 MB
+    for i in range(6):
+        with torch.cuda.stream(noise):
+            torch.cuda._sleep(20000 * (i + 1))   # one CU busy for ~10-60 us
+            for _ in range(2):
+                big.add_(1.0)
+        eng._run("fwd", st.cuda_stream)
+        eng._run_bwd(st.cuda_stream)
+        torch.cuda.synchronize()
+        assert not eng.persist_error()
+        assert torch.equal(eng.grad, ref), f"run {i}: gradient differs under concurrent load"
