@@ -194,7 +194,7 @@ class Engine:
         # 0.994 / 1.017 / 1.011, bs64 1.128 / 1.131 / 1.131 / 1.130, bs128 1.326 / 1.316 /
         # 1.314 / 1.303 (scripts/ab_tail.sh).  ImageNet, after the streaming 1x1 kernels
         # shortened the main stream's chain: RN50 bs128 1 / 0.5 / 0.25 = 10.56 / 10.49 /
-        # 10.49 ms, RN101 bs256 1 / 0.5 = 32.78 / 32.66 ms (scripts/gpu_r3_final.sh).
+        # 10.49 ms, RN101 bs256 1 / 0.5 = 32.78 / 32.66 ms (scripts/gpurun/gpu_r3_final.sh).
         tm = tune.get("tail_main")
         if tm < 0:
             tm = 1.0 if spec.dataset.startswith("cifar") else 0.5

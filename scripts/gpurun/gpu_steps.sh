@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Run GPU steps in order, each under its own time limit; stop at the first step
 # that faults/aborts/times out (rc not in {0,1}) so nothing else touches the GPU
-# after a fault.  Usage: scripts/gpu_steps.sh SECONDS "cmd1" SECONDS "cmd2" ...
+# after a fault.  Usage: scripts/gpurun/gpu_steps.sh SECONDS "cmd1" SECONDS "cmd2" ...
 # Logs go to gpurun_out/step_<n>.log.
 set -u
 mkdir -p gpurun_out
