@@ -89,6 +89,35 @@ def local_device_index() -> int:
     return local % n if n > 0 else local
 
 
+_STREAMS: dict = {}
+
+
+def engine_streams(device: torch.device):
+    """The engine's side (weight-gradient) and comm (all-reduce) streams of `device`,
+    created once per process.
+
+    Created BEFORE the c10d NCCL group and RCCL set up their own streams: a stream's
+    hardware queue is assigned at creation (GPU_MAX_HW_QUEUES = 4), and created after
+    RCCL's eight internal streams the side stream landed on the main stream's queue and
+    the comm stream on a queue shared with RCCL's proxy copies (rocprofv3 queue ids,
+    profiles/stream_queues.md).  DistContext calls this before init_process_group; the
+    engine takes the same pair."""
+    key = (device.type, device.index)
+    if key not in _STREAMS and device.type == "cuda" and not os.environ.get("DTR_LATE_STREAMS"):
+        pair = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+        # a stream is bound to its hardware queue at its first dispatch: dispatch on the
+        # default stream and on both engine streams now, before RCCL's streams do
+        torch.zeros(1, device=device)
+        for s in pair:
+            with torch.cuda.stream(s):
+                torch.zeros(1, device=device)
+        torch.cuda.synchronize(device)
+        _STREAMS[key] = pair
+    if key not in _STREAMS:   # (DTR_LATE_STREAMS: the old creation order, for the rehearsal A/B)
+        return torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
+    return _STREAMS[key]
+
+
 def gpu_shared_by_ranks() -> bool:
     """Whether this node's ranks are folded onto fewer GPUs than ranks (the one-GPU
     rehearsals).  Kernels that need every workgroup co-resident (the persistent CIFAR
@@ -110,6 +139,8 @@ class DistContext:
         self.timeout_s = float(timeout_s)
         self.comm_fallback_reason = None
         self.initialized_here = False
+        if device is not None and device.type == "cuda":
+            engine_streams(device)   # before RCCL's streams: distinct hardware queues
         if self.world_size > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")

@@ -224,8 +224,10 @@ class Engine:
         self.mom = torch.zeros(self.params.n_train, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
         self.scalars = torch.zeros(8, device=dev)  # loss_sum, correct, lr, l2
-        self.side = torch.cuda.Stream(device=dev)   # weight-gradient stream
-        self.comm_stream = torch.cuda.Stream(device=dev)   # RCCL all-reduces
+        # weight-gradient and all-reduce streams: one pair per process, created before
+        # the process group's (parallel/dist.py engine_streams: hardware queue order)
+        from ..parallel.dist import engine_streams
+        self.side, self.comm_stream = engine_streams(dev)
         # Native communicator (csrc/comm.h: RCCL, or the shm rehearsal transport):
         # the bucket all-reduces are plan ops on the comm stream.  None: world 1
         # (nothing to reduce), the c10d transport, or a fallback after a failed
