@@ -723,17 +723,21 @@ static void launch_flags(const GemmArgs& a, hipStream_t s) {
   }
 }
 
-// Tile selection by output width; BM shrinks for small M so the grid still
-// covers the 256 CUs.  Shared by the launcher and by the host (the BN-stat
-// partial buffer has one row per M tile).  Row thresholds: tune.h.
+// Tile selection: one function of (rows M = images x output pixels, output columns).
+// BM shrinks with M so the grid still covers the 256 CUs.  Shared by the launcher and
+// by the host (the BN-stat partial buffer has one row per M tile).  The narrow-column
+// rows are the CIFAR shapes, measured per per-rank batch on MI355X (CIFAR RN50 step,
+// round 3; these replaced the smallc_bm16/32 and c16_mid/c32_mid keys):
+//   16 columns (32x32 maps): 256 rows from 128 images (M >= 131072), 128 from 32 images
+//     (bs64 1.233 -> 1.08 ms against 64), 64 below;
+//   32 columns (16x16 maps): 128 rows from 32768 rows (bs128 1.303 -> 1.273 ms against
+//     64), 64 below;
+//   64 columns: 128 rows from 32768, else 64.
+// Per-rank CIFAR batches <= 240 take the persistent step instead (train/persist.py).
 int conv_gemm_bm(int M, int nc) {
   const long m = M;
-  long b16 = tune(T_SMALLC_BM16), b32 = tune(T_SMALLC_BM32);
-  if (b16 != 256 && b16 != 128 && b16 != 64) b16 = 256;
-  if (b32 != 128 && b32 != 64) b32 = 128;
-  const long mid16 = tune(T_C16_MID), mid32 = tune(T_C32_MID);
-  if (nc <= 16) return m >= 256L * 512 ? (int)b16 : (mid16 >= 0 && m >= mid16) ? 128 : 64;
-  if (nc <= 32) return m >= 128L * 512 ? (int)b32 : (mid32 >= 0 && m >= mid32) ? 128 : 64;
+  if (nc <= 16) return m >= 256L * 512 ? 256 : m >= 32768 ? 128 : 64;
+  if (nc <= 32) return m >= 32768 ? 128 : 64;
   if (nc <= 64) return m >= 128L * 256 ? 128 : 64;
   return (m >= tune(T_BM128_MIN) && nc % 128 == 0) ? 128 : 64;
 }

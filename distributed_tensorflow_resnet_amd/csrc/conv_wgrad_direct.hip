@@ -200,12 +200,21 @@ static void wgd_launch(const WgradArgs& a0, hipStream_t s) {
 
 void set_wgrad_direct(int enabled) { tune_set(T_DIRECT_WGRAD, enabled ? 1 : 0); }
 
-// Workgroups the direct kernel should at least launch (tune wgd_target): below it
-// the tile shrinks (fewer pixels per split, then fewer taps per workgroup).  At 16-32
-// images per rank (the 8-GPU strong-scaling share of the global batch 128) the
-// bs128-tuned tiles left 12-32 workgroups per stage-3/2 wgrad, ~10 us each, and the
-// side stream became the backward's critical path.
-static int wgd_target() { return (int)tune(T_WGD_TARGET); }
+// Workgroups the direct kernel should at least launch: below it the tile shrinks (fewer
+// pixels per split, then fewer taps per workgroup).  At 16-32 images per rank (the
+// 8-GPU strong-scaling share of the global batch 128) the bs128-tuned tiles left 12-32
+// workgroups per stage-3/2 wgrad, ~10 us each, and the side stream became the
+// backward's critical path.
+static int wgd_target() { return 96; }
+
+// Pixels per split by (channels, pixels) -- the selection that replaced the wgd_bmp16 /
+// 32 / 64 keys, measured on the CIFAR RN50 step (MI355X, round 3): 512 for 16 and 32
+// channels (256 -> 512: bs128 1.396 -> 1.320 ms); 64 channels 256, or 0 = the split-K
+// implicit-GEMM wgrad at <= 1024 pixels (16 images: bs16 step 0.928 -> 0.919 ms).
+static int wgd_bmp_for(int C, long P) {
+  if (C == 16 || C == 32) return 512;
+  return P <= 1024 ? 0 : 256;
+}
 
 // smallest pixel tile instantiated per channel count
 static int wgd_min_bmp(int C) { return C == 16 ? 128 : 64; }
@@ -226,16 +235,11 @@ int wgrad_direct_bmp(const ConvGeom& g) {
       g.Ho != g.H || g.Wo != g.W)
     return 0;
   // pixels per split (= per workgroup): larger -> fewer split-K slabs for the grouped
-  // reduce to read, fewer workgroups (tune wgd_bmp16 / 32 / 64)
-  int bmp = 0;
-  if (g.C == 16 && g.W == 32) bmp = (int)tune(T_WGD_BMP16);
-  else if (g.C == 32 && g.W == 16) bmp = (int)tune(T_WGD_BMP32);
+  // reduce to read, fewer workgroups
   const long P = (long)g.N * g.H * g.W;
-  if (g.C == 64 && g.W == 8) {
-    bmp = (int)tune(T_WGD_BMP64);
-    // -1 auto: at 16 images (1024 pixels) the split-K implicit-GEMM wgrad wins
-    if (bmp < 0) bmp = P <= 1024 ? 0 : 256;
-  }
+  int bmp = 0;
+  if ((g.C == 16 && g.W == 32) || (g.C == 32 && g.W == 16) || (g.C == 64 && g.W == 8))
+    bmp = wgd_bmp_for(g.C, P);
   const int lo = wgd_min_bmp(g.C);               // smallest instantiated tile
   const int hi = g.C == 16 ? 1024 : g.C == 32 ? 512 : 256;
   if (bmp < lo || bmp > hi || (bmp & (bmp - 1))) return 0;

@@ -27,12 +27,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"nbuf1_kt", 1,
      "single-buffered LDS for K loops of <= this many 64-wide tiles: the 64-channel 1x1 convs "
      "fit 4 workgroups per CU instead of 2"},
-    {"smallc_bm16", 256, "tile rows of the large-M 16-column convs (CIFAR stage 1 at 128 images)"},
-    {"smallc_bm32", 128, "tile rows of the large-M 32-column convs (CIFAR stage 2)"},
-    {"c16_mid", 32768,
-     "rows from which mid-size 16-column grids use 128-row tiles (CIFAR RN50 bs64 1.233 -> "
-     "1.08 ms)"},
-    {"c32_mid", 32768, "likewise for 32 columns (CIFAR RN50 bs128 1.303 -> 1.273 ms)"},
     {"bm128_min", 4096,
      "rows from which >= 128-column convs use 128x128 tiles (7x7 fwd 118 -> 87 us)"},
     {"parity_dgrad", 1,
@@ -48,13 +42,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"direct_wgrad", 1, "direct halo wgrad for the CIFAR 3x3 shapes"},
     {"wgd_wt", 1,
      "direct wgrad split partials stored write-through (bs128 step 1.315 -> 1.302 ms)"},
-    {"wgd_target", 96,
-     "workgroups the direct wgrad launches at least (small per-rank batches shrink its tiles)"},
-    {"wgd_bmp16", 512, "direct wgrad pixels per split, 16 channels (256 -> 512: 1.396 -> 1.320 ms)"},
-    {"wgd_bmp32", 512, "... 32 channels"},
-    {"wgd_bmp64", -1,
-     "... 64 channels, -1 auto: 256, or the implicit-GEMM wgrad at <= 1024 pixels (bs16 "
-     "step 0.928 -> 0.919 ms; bs128 1.277 vs 1.282 kept)"},
     {"wgrad_target_wg", 768,
      "split-K wgrad: target workgroups (3 per CU hide the per-tile load latency)"},
     {"wgrad_slab_mb", 16,

@@ -17,10 +17,6 @@ enum TuneId : int {
   T_SPLITK_TILES,      // largest grid (tiles) that is split
   T_DGRAD_SPLITK,      // 7x7 dgrads: FAST loop once split-K doubles their grid
   T_NBUF1_KT,          // single-buffered LDS for K loops of <= this many tiles
-  T_SMALLC_BM16,       // tile rows of the large-M 16-column convs
-  T_SMALLC_BM32,       // ... of the 32-column convs
-  T_C16_MID,           // rows from which mid-size 16-column grids use 128-row tiles
-  T_C32_MID,           // ... 32-column
   T_BM128_MIN,         // rows from which 128x128 tiles are used (>= 128 columns)
   T_PARITY_DGRAD,      // stride-2 dgrads as 4 output-parity classes
   T_DIRECT_CONV,       // direct halo 3x3 kernel for the CIFAR shapes
@@ -28,10 +24,6 @@ enum TuneId : int {
   T_DIRECT_LDSW,       // its weight staging through LDS, mask of C16/C32/C64
   T_DIRECT_WGRAD,      // direct halo wgrad for the CIFAR shapes
   T_WGD_WT,            // its split partials stored write-through
-  T_WGD_TARGET,        // workgroups the direct wgrad should at least launch
-  T_WGD_BMP16,         // its pixel tile per split, 16 / 32 / 64 channels (0 auto)
-  T_WGD_BMP32,
-  T_WGD_BMP64,
   T_WGRAD_TARGET_WG,   // split-K wgrad: target workgroups
   T_WGRAD_SLAB_MB,     // split-K wgrad: cap of one layer's fp32 partial slabs (MB)
   T_FIN_V,             // BN finalize kernel variant (-1 auto)

@@ -103,7 +103,7 @@ def engine_streams(device: torch.device):
     profiles/stream_queues.md).  DistContext calls this before init_process_group; the
     engine takes the same pair."""
     key = (device.type, device.index)
-    if key not in _STREAMS and device.type == "cuda" and not os.environ.get("DTR_LATE_STREAMS"):
+    if key not in _STREAMS and device.type == "cuda":
         pair = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
         # a stream is bound to its hardware queue at its first dispatch: dispatch on the
         # default stream and on both engine streams now, before RCCL's streams do
@@ -113,7 +113,7 @@ def engine_streams(device: torch.device):
                 torch.zeros(1, device=device)
         torch.cuda.synchronize(device)
         _STREAMS[key] = pair
-    if key not in _STREAMS:   # (DTR_LATE_STREAMS: the old creation order, for the rehearsal A/B)
+    if key not in _STREAMS:
         return torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
     return _STREAMS[key]
 

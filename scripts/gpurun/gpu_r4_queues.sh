@@ -7,8 +7,7 @@ set -o pipefail
 for order in early late; do
   for cfg in "cifar_resnet50 32" "imagenet_resnet50 64"; do
     set -- $cfg
-    if [ $order = late ]; then export DTR_LATE_STREAMS=1; else unset DTR_LATE_STREAMS; fi
-    timeout -k 10 240 rocprofv3 --kernel-trace --hip-runtime-trace -d gpurun_out/queues_${order}_$1 -o run -- python3 scripts/stream_rehearsal.py $1 $2 6 > gpurun_out/queues_${order}_$1.log 2>&1 || { tail -20 gpurun_out/queues_${order}_$1.log; exit 1; }
+    timeout -k 10 240 rocprofv3 --kernel-trace --hip-runtime-trace -d gpurun_out/queues_${order}_$1 -o run -- python3 scripts/stream_rehearsal.py $1 $2 6 $order > gpurun_out/queues_${order}_$1.log 2>&1 || { tail -20 gpurun_out/queues_${order}_$1.log; exit 1; }
     echo "$order $1: $(grep -E 'STREAMS' gpurun_out/queues_${order}_$1.log)"
   done
 done

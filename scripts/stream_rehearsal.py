@@ -8,7 +8,9 @@ all-reduce per step like the metrics / timing reductions of bench.py.  Run it un
 ``rocprofv3 --kernel-trace --hip-runtime-trace`` and summarise the trace with
 ``scripts/queue_table.py``: every stream's hardware queue id.
 
-usage: python scripts/stream_rehearsal.py MODEL BATCH STEPS"""
+usage: python scripts/stream_rehearsal.py MODEL BATCH STEPS [late]
+(late: the round-3 order -- engine streams created and first used after the process
+group -- for the A/B in profiles/stream_queues.md)"""
 import os
 import sys
 
@@ -30,10 +32,16 @@ def main():
     os.environ.setdefault("MASTER_PORT", "29561")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    ctx0 = DistContext(device=dev)   # (world 1: creates the engine streams, like a rank does)
+    late = len(sys.argv) > 4 and sys.argv[4] == "late"
+    if not late:
+        ctx0 = DistContext(device=dev)   # (world 1: creates the engine streams, like a rank does)
+        del ctx0
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    if late:
+        from distributed_tensorflow_resnet_amd.parallel import dist as dmod
+        dmod._STREAMS[(dev.type, dev.index)] = (torch.cuda.Stream(device=dev),
+                                               torch.cuda.Stream(device=dev))
     ctx = DistContext(device=dev)
-    del ctx0
     spec = build_spec(dataset, size)
     cifar = dataset.startswith("cifar")
     eng = Engine(spec, batch, weight_decay=2e-4 if cifar else 1e-4,
