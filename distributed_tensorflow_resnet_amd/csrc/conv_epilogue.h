@@ -8,6 +8,11 @@ namespace dtr {
 
 enum { F_PRE = 1, F_STATS = 2, F_BNB = 4, F_ABWD = 8 };
 
+// The epilogue's thread index: 256 threads per tile.  The 512-thread 8-wave ring kernel
+// (conv_ring8.hip) runs two epilogues side by side, one per 128-row half of its
+// 256-row tile (waves 0-3 and 4-7, the same barriers in lockstep), each on its own LDS.
+__device__ __forceinline__ int ep_tid() { return (int)(threadIdx.x & 255); }
+
 // Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
 // it fits in 64 KiB (one phase), else one wave-row per phase (128x128 tiles).
 template <int BM, int BN, int WM>
@@ -39,7 +44,7 @@ __device__ __forceinline__ void welford_combine(const float* src, int NC, int n0
                                                 float* red, float* red2, float* red3,
                                                 float& out_n, float& out_mu, float& out_m2) {
   constexpr int G = 256 / BN;
-  const int tid = threadIdx.x, c = tid % BN, q = tid / BN, col = n0 + c;
+  const int tid = ep_tid(), c = tid % BN, q = tid / BN, col = n0 + c;
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (col < NC) {
     float mv[FIN_UNROLL], qv[FIN_UNROLL];
@@ -88,7 +93,7 @@ template <int BN>
 __device__ __forceinline__ void sum_combine(const float* src, int NC, int n0, int first, int cnt,
                                             float* red, float* red2, float& o1, float& o2) {
   constexpr int G = 256 / BN;
-  const int tid = threadIdx.x, c = tid % BN, q = tid / BN, col = n0 + c;
+  const int tid = ep_tid(), c = tid % BN, q = tid / BN, col = n0 + c;
   float a1 = 0.f, a2 = 0.f;
   if (col < NC) {
     float v1[FIN_UNROLL], v2[FIN_UNROLL];
@@ -166,7 +171,7 @@ __device__ __forceinline__ float lanes_colsum(float v) {
 template <int CPR, int BN>
 __device__ __forceinline__ void colsum8(float (&v)[8], float* wred) {
   static_assert(CPR >= 1 && CPR <= 16 && (CPR & (CPR - 1)) == 0, "CPR");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = ep_tid() & 63, wave = ep_tid() >> 6;
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = lanes_colsum<CPR>(v[j]);
   if (lane < CPR) {
@@ -181,7 +186,7 @@ template <int CPR, int BN>
 __device__ __forceinline__ void colsum8x2(float (&v)[8], float (&w)[8], float* wred,
                                           float* wred2) {
   static_assert(CPR >= 1 && CPR <= 16 && (CPR & (CPR - 1)) == 0, "CPR");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = ep_tid() & 63, wave = ep_tid() >> 6;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     v[j] = lanes_colsum<CPR>(v[j]);
@@ -233,7 +238,7 @@ __device__ __forceinline__ void epi_prefetch(const GemmArgs& args, const int m0,
   using EL = EpiLayout<BM, BN, WM>;
   using PP = EpiPre<BM, BN, WM, XO>;
   if constexpr (PP::ON) {
-    const int tid = threadIdx.x;
+    const int tid = ep_tid();
     const int cc = tid % EL::CPR, r0 = tid / EL::CPR;
     const int col0 = n0 + cc * 8;
     const bf16x8 zero8 = {};
@@ -316,7 +321,11 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs& args, f32x4 (&acc
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN
 // backward sums (BNB) and the optional last-arriver finalize.  Entered after a
 // workgroup barrier (the caller's LDS is dead).
-template <int BM, int BN, int WM, int WN, int FLAGS, bool XO = false>
+// SYNC_ALL (the two side-by-side epilogues of conv_ring8.hip): every phase runs, rows
+// past M included (as no-ops), so both halves pass the same barriers; the caller then
+// uses accumulator-mode BN statistics / sums only (no per-tile partial rows, no
+// last-arriver finalize).
+template <int BM, int BN, int WM, int WN, int FLAGS, bool XO = false, bool SYNC_ALL = false>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
                                               f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                               char* smem, const int m0, const int n0,
@@ -331,7 +340,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MR = WTM / 16, NR = WTN / 16;
   const int M = args.M, NC = args.Ncol;
-  const int tid = threadIdx.x;
+  const int tid = ep_tid();
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fq = lane >> 4;
@@ -382,7 +391,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
   for (int ph = 0; ph < EL::PHASES; ++ph) {
     const int prow0 = m0 + ph * EL::PR;
     const int nph = min(EL::PR, M - prow0);   // block-uniform
-    if (nph <= 0) break;
+    if (nph <= 0 && !SYNC_ALL) break;
     // Operand loads of this phase's rows, all issued before the staging writes and
     // the barrier so they overlap them (one round trip, not one per row iteration);
     // kernels that prefetched them at kernel start (EpiPre) skip this.
@@ -556,7 +565,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
     if (args.probe && tid == 0) args.probe[8 * (tile_m + gridDim.x * tile_n) + 5] = wall_clock64();
     if constexpr (STATS) {
       colsum8x2<EL::CPR, BN>(p1, p2, red, red2);
-      if (tid < BN) {
+      if (tid < BN && nph > 0) {
         const float sd = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
         const float sdd = red2[tid] + red2[BN + tid] + red2[2 * BN + tid] + red2[3 * BN + tid];
         const float nb = (float)nph, dm = sd / nb;
@@ -570,7 +579,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs& args,
       }
     }
     if constexpr (BNB) {
-      if (ph == EL::PHASES - 1 || prow0 + EL::PR >= M) {   // last phase: reduce before storing
+      if (ph == EL::PHASES - 1 || (!SYNC_ALL && prow0 + EL::PR >= M)) {   // last phase: reduce
         colsum8x2<EL::CPR, BN>(s1, s2, red, red2);   // both sums behind one barrier
         if (tid < BN) {
           bnb_t1 = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];

@@ -199,6 +199,11 @@ int conv_gemm_bm(int M, int Ncol);
 // caller's grid (split-K / parity set up by the caller, conv_gemm.hip)
 bool conv_ring_covers(const GemmArgs& a, int mode);
 void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
+// 8-wave 256 x 128 tile, 3-stage ring for the deep-K (>= 1152) convs (conv_ring8.hip)
+bool conv_ring8_covers(const GemmArgs& a, int mode);
+void conv_ring8(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
+size_t conv_ring8_lds();
+bool conv_gemm_uses_ring8(const GemmArgs& a, int mode);   // (parity classes resolved)
 bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 

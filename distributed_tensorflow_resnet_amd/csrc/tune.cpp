@@ -13,6 +13,7 @@ namespace dtr {
 
 namespace {
 
+// one entry per TuneId, in the enum order of tune.h
 const TuneEntry kTable[T_COUNT] = {
     {"conv_pipe", 1,
      "2-deep pipelined (FAST) implicit-GEMM / wgrad loops where they pay: K loops >= 4 tiles, "
@@ -75,6 +76,9 @@ const TuneEntry kTable[T_COUNT] = {
     {"ring_kt_dgrad", 4,
      "ring dgrads from this many 64-deep K tiles (the 4-tile 14x14 1024->256 dgrad: 75.8 -> "
      "68.8 us on the ring)"},
+    {"ring8", 1,
+     "8-wave 256x128-tile 3-stage LDS-DMA ring (conv_ring8.hip) for the 3x3 convs with K >= 1024 "
+     "(the 3x3 layers of stages 2-4)"},
 };
 
 std::atomic<long> g_val[T_COUNT];

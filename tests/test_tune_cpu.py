@@ -104,3 +104,19 @@ def test_dtr_tune_parsing_and_validation(monkeypatch):
     monkeypatch.setenv("DTR_TUNE", "fork_every=2.5")
     with pytest.raises(ValueError, match="integer is required"):
         tune.get("fork_every")
+
+
+def test_native_table_follows_the_enum_order():
+    """csrc/tune.cpp's kTable is indexed by TuneId: entry i must be the key of enum entry
+    i (T_FOO_BAR <-> "foo_bar"), or tune(T_X) silently reads another knob."""
+    import re
+
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "distributed_tensorflow_resnet_amd", "csrc")
+    h = open(os.path.join(root, "tune.h")).read()
+    enum = re.search(r"enum TuneId : int \{(.*?)\};", h, re.S).group(1)
+    names = [n.lower()[2:] for n in re.findall(r"\b(T_[A-Z0-9_]+)", enum) if n != "T_COUNT"]
+    cpp = open(os.path.join(root, "tune.cpp")).read()
+    table = cpp[cpp.index("kTable[T_COUNT]"):cpp.index("std::atomic<long> g_val")]
+    keys = re.findall(r'\{"([a-z0-9_]+)",', table)
+    assert keys == names
