@@ -1229,6 +1229,8 @@ PYBIND11_MODULE(_C, m) {
     return conv_gemm_uses_ring8(g, mode);
   }, "whether conv_gemm(mode, geom) (no prologue, accumulator-mode BN sums) runs the 8-wave "
      "256x128 ring (conv_ring8.hip)");
+  m.def("set_ring8_probe", [](ptr_t p) { set_ring8_probe(P<long long>(p)); },
+        "diagnostics: conv_ring8 workgroup 0 writes its timeline (53 wall-clock stamps) to p");
   m.def("set_direct_probe", [](ptr_t p) { set_direct_probe(P<long long>(p)); },
         "diagnostics: direct-conv workgroups write 4 wall-clock stamps each to p (0 = off)");
   m.def("set_wgrad_direct", &set_wgrad_direct,

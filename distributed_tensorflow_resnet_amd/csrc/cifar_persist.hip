@@ -67,7 +67,8 @@ struct Stg {                                  // stage S: R x R maps, C channels
   static constexpr int PBW = NPB >= NW ? NPB / NW : 1;   // pixel blocks per wave
   static constexpr int CBW = NCB / WPB > 0 ? NCB / WPB : 1;   // channel blocks per wave
   static constexpr int TPW = PBW * CBW;                  // 16x16 tiles per wave
-  static constexpr bool ALL = NPB * NCB >= NW;           // every wave holds tiles
+  static constexpr int NT = NPB * NCB;                   // 16x16 output tiles
+  static constexpr bool ALL = NT >= NW;                  // every wave holds tiles
   static constexpr bool CLS = R > 8;                     // parity-class-major pixel order
   static_assert(RS >= 2 && (!CLS || RS % 2 == 0) && NPX % 16 == 0 && TPW <= 8, "slices");
   static_assert(!CLS || (NPB / 4) % PBW == 0, "a wave's pixel blocks lie in one class");
@@ -304,15 +305,27 @@ __device__ __forceinline__ WLoad wl_dgrad(const bf16* src, int co, int ci, int k
 // w*STR + s - PAD), PAD = 1 for 3x3 (TF fixed padding), 0 for 1x1.
 // Stride-1 dgrad (FLIP = true, 3x3): input (h + 1 - r, w + 1 - s) of the output gradient.
 // Weights in LDS: [channel][k = tap * CI + ci] rows of KP.
+// When the slice has fewer output tiles than waves (stage 3 at 4 slices: 4 tiles), the
+// idle waves take half of each tile's k-steps (SPLIT) and their partial sums are added
+// through the LDS scratch `xred` (two barriers; every wave calls this function).
 template <int SO, int P, int CI, int KSZ, int STR, bool FLIP>
 __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const bf16* wl,
-                                         int kslice, int wave, int lane) {
+                                         int kslice, int wave, int lane, float* xred) {
   using G = Stg<SO, P>;
   lane = opaque_v(lane);
-  if (!wave_active<SO, P>(wave)) return;
   constexpr int RI = G::R * STR, RSI = G::RS * STR, W2I = RI + 2, UI = CI >= 8 ? CI / 8 : 1;
   constexpr int K = KSZ * KSZ * CI, KS = (K + 31) / 32, KP = kpad_of(K);
   constexpr int PAD = KSZ == 3 ? 1 : 0;
+  constexpr bool SPLIT = !G::ALL && KS >= 4 && NW % G::NT == 0;
+  constexpr int WPT = SPLIT ? NW / G::NT : 1;   // waves per tile
+  static_assert(!SPLIT || (G::TPW == 1 && G::NT * 256 * (WPT - 1) <= 8 * 128), "split scratch");
+  int kh = 0;
+  if constexpr (SPLIT) {
+    kh = wave / G::NT;
+    wave = wave % G::NT;
+  } else if (!wave_active<SO, P>(wave)) {
+    return;
+  }
   const int fr = lane & 15, fq = lane >> 4;
   int hb[G::PBW], hcb[G::PBW];
 #pragma unroll
@@ -327,7 +340,7 @@ __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const
   int cb0, pb0;
   tile_of<SO, P>(wave, 0, pb0, cb0);
 #pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
+  for (int ks = kh; ks < KS; ks += WPT) {
     const int k = ks * 32 + fq * 8;
     int tap = k / CI;
     const int c = k - tap * CI;
@@ -343,6 +356,16 @@ __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const
 #pragma unroll
       for (int j = 0; j < G::CBW; ++j) acc[i * G::CBW + j] = mfma16(a[j], b, acc[i * G::CBW + j]);
     }
+  }
+  if constexpr (SPLIT) {   // partial sums of waves kh > 0 -> the tile's kh = 0 wave
+    if (kh > 0) *reinterpret_cast<f32x4*>(xred + ((kh - 1) * G::NT + wave) * 256 + lane * 4) = acc[0];
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int j = 1; j < WPT; ++j)
+        acc[0] += *reinterpret_cast<const f32x4*>(xred + ((j - 1) * G::NT + wave) * 256 + lane * 4);
+    }
+    __syncthreads();   // (xred is the BN sums' scratch next)
   }
 }
 
@@ -871,11 +894,11 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   f32x4 acc[8];
   if constexpr (PROJ) {
     zero_acc(acc);
-    conv_acc<S, P, GI::C, 1, STR, false>(acc, x.m.ha, x.m.w2, x.kslice, wave, lane);
+    conv_acc<S, P, GI::C, 1, STR, false>(acc, x.m.ha, x.m.w2, x.kslice, wave, lane, x.m.red);
     round_acc<S, P, false>(pr, acc, pr);
   }
   zero_acc(acc);
-  conv_acc<S, P, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+  conv_acc<S, P, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane, x.m.red);
   round_acc<S, P, false>(hr, acc, hr);
   probe(x, 3);
   publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
@@ -897,7 +920,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   __syncthreads();
   probe(x, 8);
   zero_acc(acc);
-  conv_acc<S, P, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
+  conv_acc<S, P, G::C, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane, x.m.red);
   if constexpr (PROJ) round_acc<S, P, true>(xr, acc, pr);
   else round_acc<S, P, true>(xr, acc, xr);
   probe(x, 9);
@@ -959,7 +982,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
   {
     f32x4 acc[8];
     zero_acc(acc);
-    conv_acc<0, P, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, x.wave, x.lane);
+    conv_acc<0, P, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, x.wave, x.lane, x.m.red);
     round_acc<0, P, false>(xr, acc, xr);
     publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
@@ -1230,7 +1253,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   probe(x, 1);
   f32x4 acc[8];
   zero_acc(acc);
-  conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, x.kslice, wave, lane);
+  conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.hb, x.m.w1, x.kslice, wave, lane, x.m.red);
   bf16x4 da[8];
   round_acc<S, P, false>(da, acc, da);
   probe(x, 3);
@@ -1270,8 +1293,8 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     dgrad_s2_acc<SI, P, G::C, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
     dgrad_s2_acc<SI, P, G::C, true>(acc, x.m.hb, x.m.w2, x.kslice, wave, lane);
   } else {
-    conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane);
-    if constexpr (PROJ) conv_acc<S, P, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, x.kslice, wave, lane);
+    conv_acc<S, P, G::C, 3, 1, true>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane, x.m.red);
+    if constexpr (PROJ) conv_acc<S, P, G::C, 1, 1, false>(acc, x.m.hb, x.m.w2, x.kslice, wave, lane, x.m.red);
   }
   round_acc<SI, P, false>(da, acc, da);
   probe(x, 9);
@@ -1533,7 +1556,7 @@ void prn_set_probe(long long* p) { g_prn_probe = p; }
 size_t prn_lds_bytes() { return LDS_TOTAL; }
 
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad) {
-  return N >= 1 && (P == 1 || P == 2 || P == 4) && N * P <= 224 && nblocks >= 3 && nblocks % 3 == 0 &&
+  return N >= 1 && (P == 1 || P == 2 || P == 4) && N * P <= 256 && nblocks >= 3 && nblocks % 3 == 0 &&
          classes >= 1 && classes <= kpad && kpad <= 64 && kpad % 16 == 0;
 }
 

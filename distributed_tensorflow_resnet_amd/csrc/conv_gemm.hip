@@ -672,7 +672,14 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
         if (ring && conv_ring8_covers(a, MODE)) {   // deep K: 8-wave 256 x 128 ring
           dim3 g8((a.M + 255) / 256, (a.Ncol + 127) / 128, a.par ? 4 : 1);
           const long tiles8 = (long)g8.x * g8.y;
-          const int S = a.par ? 1 : pick_ksplit(tiles8, (a.Kdim + 63) / 64);
+          // one workgroup per CU: split only while the slices still fit in one round of
+          // the CUs (the 14x14 grid's 196 tiles run unsplit; 2 slices would be 392
+          // workgroups, a second round 53 % full)
+          int S = 1;
+          const int kt8 = (a.Kdim + 63) / 64;
+          while (!a.par && S * 2 <= tune(T_SPLITK) && tiles8 * S * 2 <= cu_count() &&
+                 kt8 / (S * 2) >= 8)
+            S *= 2;
           const size_t need = (size_t)S * tiles8 * 256 * 128 * sizeof(float);
           if (g_sk_query) {
             if (S > 1) {

@@ -102,6 +102,12 @@ conv_ring8_kernel(GemmArgs args) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ConvGeom& g = args.g;
+  // diagnostics (set_ring8_probe): workgroup (0, 0, 0)'s lane 0 stamps the wall clock at
+  // start [0], after the prologue [1], after each K tile's MFMAs [2 + t] (t < 48), after
+  // the loop [50], after the split-K combine [51] and at the end [52]
+  long long* const kp = (args.kprobe != nullptr && blockIdx.x == 0 && blockIdx.y == 0 &&
+                         blockIdx.z == 0 && threadIdx.x == 0) ? args.kprobe : nullptr;
+  if (kp) kp[0] = wall_clock64();
   // XCD-aware order (T1): consecutive tiles of one column block land on one XCD (whose
   // L2 then holds its B columns and neighbouring A rows).  Bijective for any count.
   const int nx = gridDim.x, ny = gridDim.y, nwg = nx * ny;
@@ -285,6 +291,7 @@ conv_ring8_kernel(GemmArgs args) {
 
   // ---- 3-stage ring: tiles t+1 and t+2 in flight during the MFMAs of tile t ----
   const int nt = t_end - t_beg;
+  if (kp) kp[1] = wall_clock64();
   if (nt > 0) issue(0);
   if (nt > 1) issue(1);
   int rd = 0;
@@ -297,10 +304,13 @@ conv_ring8_kernel(GemmArgs args) {
     if (t + 2 < nt) issue(rd == 0 ? 2 : rd - 1);
     mma_stage(rd);
     rd = rd == 2 ? 0 : rd + 1;
+    if (kp && t < 48) kp[2 + t] = wall_clock64();
   }
   __syncthreads();   // every wave's MFMA reads are done: the epilogue reuses the LDS
+  if (kp) kp[50] = wall_clock64();
 
   if (sk_n > 1 && !r8_splitk_combine(args, acc, smem, tm * ny + tn, lz)) return;
+  if (kp) kp[51] = wall_clock64();
   char* hs = smem + half * R8_EPI_HALF;
   if constexpr (BNB)
     conv_epilogue<128, 128, 2, 2, FLAGS, true, true>(args, acc, hs, m0 + half * 128, n0, &epre,
@@ -308,6 +318,7 @@ conv_ring8_kernel(GemmArgs args) {
   else
     conv_epilogue<128, 128, 2, 2, FLAGS, false, true>(args, acc, hs, m0 + half * 128, n0,
                                                       nullptr, 2 * tm + half, tn);
+  if (kp) kp[52] = wall_clock64();
 }
 
 // ---------------------------------------------------------------------------
@@ -331,8 +342,13 @@ bool conv_ring8_covers(const GemmArgs& a, int mode) {
 
 size_t conv_ring8_lds() { return R8_LDS; }
 
+static long long* g_r8_probe = nullptr;
+void set_ring8_probe(long long* p) { g_r8_probe = p; }
+
 template <int MODE, int FLAGS>
-static void r8_launch(const GemmArgs& a, dim3 grid, hipStream_t s) {
+static void r8_launch(const GemmArgs& a0, dim3 grid, hipStream_t s) {
+  GemmArgs a = a0;
+  a.kprobe = g_r8_probe;
   hipLaunchKernelGGL((conv_ring8_kernel<MODE, FLAGS>), grid, dim3(512), R8_LDS, s, a);
   DTR_CHECK_LAUNCH();
 }

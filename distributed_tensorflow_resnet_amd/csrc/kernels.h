@@ -129,6 +129,7 @@ struct GemmArgs {
   ConvGeom g;
   int M, Ncol, Kdim;
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
+  long long* kprobe = nullptr;  // ring8: workgroup 0's phase / K-tile timeline (diagnostics)
   int wt = 0;                   // epilogue output stores write-through (sc1): tune wt_store
   // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
   // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
@@ -204,6 +205,7 @@ bool conv_ring8_covers(const GemmArgs& a, int mode);
 void conv_ring8(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
 size_t conv_ring8_lds();
 bool conv_gemm_uses_ring8(const GemmArgs& a, int mode);   // (parity classes resolved)
+void set_ring8_probe(long long* p);   // diagnostics: workgroup 0's timeline (nullptr = off)
 bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 

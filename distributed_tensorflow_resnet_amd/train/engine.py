@@ -1302,8 +1302,9 @@ class Engine:
                                self.gstep.data_ptr(), 1, 0, *zero)
         else:
             plan.memset(*zero)
-        ptrs, ints, floats = self.prn.args(self.prn_pool, self.prn_bar, BN_DECAY, BN_EPS)
+        ptrs, ints, floats = self.prn.args(self.prn_pool, self.prn_bar, BN_DECAY, BN_EPS, fwd=True)
         plan.prn(0, ptrs, ints, floats)
+        ptrs, ints, floats = self.prn.args(self.prn_pool, self.prn_bar, BN_DECAY, BN_EPS)
         self.seg["fwd"] = (b0, plan.size())
 
         b1 = plan.size()

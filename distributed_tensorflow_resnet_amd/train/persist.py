@@ -50,6 +50,18 @@ def slices_for(N: int, cus: int, override: int = -1) -> int:
     return 2 if N <= 64 and 2 * N + 32 <= cus else 1
 
 
+def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:
+    """Row slices per image of the forward launch.  The forward has no weight-gradient
+    workgroups to leave CUs for, and its slicing is independent of the backward's (both
+    launches exchange only whole NHWC tensors and global BN sums): 4 up to 16 images,
+    2 while 2N slices fit the CUs, else 1.  The engine's tune persist_slices overrides."""
+    if override in (1, 2, 4):
+        return override
+    if N <= 16 and 4 * N <= cus:
+        return 4
+    return 2 if 2 * N <= cus else 1
+
+
 def supported(eng) -> bool:
     """Whether the persistent kernels cover this engine's network and batch."""
     spec, nat = eng.spec, eng.nat
@@ -104,7 +116,8 @@ class PersistStep:
             r["acc"], r["bacc"] = e.acc.data_ptr(), e.bacc.data_ptr()
         self.bn_dev = self._dev(bn_rows)
         self.cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        self.P = slices_for(N, self.cus, eng.persist_slices)
+        self.P = slices_for(N, self.cus, eng.persist_slices)          # backward
+        self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.dpool = torch.zeros((N, 64), device=dev)
         self.dx0 = torch.empty_like(eng.X[0])
@@ -204,7 +217,9 @@ class PersistStep:
                            s.cout, s.cout, s.kh * s.kw, c.cin, c.cin_valid)
         return out
 
-    def args(self, pool_ptr: int, bar_ptr: int, bn_decay: float, bn_eps: float):
+    def args(self, pool_ptr: int, bar_ptr: int, bn_decay: float, bn_eps: float,
+             fwd: bool = False):
+        """Plan-op arguments of the forward (fwd) or backward launch."""
         eng, spec = self.eng, self.eng.spec
         ptrs = [self.block_dev.data_ptr(), self.bn_dev.data_ptr(), eng.x_in.data_ptr(),
                 eng.convs[spec.stem.name].ohwi, pool_ptr,
@@ -212,7 +227,8 @@ class PersistStep:
                 eng.labels.data_ptr(), eng.pooled.data_ptr(), eng.dlogits.data_ptr(),
                 eng.xent_ws.data_ptr(), self.dpool.data_ptr(), self.dx0.data_ptr(),
                 self.item_dev.data_ptr()]
-        ints = [self.nblocks, len(self.items), eng.N, self.P, spec.num_classes, eng.kpad, 1,
+        ints = [self.nblocks, len(self.items), eng.N, self.P_fwd if fwd else self.P,
+                spec.num_classes, eng.kpad, 1,
                 self.wgrad_wgs]
         floats = [1.0 / eng.global_batch, bn_decay, bn_eps]
         return ptrs, ints, floats

@@ -78,3 +78,17 @@ def test_gpu_shared_by_ranks(monkeypatch):
     assert gpu_shared_by_ranks()
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
     assert not gpu_shared_by_ranks()
+
+
+def test_persistent_slice_selection():
+    """Row slices per image of the persistent CIFAR step (train/persist.py): the backward
+    leaves >= 32 CUs for the weight-gradient workgroups, the forward may fill the chip,
+    and tune persist_slices overrides both."""
+    from distributed_tensorflow_resnet_amd.train.persist import fwd_slices_for, slices_for
+
+    assert [slices_for(n, 256) for n in (8, 16, 32, 64, 96, 128, 224)] == [4, 4, 2, 2, 1, 1, 1]
+    assert [fwd_slices_for(n, 256) for n in (8, 16, 32, 64, 96, 128, 200)] == [4, 4, 2, 2, 2, 2, 1]
+    assert slices_for(128, 256, 2) == 2 and fwd_slices_for(16, 256, 1) == 1
+    for n in range(1, 241):
+        assert n * slices_for(n, 256) + 16 <= 256
+        assert n * fwd_slices_for(n, 256) <= 256
