@@ -218,7 +218,10 @@ conv_ring8_kernel(GemmArgs args) {
   int it_tl = t_beg / cpt;
   int it_c = (t_beg - it_tl * cpt) * BK;
   int it_ta = it_tl / taw, it_tb = it_tl - it_ta * taw;
-  auto issue = [&](int stage) {   // next tile -> stage: 4 A + 2 B DMAs per wave
+  // next tile -> stage: 4 A + 2 B DMAs per wave, in two halves (part 0: A 0-1 + B 0,
+  // part 1: A 2-3 + B 1, then the tap walk advances) so the loop can put each half in
+  // front of one k-step's MFMAs instead of issuing all six in one burst
+  auto issue_part = [&](int stage, int part) {
     const int a_pix = MODE == MODE_FWD ? it_ta * g.W + it_tb : -(it_ta * g.Wo + it_tb);
     const int sa = (a_pix * Acin + it_c) * 2;
     int sb;
@@ -230,17 +233,17 @@ conv_ring8_kernel(GemmArgs args) {
     }
     char* st = smem + stage * R8_STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 2; ++j) {
+      const int i = 2 * part + j;
       const bool ok = (a_mask[i] >> it_tl) & 1u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs_a, (lds_void8*)(st + (wave * 4 + i) * 1024), 16, ok ? a_off[i] + sa : R8_OOB, 0, 0,
           0);
     }
     char* const stb = st + R8_A_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_b, (lds_void8*)(stb + (wave * 2 + i) * 1024), 16, b_off[i] + sb, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs_b, (lds_void8*)(stb + (wave * 2 + part) * 1024), 16, b_off[part] + sb, 0, 0, 0);
+    if (part == 0) return;
     it_c += BK;
     if (it_c == Acin) {
       it_c = 0;
@@ -259,11 +262,10 @@ conv_ring8_kernel(GemmArgs args) {
     for (int b = 0; b < NR; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  auto mma_stage = [&](int stage) {
+  auto mma_kstep = [&](int stage, int ks) {
     const bf16* A = reinterpret_cast<const bf16*>(smem + stage * R8_STAGE);
     const bf16* B = reinterpret_cast<const bf16*>(smem + stage * R8_STAGE + R8_A_BYTES);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    {
       const int ch = ks * 4 + fq;
       bf16x8 af[MR], bfr[NR];
 #pragma unroll
@@ -292,8 +294,14 @@ conv_ring8_kernel(GemmArgs args) {
   // ---- 3-stage ring: tiles t+1 and t+2 in flight during the MFMAs of tile t ----
   const int nt = t_end - t_beg;
   if (kp) kp[1] = wall_clock64();
-  if (nt > 0) issue(0);
-  if (nt > 1) issue(1);
+  if (nt > 0) {
+    issue_part(0, 0);
+    issue_part(0, 1);
+  }
+  if (nt > 1) {
+    issue_part(1, 0);
+    issue_part(1, 1);
+  }
   int rd = 0;
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) r8_wait_vm<6>();   // this wave's tile-t DMAs have landed
@@ -301,8 +309,12 @@ conv_ring8_kernel(GemmArgs args) {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();      // ... every wave's; stage (t+2) % 3 is free
     asm volatile("" ::: "memory");
-    if (t + 2 < nt) issue(rd == 0 ? 2 : rd - 1);
-    mma_stage(rd);
+    const bool more = t + 2 < nt;
+    const int ws = rd == 0 ? 2 : rd - 1;
+    if (more) issue_part(ws, 0);
+    mma_kstep(rd, 0);
+    if (more) issue_part(ws, 1);
+    mma_kstep(rd, 1);
     rd = rd == 2 ? 0 : rd + 1;
     if (kp && t < 48) kp[2 + t] = wall_clock64();
   }
