@@ -28,9 +28,11 @@
 //     and 16x16 maps, so every stride-2 dgrad tile (sub-pixel decomposition: 1, 2, 2 or
 //     4 taps per output parity class) is made of pixels of one class.
 // In the backward launch the workgroups beyond the N x P slices compute the 52 weight
-// gradients (dW = sum_p dy x im2col(relu(bn(x)))) per image group into fp32 slabs, each
-// item as soon as the slices' barrier counter says its dy is published; the existing
-// deterministic grouped reduce sums the slabs afterwards.
+// gradients (dW = sum_p dy x im2col(relu(bn(x)))) per image group into fp32 slabs: they
+// take items from one queue in readiness order (the slices join once their dgrad chain
+// is done), each as soon as the readiness count says its dy is published; the existing
+// deterministic grouped reduce sums the slabs afterwards (which workgroup ran an item
+// does not change its slab: bitwise deterministic).
 //
 // Hand-off protocol (MI355X_MICROARCH.md, "Valid forms" row 1): every byte another
 // workgroup reads inside the launch (published tensors) is stored write-through (sc1),
@@ -825,6 +827,7 @@ __device__ __forceinline__ bool wait_fwd(Ctx& x) {
 // cache line (bar + PRN_READY, 256 B away): the ~190 weight-gradient workgroups poll that
 // line instead of the arrival counter the slices' atomics go to.
 constexpr int PRN_READY = 64;
+constexpr int PRN_QUEUE = 96;   // the weight-gradient item queue (its own 128-B line)
 __device__ __forceinline__ bool wait_bwd(Ctx& x) {
   ++x.nbar;
   const bool ok = grid_wait(x.a->bar + 1, x.nbar * x.slices, x.a->err, x.m.flag);
@@ -901,10 +904,14 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   conv_acc<S, P, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane, x.m.red);
   round_acc<S, P, false>(hr, acc, hr);
   probe(x, 3);
-  publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
+  // With neighbour slices (P > 1) the saved tensor is read inside this launch, so it is
+  // published before the arrive; at one slice only the backward launch reads it, and it
+  // is stored after the arrive, its drain overlapping the barrier wait.
+  if constexpr (P > 1) publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, hr, B.bn2, wave, lane);
   probe(x, 4);
   grid_arrive(a.bar);
+  if constexpr (P == 1) publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
   probe(x, 5);
   {
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
@@ -924,10 +931,11 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   if constexpr (PROJ) round_acc<S, P, true>(xr, acc, pr);
   else round_acc<S, P, true>(xr, acc, xr);
   probe(x, 9);
-  publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
+  if constexpr (P > 1) publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, xr, bi_next, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar);
+  if constexpr (P == 1) publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
   probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
@@ -984,9 +992,10 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     zero_acc(acc);
     conv_acc<0, P, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, x.wave, x.lane, x.m.red);
     round_acc<0, P, false>(xr, acc, xr);
-    publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
+    if constexpr (P > 1) publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
     grid_arrive(a.bar);
+    if constexpr (P == 1) publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
     WLoad LP{};
     if (B0.wpf) LP = wl_fwd(B0.wpf, 16, 16, 1);
@@ -1453,22 +1462,12 @@ __device__ __forceinline__ void run_item(const PrnItem& it, char* smem, int wave
 
 }  // namespace
 
+// The slice role of the backward launch: the dgrad chain with its BatchNorm backwards
+// (returns false when a barrier wait timed out).
 template <int P>
-__global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+__device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int wave, int lane) {
   const int nsl = a.N * P;
-  if ((int)blockIdx.x >= nsl) {
-    // ---- weight-gradient role: items w, w + W, ... in readiness order ----
-    const int w = blockIdx.x - nsl, W = gridDim.x - nsl;
-    int* flag = reinterpret_cast<int*>(smem + OFF_MISC);
-    for (int i = w; i < a.nitems; i += W) {
-      const PrnItem& it = ld_const(a.items + i);
-      if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
-      run_item(it, smem, wave, lane);
-    }
-    return;
-  }
+  const int tid = threadIdx.x;
   Ctx x;
   x.a = &a;
   x.m = carve(smem);
@@ -1513,7 +1512,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     grid_arrive(a.bar + 1);
     bn_prefetch_bwd(ld_const(a.bns + (fb)), 64, x.bnr);
     bn_prefetch_tab(ld_const(a.bns + (BL.bn2)), 64, x.ftr);
-    if (!wait_bwd(x)) return;
+    if (!wait_bwd(x)) return false;
     const Nbr<2, P> nb(x.kslice);
     NbrBwd q;
     bwd_nbr_issue<2, P>(nb, nullptr, BL.out + img_o, nullptr, q);
@@ -1534,19 +1533,44 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     return block_bwd<S, STR, PROJ, P>(x, dout, hs, n2, hp, Bp, ld_const(a.blocks + (bi)));
   };
   for (int bi = nb - 1; bi > 2 * nps; --bi)
-    if (!run(BlkTag<2, 1, false>{}, bi)) return;
-  if (!run(BlkTag<2, 2, true>{}, 2 * nps)) return;
+    if (!run(BlkTag<2, 1, false>{}, bi)) return false;
+  if (!run(BlkTag<2, 2, true>{}, 2 * nps)) return false;
   for (int bi = 2 * nps - 1; bi > nps; --bi)
-    if (!run(BlkTag<1, 1, false>{}, bi)) return;
-  if (!run(BlkTag<1, 2, true>{}, nps)) return;
+    if (!run(BlkTag<1, 1, false>{}, bi)) return false;
+  if (!run(BlkTag<1, 2, true>{}, nps)) return false;
   for (int bi = nps - 1; bi > 0; --bi)
-    if (!run(BlkTag<0, 1, false>{}, bi)) return;
-  if (!run(BlkTag<0, 1, true>{}, 0)) return;
+    if (!run(BlkTag<0, 1, false>{}, bi)) return false;
+  if (!run(BlkTag<0, 1, true>{}, 0)) return false;
   probe(x, 200);
   // ---- the stem output's gradient: published for the stem's weight gradient ----
   publish<0, P>(dout, a.dx0 + (long)x.img * 1024 * 16, x.kslice, wave, lane);
   grid_arrive(a.bar + 1);
   if (blockIdx.x == 0) wait_bwd(x);   // publishes the stem item's readiness
+  return true;
+}
+
+template <int P>
+__global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if ((int)blockIdx.x < a.N * P && !prn_bwd_slices<P>(a, smem, wave, lane)) return;
+  // ---- weight-gradient items from one queue in readiness order: the workgroups beyond
+  //      the slices from the start, every slice once its dgrad chain is done (the last
+  //      items -- the first stage and the stem -- only become ready at the very end) ----
+  int* flag = reinterpret_cast<int*>(smem + OFF_MISC);
+  int* slot = flag + 1;
+  for (;;) {
+    __syncthreads();   // the previous item's LDS and the slot word are free
+    if (tid == 0)
+      *slot = (int)__hip_atomic_fetch_add(a.bar + PRN_QUEUE, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int i = __builtin_amdgcn_readfirstlane(*slot);
+    if (i >= a.nitems) return;
+    const PrnItem& it = ld_const(a.items + i);
+    if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
+    run_item(it, smem, wave, lane);
+  }
 }
 
 // ---- host ------------------------------------------------------------------------------

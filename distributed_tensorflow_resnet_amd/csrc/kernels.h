@@ -269,7 +269,8 @@ struct PrnArgs {
   const bf16* stem_w;        // OHWI [16][3][3][8]
   double* pool_acc;          // [N][64] fp64 average-pool sums (zeroed every step)
   unsigned* bar;             // [128]: barrier counters (forward, backward) at 0, 1; the backward
-                             // readiness count at 64 -- zeroed every step
+                             // readiness count at 64, the weight-gradient item queue at 96 --
+                             // zeroed every step
   int* err;                  // set when a barrier wait times out
   const bf16* dense_w;       // [64][kpad] bf16 HWIO
   const float* dense_b;
