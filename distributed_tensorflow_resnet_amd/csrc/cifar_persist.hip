@@ -453,15 +453,25 @@ __device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, 
     v[t] = ldg(reinterpret_cast<const bf16x4*>(img_base + gofs<S, P>(kslice, wave, lane, t)));
 }
 
-// write-through (sc1) stores: these tensors are read by other workgroups in the launch
-template <int S, int P>
+// write-through (sc1) stores: these tensors are read by other workgroups in the launch.
+// ROWS 1: only the slice's first and last rows (what the neighbouring slices read inside
+// the launch), 2: only the rows between them, 0: all.
+template <int S, int P, int ROWS = 0>
 __device__ __forceinline__ void publish(const bf16x4 (&v)[8], bf16* img_base, int kslice,
                                         int wave, int lane) {
+  using G = Stg<S, P>;
   lane = opaque_v(lane);
   if (!wave_active<S, P>(wave)) return;
 #pragma unroll
-  for (int t = 0; t < Stg<S, P>::TPW; ++t)
-    st_sc1_b64(img_base, gofs<S, P>(kslice, wave, lane, t), v[t]);
+  for (int t = 0; t < G::TPW; ++t) {
+    int pb, cb, h, w;
+    tile_of<S, P>(wave, t, pb, cb);
+    canon<S, P>(kslice, pb * 16 + (lane & 15), h, w);
+    const int lr = h - kslice * G::RS;
+    const bool border = lr == 0 || lr == G::RS - 1;
+    if (ROWS == 0 || (ROWS == 1) == border)
+      st_sc1_b64(img_base, (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4), v[t]);
+  }
 }
 
 // ---- halos -------------------------------------------------------------------------------
@@ -904,14 +914,14 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   conv_acc<S, P, GI::C, 3, STR, false>(acc, x.m.ha, x.m.w1, x.kslice, wave, lane, x.m.red);
   round_acc<S, P, false>(hr, acc, hr);
   probe(x, 3);
-  // With neighbour slices (P > 1) the saved tensor is read inside this launch, so it is
-  // published before the arrive; at one slice only the backward launch reads it, and it
-  // is stored after the arrive, its drain overlapping the barrier wait.
-  if constexpr (P > 1) publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
+  // Inside this launch only the neighbouring slices read the saved tensor, and only its
+  // border rows: those are published before the arrive; the rest (read by the backward
+  // launch) is stored after it, its drain overlapping the barrier wait.
+  if constexpr (P > 1) publish<S, P, 1>(hr, B.h1 + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, hr, B.bn2, wave, lane);
   probe(x, 4);
   grid_arrive(a.bar);
-  if constexpr (P == 1) publish<S, P>(hr, B.h1 + img_o, x.kslice, wave, lane);
+  publish<S, P, P == 1 ? 0 : 2>(hr, B.h1 + img_o, x.kslice, wave, lane);
   probe(x, 5);
   {
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
@@ -931,11 +941,11 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   if constexpr (PROJ) round_acc<S, P, true>(xr, acc, pr);
   else round_acc<S, P, true>(xr, acc, xr);
   probe(x, 9);
-  if constexpr (P > 1) publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
+  if constexpr (P > 1) publish<S, P, 1>(xr, B.out + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, xr, bi_next, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar);
-  if constexpr (P == 1) publish<S, P>(xr, B.out + img_o, x.kslice, wave, lane);
+  publish<S, P, P == 1 ? 0 : 2>(xr, B.out + img_o, x.kslice, wave, lane);
   probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
@@ -992,10 +1002,10 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     zero_acc(acc);
     conv_acc<0, P, 8, 3, 1, false>(acc, x.m.ha, x.m.w1, x.kslice, x.wave, x.lane, x.m.red);
     round_acc<0, P, false>(xr, acc, xr);
-    if constexpr (P > 1) publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
+    if constexpr (P > 1) publish<0, P, 1>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
     grid_arrive(a.bar);
-    if constexpr (P == 1) publish<0, P>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
+    publish<0, P, P == 1 ? 0 : 2>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
     WLoad LP{};
     if (B0.wpf) LP = wl_fwd(B0.wpf, 16, 16, 1);
@@ -1257,7 +1267,6 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   bf16x4 xs[8];
   load_regs<SI, P>(xs, B.x + img_i, x.kslice, wave, lane);     // BN1 input (used after a barrier)
   tab_store(x.ftr, G::C, x.m.tbl);
-  publish<S, P>(dout, B.dout + img_o, x.kslice, wave, lane);   // conv2 / projection wgrads
   __syncthreads();
   probe(x, 1);
   f32x4 acc[8];
@@ -1266,11 +1275,14 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   bf16x4 da[8];
   round_acc<S, P, false>(da, acc, da);
   probe(x, 3);
-  if constexpr (P > 1)   // only the neighbouring slices read it
-    publish<S, P>(da, B.da2 + img_o, x.kslice, wave, lane);
+  if constexpr (P > 1)   // only the neighbouring slices read it, only its border rows
+    publish<S, P, 1>(da, B.da2 + img_o, x.kslice, wave, lane);
   bwd_sums<S, P>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
   probe(x, 4);
   grid_arrive(a.bar + 1);
+  // dout for the conv2 / projection weight gradients and the neighbours' residual rows:
+  // stored after this arrive (its drain overlaps the wait), drained by the next one
+  publish<S, P>(dout, B.dout + img_o, x.kslice, wave, lane);
   probe(x, 5);
   {
     const WLoad L1 = wl_dgrad(B.w1b, G::C, GI::C, 3);
@@ -1307,8 +1319,8 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   }
   round_acc<SI, P, false>(da, acc, da);
   probe(x, 9);
-  if constexpr (P > 1)   // only the neighbouring slices read it
-    publish<SI, P>(da, B.da1 + img_i, x.kslice, wave, lane);
+  if constexpr (P > 1)   // only the neighbouring slices read it, only its border rows
+    publish<SI, P, 1>(da, B.da1 + img_i, x.kslice, wave, lane);
   bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar + 1);
