@@ -184,6 +184,10 @@ __device__ __forceinline__ void st_sc1_b64(bf16* base, long elem, bf16x4 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 16);
 }
+__device__ __forceinline__ void st_sc1_b128(bf16* base, long elem, bf16x8 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (int)(elem * 2), 0, 16);
+}
 __device__ __forceinline__ bf16x8 ld_sc1_b128(const bf16* base, long elem) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(const_cast<bf16*>(base)), 0,
                                                     0x7fffffff, 0x00020000);
@@ -471,6 +475,22 @@ __device__ __forceinline__ void publish(const bf16x4 (&v)[8], bf16* img_base, in
     const bool border = lr == 0 || lr == G::RS - 1;
     if (ROWS == 0 || (ROWS == 1) == border)
       st_sc1_b64(img_base, (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4), v[t]);
+  }
+}
+
+// The slice's own rows of a halo (rows 1..RS) -> the image tensor (write-through 16-B
+// stores): publishes a tensor some time after it was staged, from LDS, without holding
+// its registers live in between.
+template <int S, int P>
+__device__ __forceinline__ void halo_to_global(const bf16* hal, bf16* img_base, int kslice) {
+  using G = Stg<S, P>;
+  constexpr int UNITS = G::RS * G::R * G::U;
+  for (int q = threadIdx.x; q < UNITS; q += PT) {
+    const int row = q / (G::R * G::U), rem = q - row * G::R * G::U;
+    const int col = rem / G::U, u = rem - col * G::U;
+    const int lr = row + 1, lc = col + 1;
+    st_sc1_b128(img_base, ((long)(kslice * G::RS + row) * G::R + col) * G::C + u * 8,
+                lds16(hal + haddr<G::U>(lr * G::W2 + lc, lc, u * 8)));
   }
 }
 
@@ -1301,7 +1321,6 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     bn_bwd_table(ld_const(a.bns + (B.bn2)), x.bnr, G::C, (float)a.N * G::R * G::R, x.m.tbl2);
     bf16x4 dh[8];
     bwd_apply<S, P, false>(dh, da, hs, dh, x.m.tbl2, wave, lane);
-    publish<S, P>(dh, B.dh1 + img_o, x.kslice, wave, lane);    // conv1 weight gradient
     bwd_halo<S, P>(x, x.m.ha, dh, nb, q, nullptr, false, x.m.tbl2, wave, lane);
     tab_store(x.ftr, GI::C, x.m.tbl);
     w_store(L1, w1r, x.m.w1);
@@ -1324,6 +1343,9 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar + 1);
+  // dh1 for the conv1 weight gradient, from its halo (HA, intact until the next block
+  // stages its own): stored after this arrive, drained by the next one
+  halo_to_global<S, P>(x.m.ha, B.dh1 + img_o, x.kslice);
   probe(x, 11);
   bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
   w_prefetch(next_w2, w2r);

@@ -154,8 +154,8 @@ class PersistStep:
         """Weight-gradient work items in the order the backward publishes their dy
         (`ready` = backward barrier count after which it is visible; barrier 1 is the
         final BN): per block j (last block first) conv2 and the projection with the
-        block's dout (stored after the block's first arrive) at 2j + 3, conv1 with dh1 at
-        2j + 3; the stem after the final arrive.
+        block's dout (stored after the block's first arrive) at 2j + 3, conv1 with dh1
+        (stored after the second) at 2j + 4; the stem after the final arrive (2nb + 2).
         Images are grouped per item (the grouped reduce sums one slab per group): a
         quarter of the batch for stages 2-3, whose items have the rest of the backward
         to run in; 4 images for stage 1 and the stem, whose items only become ready at
@@ -178,7 +178,7 @@ class PersistStep:
             convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 3))
             if b.proj is not None:
                 convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 3))
-            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 3))
+            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 4))
         convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 2))
         tot = 0
         self.part_off, self.splits = {}, {}
