@@ -38,14 +38,15 @@ AUTO_MAX_BATCH = 240
 
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
-    """Row slices (workgroups) per image: 4 up to 16 images, 2 up to 64, else 1
-    (MI355X, CIFAR RN50 step ms: bs16 0.667 at 4 / 0.684 at 2; bs32 0.722 at 2 / 0.826
-    at 1; bs64 0.836 / 0.893; bs96 1.025 at 2 / 0.998 at 1 -- more slices shorten each
-    layer, more arrivals lengthen each barrier and leave fewer CUs for the weight
-    gradients).  The engine's tune persist_slices overrides."""
+    """Row slices (workgroups) per image of the backward: 4 up to 32 images, 2 up to 64,
+    else 1 (MI355X, CIFAR RN50 step ms: bs24 0.637 at 4 / 0.712 at 2; bs32 0.670 at 4 /
+    0.712 at 2; bs48 0.757 at 4 / 0.733 at 2; bs64 0.836 at 2 / 0.893 at 1; bs96 1.025
+    at 2 / 0.998 at 1 -- more slices shorten each layer, more arrivals lengthen each
+    barrier and leave fewer CUs for the weight gradients).  The engine's tune
+    persist_slices overrides."""
     if override in (1, 2, 4):
         return override
-    if N <= 16 and 4 * N + 32 <= cus:
+    if N <= 32 and 4 * N + 32 <= cus:
         return 4
     return 2 if N <= 64 and 2 * N + 32 <= cus else 1
 
@@ -53,13 +54,14 @@ def slices_for(N: int, cus: int, override: int = -1) -> int:
 def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:
     """Row slices per image of the forward launch.  The forward has no weight-gradient
     workgroups to leave CUs for, and its slicing is independent of the backward's (both
-    launches exchange only whole NHWC tensors and global BN sums): 4 up to 16 images,
-    2 while 2N slices fill at most 3/4 of the CUs, else 1 (MI355X, CIFAR RN50 step: bs96
-    0.961 -> 0.918 ms with a 2-slice forward; bs128's 256-workgroup forward ran 0.58 ms
-    against 0.43 at 1 slice).  The engine's tune persist_slices overrides."""
+    launches exchange only whole NHWC tensors and global BN sums): 4 up to 32 images,
+    2 while 2N slices fill at most 3/4 of the CUs, else 1 (MI355X, CIFAR RN50 forward:
+    bs32 0.294 ms at 4 / 0.302 at 2, bs48 0.343 / 0.315; step bs96 0.961 -> 0.918 ms with
+    a 2-slice forward; bs128's 256-workgroup forward ran 0.58 ms against 0.43 at 1
+    slice).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
-    if N <= 16 and 4 * N <= cus:
+    if N <= 32 and 4 * N <= cus:
         return 4
     return 2 if 8 * N <= 3 * cus else 1
 

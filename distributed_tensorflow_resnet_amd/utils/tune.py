@@ -54,7 +54,7 @@ ENGINE = {
                     "one workgroup per image row slice; train/persist.py): -1 auto = per-rank "
                     "batch <= 240, 0 off, 1 whenever the network is supported"),
     "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (backward: 4 "
-                           "up to 16 images, 2 up to 64, else 1; forward: 4 up to 16, 2 while "
+                           "up to 32 images, 2 up to 64, else 1; forward: 4 up to 32, 2 while "
                            "2N <= 3/4 of the CUs, else 1), 1, 2 or 4 for both"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }

@@ -86,8 +86,8 @@ def test_persistent_slice_selection():
     and tune persist_slices overrides both."""
     from distributed_tensorflow_resnet_amd.train.persist import fwd_slices_for, slices_for
 
-    assert [slices_for(n, 256) for n in (8, 16, 32, 64, 96, 128, 224)] == [4, 4, 2, 2, 1, 1, 1]
-    assert [fwd_slices_for(n, 256) for n in (8, 16, 32, 64, 96, 128, 200)] == [4, 4, 2, 2, 2, 1, 1]
+    assert [slices_for(n, 256) for n in (8, 16, 32, 48, 64, 96, 128, 224)] == [4, 4, 4, 2, 2, 1, 1, 1]
+    assert [fwd_slices_for(n, 256) for n in (8, 16, 32, 48, 64, 96, 128, 200)] == [4, 4, 4, 2, 2, 2, 1, 1]
     assert slices_for(128, 256, 2) == 2 and fwd_slices_for(16, 256, 1) == 1
     for n in range(1, 241):
         assert n * slices_for(n, 256) + 16 <= 256

@@ -176,7 +176,7 @@ def test_persistent_training_tracks_per_layer(gpu, monkeypatch):
 
 
 def test_persistent_auto_selection(gpu, monkeypatch):
-    """tune persist -1: on for every supported per-rank batch (4 slices up to 16 images,
+    """tune persist -1: on for every supported per-rank batch (4 slices up to 32 images,
     then 2, then 1); never for ImageNet."""
     from distributed_tensorflow_resnet_amd.models.spec import imagenet_spec
 
@@ -184,6 +184,7 @@ def test_persistent_auto_selection(gpu, monkeypatch):
     mk = lambda spec, N: Engine(spec, N, weight_decay=2e-4,  # noqa: E731
                                 lr_schedule=cifar_lr_schedule(), device=gpu)
     assert mk(cifar_spec(8), 16).prn.P == 4
+    assert mk(cifar_spec(8), 32).prn.P == 4
     assert mk(cifar_spec(8), 64).prn.P == 2
     assert mk(cifar_spec(8), 128).prn.P == 1
     assert not mk(imagenet_spec(18, image_hw=64), 8).persist
