@@ -650,13 +650,20 @@ __device__ __forceinline__ void acc_read(const double* acc, int C, int c, double
 
 // BN parameters prefetched into registers (thread c < C) before a barrier wait
 struct BnRegs {
-  float g, b, mean, rstd, scale, shift;
+  float g, b, mean, rstd, scale, shift, mm, mv;
 };
+// (workgroup 0 also updates the moving averages: their old values are prefetched too,
+// or its read-modify-write would put a memory round trip in front of its next arrive --
+// and every workgroup waits for that one)
 __device__ __forceinline__ void bn_prefetch_fwd(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
     r.g = ldg(bn.gamma + c);
     r.b = ldg(bn.beta + c);
+    if (blockIdx.x == 0) {
+      r.mm = ldg(bn.mmean + c);
+      r.mv = ldg(bn.mvar + c);
+    }
   }
 }
 __device__ __forceinline__ void bn_prefetch_bwd(const PrnBn& bn, int C, BnRegs& r) {
@@ -718,7 +725,7 @@ __device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const BnRegs& pr, 
       stg(bn.shift + c, sh);
       if (update_moving) {
         const float uvar = M > 1.0 ? (float)(var * M / (M - 1.0)) : fvar;
-        const float mm = ldg(bn.mmean + c), mv = ldg(bn.mvar + c);
+        const float mm = pr.mm, mv = pr.mv;
         stg(bn.mmean + c, mm - (1.f - momentum) * (mm - fmu));
         stg(bn.mvar + c, mv - (1.f - momentum) * (mv - uvar));
       }
