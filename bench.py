@@ -259,8 +259,15 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
                 acc[k] = acc.get(k, 0.0) + v
         phases = {k: round(v / args.phase_steps, 4) for k, v in acc.items()}
     dog.stop()
+    # the persistent CIFAR step bounds every grid-barrier wait (2 s) and flags a timeout
+    # instead of hanging: a flagged run computed garbage, so its timing is not reported
+    if eng.persist_error():
+        raise SystemExit(f"bench.py: rank {ctx.rank}: a persistent-step barrier wait timed "
+                         "out (workgroups not co-resident?) -- the measurement is invalid")
     extra = {"dtype": "bf16", "device": torch.cuda.get_device_name(device),
              "graph": use_graph, "wgrad_stream": eng.fork_wgrad, "comm": eng.comm_info(),
+             "step_path": ("persistent (P fwd/bwd = %d/%d)" % (eng.prn.P_fwd, eng.prn.P)
+                           if eng.persist else "per-layer plan"),
              "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
     return ctx, elapsed, m, extra, phases
 
