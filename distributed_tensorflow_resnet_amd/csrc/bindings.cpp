@@ -581,6 +581,21 @@ static Launch mk_sgd_update_pack(ptr_t master, ptr_t grad, ptr_t mom, long n, fl
   };
 }
 
+static Launch mk_sgd_tiles(ptr_t master, ptr_t grad, ptr_t mom, float init,
+                           long long warm_steps, float warm_from, float warm_to,
+                           std::vector<long long> bounds, std::vector<float> vals, ptr_t gstep,
+                           float momentum, float wd, float grad_scale, int use_momentum,
+                           ptr_t segs, ptr_t work, ptr_t blk_seg, int nblocks, ptr_t bf,
+                           ptr_t lr_out, ptr_t ticket) {
+  const LrSchedule sc = make_sched(init, warm_steps, warm_from, warm_to, bounds, vals);
+  return [=](hipStream_t s) {
+    sgd_tiles(P<float>(master), P<float>(grad), P<float>(mom), sc, P<long long>(gstep),
+              momentum, wd, grad_scale, use_momentum, P<const ParamSeg>(segs),
+              P<const OptWork>(work), P<const int>(blk_seg), nblocks, P<bf16>(bf),
+              P<float>(lr_out), P<unsigned>(ticket), s);
+  };
+}
+
 static Launch mk_step_increment(ptr_t gstep) {
   return [=](hipStream_t s) { step_increment(P<long long>(gstep), s); };
 }
@@ -1175,6 +1190,7 @@ PYBIND11_MODULE(_C, m) {
   def_op(m, plan, "maxpool_bwd", mk_maxpool_bwd);
   def_op(m, plan, "sgd_update_pack", mk_sgd_update_pack);
   def_op(m, plan, "ohwi_pack", mk_ohwi_pack);
+  def_op(m, plan, "sgd_tiles", mk_sgd_tiles);
   def_op(m, plan, "step_increment", mk_step_increment);
   def_op(m, plan, "l2_half_sum", mk_l2_half_sum);
   def_op(m, plan, "fill", mk_fill);
@@ -1280,6 +1296,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("param_seg_bytes", []() { return (int)sizeof(ParamSeg); });
   m.def("wg_desc_bytes", []() { return (int)sizeof(WgReduceDesc); });
+  m.def("opt_work_bytes", []() { return (int)sizeof(OptWork); });
   m.def("device_count", &hip_device_count);
   m.def(
       "crc32c",

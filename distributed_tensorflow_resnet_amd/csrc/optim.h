@@ -22,6 +22,23 @@ void sgd_update_pack(float* master, const float* grad, float* mom, long n, const
 // gstep_inc (optional): global_step += 1 in the same launch.
 void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0, int nseg,
                long long total_tiles, bf16* bf, long long* gstep_inc, hipStream_t s);
+// The fused optimizer of the persistent step (sgd_tiles): per parameter segment, the
+// work map of one launch that (optionally) sums the split-K weight-gradient slabs,
+// applies SGD-momentum + wd and writes both bf16 copies.
+struct OptWork {
+  const float* part;       // slabs [splits][K'][taps*cslab] (null: the gradient is in grad)
+  long long tile0;         // first workgroup of the segment
+  int splits, kslab;       // slab count and rows (output channels, padded) of a slab
+  int cslab;               // padded input channels of a slab row (taps*cslab columns)
+  int tiled;               // 1: tr (tap*C+ci) x tc (co) tiles; 0: 1024-element chunks
+  int tr, tc;              // tile rows / columns (<= 64 each)
+};
+// blk_seg[b] = the segment of workgroup b; ticket: a zero-initialised int the last
+// workgroup resets after its global_step += 1 (every workgroup has read the step).
+void sgd_tiles(float* master, float* grad, float* mom, const LrSchedule& s, long long* gstep,
+               float momentum, float wd, float grad_scale, int use_momentum,
+               const ParamSeg* segs, const OptWork* work, const int* blk_seg, int nblocks,
+               bf16* bf, float* lr_out, unsigned* ticket, hipStream_t st);
 void step_increment(long long* gstep, hipStream_t s);
 int l2_workspace_floats();
 void l2_half_sum(const float* v, long n, float* ws, float* out, hipStream_t s);

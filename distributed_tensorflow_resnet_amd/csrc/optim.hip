@@ -212,6 +212,187 @@ void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0
   DTR_CHECK_LAUNCH();
 }
 
+// The persistent step's optimizer in ONE launch, instead of the grouped slab reduce,
+// sgd_pack and ohwi_pack (three dependent launches, ~31 us of a 0.87 ms CIFAR step,
+// profiles/cifar_persist_bs128_kernels.md).  A weight is cut into TR (rows tap*C+ci)
+// x TC (co) tiles of its HWIO master (host-chosen so a tile's slab loads are <= 8
+// 16-byte loads per thread: 64x64 without slabs, 16x16 for 32 splits):
+//   1. (slab mode) its split-K slabs ([split][co][tap*cslab+ci]) summed -- 16-byte
+//      loads along (tap, ci), the slabs' contiguous axis; past 8 splits 4 thread groups
+//      take every 4th split and their partials are added in group order, the grouped
+//      reduce's order -- into LDS [co][r];
+//   2. per element: g' = g*scale + wd*w, acc = momentum*acc + g', w -= lr*acc; the fp32
+//      gradient (slab mode), master, momentum and the bf16 HWIO copy;
+//   3. the bf16 tile transposed through LDS into the OHWI copy (written along ci).
+// Other tensors (BN gamma/beta, biases) go in 1024-element chunks.  The rate comes from
+// global_step; the last workgroup to finish (by ticket) does global_step += 1.
+__global__ void __launch_bounds__(256)
+sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict__ mom,
+                 LrSchedule sched, long long* gstep, float momentum, float wd,
+                 float grad_scale, int use_momentum, const ParamSeg* __restrict__ segs,
+                 const OptWork* __restrict__ work, const int* __restrict__ blk_seg,
+                 bf16* __restrict__ bf, float* __restrict__ lr_out, unsigned* ticket) {
+  __shared__ float gt[64][65];   // summed gradient tile [co][r]
+  __shared__ bf16 bt[64][66];    // updated bf16 tile [r][co]
+  __shared__ f32x4 red[256];     // split-group partials
+  __shared__ float lr_s;
+  const int tid = threadIdx.x;
+  const int si = blk_seg[blockIdx.x];
+  const ParamSeg sg = segs[si];
+  const OptWork ow = work[si];
+  if (tid == 0) {
+    const float lr0 = lr_at(sched, (long)*gstep);
+    lr_s = lr0;
+    if (lr_out && blockIdx.x == 0) *lr_out = lr0;
+  }
+  const int t = (int)((long long)blockIdx.x - ow.tile0);
+  if (ow.tiled) {
+    const int taps = sg.kh * sg.kw, C = sg.C, K = sg.K, R = taps * C;
+    const int TR = ow.tr, TC = ow.tc;
+    const int tc_n = (K + TC - 1) / TC;
+    const int r0 = (t / tc_n) * TR, c0 = (t - (t / tc_n) * tc_n) * TC;
+    const int nr = min(TR, R - r0), nc = min(TC, K - c0);   // valid extent
+    const bool slab = ow.part != nullptr;
+    if (slab) {
+      // slab columns: the tile's rows (cslab == C: column n = row r, nr % 4 == 0) or,
+      // for padded rows (the stem: C = 3 in rows of cslab; one row tile), all of them
+      const int cs = ow.cslab;
+      const bool padded = cs != C;
+      const long NT = (long)taps * cs;
+      const long stride = (long)ow.kslab * NT;    // one split's slab
+      const int n0 = padded ? 0 : r0;
+      const int ncol4 = padded ? (int)(NT >> 2) : (nr >> 2);
+      const int U = nc * ncol4;                  // float4 units of the tile
+      // the grouped reduce's summation order (conv_wgrad.hip, WGR_WIDE_MAX): splits in
+      // sequence up to 8, else 4 interleaved groups added in group order -- so a step
+      // with and without an all-reduce in between agree bit for bit (G*U <= 256: host)
+      const int G = ow.splits > 8 ? 4 : 1;
+      auto scatter = [&](const f32x4& a, int col, int c4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + c4 + j;
+          if (padded) {
+            const int tap = n / cs, ci = n - tap * cs;
+            if (ci < C) gt[col][tap * C + ci] = a[j];
+          } else {
+            gt[col][c4 + j] = a[j];
+          }
+        }
+      };
+      for (int q = tid; q < G * U; q += 256) {
+        const int u = q % U, gi = q / U;
+        const int col = u / ncol4, c4 = (u - col * ncol4) * 4;
+        const float* src = ow.part + (long)(c0 + col) * NT + n0 + c4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        int s = gi;
+        for (; s + 3 * G < ow.splits; s += 4 * G) {   // 4 loads in flight, order kept
+          f32x4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[j] = *reinterpret_cast<const f32x4*>(src + (long)(s + j * G) * stride);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc += v[j];
+        }
+        for (; s < ow.splits; s += G) acc += *reinterpret_cast<const f32x4*>(src + (long)s * stride);
+        if (G == 1) scatter(acc, col, c4);
+        else red[gi * U + u] = acc;
+      }
+      if (G > 1) {
+        __syncthreads();
+        for (int u = tid; u < U; u += 256) {
+          f32x4 acc = red[u];
+          for (int gi = 1; gi < G; ++gi) acc += red[gi * U + u];
+          scatter(acc, u / ncol4, (u % ncol4) * 4);
+        }
+      }
+    }
+    __syncthreads();         // gt and lr_s
+    const float lr = lr_s;
+#pragma unroll 4
+    for (int q = tid; q < TR * TC; q += 256) {
+      const int rl = q / TC, cl = q - rl * TC;
+      if (rl < nr && cl < nc) {
+        const int r = r0 + rl, co = c0 + cl;
+        const long e = sg.offset + (long)r * K + co;
+        float gv;
+        if (slab) {
+          gv = gt[cl][rl];
+          g[e] = gv;
+        } else {
+          gv = g[e];
+        }
+        float wv = w[e];
+        gv = gv * grad_scale + wd * wv;
+        if (use_momentum) {
+          const float a = momentum * mom[e] + gv;
+          mom[e] = a;
+          wv -= lr * a;
+        } else {
+          wv -= lr * gv;
+        }
+        w[e] = wv;
+        if (sg.bf_hwio >= 0) bf[sg.bf_hwio + (long)r * sg.kpad + co] = (bf16)wv;
+        bt[rl][cl] = (bf16)wv;
+      }
+    }
+    if (sg.bf_ohwi >= 0) {
+      __syncthreads();
+      for (int q = tid; q < TR * TC; q += 256) {   // along r: the OHWI copy's ci runs
+        const int cl = q / TR, rl = q - cl * TR;
+        if (rl < nr && cl < nc) {
+          const int r = r0 + rl, co = c0 + cl;
+          const int tap = r / C, ci = r - tap * C;
+          bf[sg.bf_ohwi + ((long)co * taps + tap) * sg.cpad + ci] = bt[rl][cl];
+        }
+      }
+    }
+  } else {
+    __syncthreads();
+    const float lr = lr_s;
+    const long base = (long)t * 1024;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long l = base + j * 256 + tid;
+      if (l < sg.numel) {
+        const long e = sg.offset + l;
+        float wv = w[e];
+        const float gv = g[e] * grad_scale + wd * wv;
+        if (use_momentum) {
+          const float a = momentum * mom[e] + gv;
+          mom[e] = a;
+          wv -= lr * a;
+        } else {
+          wv -= lr * gv;
+        }
+        w[e] = wv;
+      }
+    }
+  }
+  // global_step += 1 once every workgroup has read it: thread 0 consumed its read (lr_s)
+  // before it takes the ticket, so a relaxed ticket orders it -- no fence: an agent-scope
+  // release/acquire writes back and invalidates the L2 per workgroup (613 of them: the
+  // launch took 54 us with __threadfence + acq_rel); the last one re-arms the ticket
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      *gstep += 1;
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+void sgd_tiles(float* master, float* grad, float* mom, const LrSchedule& s, long long* gstep,
+               float momentum, float wd, float grad_scale, int use_momentum,
+               const ParamSeg* segs, const OptWork* work, const int* blk_seg, int nblocks,
+               bf16* bf, float* lr_out, unsigned* ticket, hipStream_t st) {
+  if (nblocks <= 0) return;
+  hipLaunchKernelGGL(sgd_tiles_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, master, grad,
+                     mom, s, gstep, momentum, wd, grad_scale, use_momentum, segs, work, blk_seg,
+                     bf, lr_out, ticket);
+  DTR_CHECK_LAUNCH();
+}
+
 __global__ void step_incr_kernel(long long* gstep) {
   if (threadIdx.x == 0) *gstep += 1;
 }

@@ -60,6 +60,47 @@ SEG_DTYPE = np.dtype([
     ("kh", "<i4"), ("kw", "<i4"), ("C", "<i4"), ("K", "<i4"), ("cpad", "<i4"), ("kpad", "<i4"),
 ])
 
+OPTW_DTYPE = np.dtype([   # csrc/optim.h OptWork
+    ("part", "<u8"), ("tile0", "<i8"), ("splits", "<i4"), ("kslab", "<i4"), ("cslab", "<i4"),
+    ("tiled", "<i4"), ("tr", "<i4"), ("tc", "<i4"),
+])
+
+OPT_TILE_LOADS = 2048   # a sgd_tiles workgroup's slab loads: <= 8 16-byte loads per thread
+
+
+def _pow2ceil(x: int) -> int:
+    return 1 << max(0, (int(x) - 1).bit_length())
+
+
+def opt_tile(R: int, K: int, splits: int, cslab: int, C: int, taps: int):
+    """Tile (rows tap*C+ci, output channels) of a weight in the one-launch optimizer
+    (csrc/optim.hip sgd_tiles_kernel): 64 x 64 without slabs; with `splits` slabs the
+    tile shrinks (columns first) until its float4 slab loads fit OPT_TILE_LOADS and,
+    past 8 splits (4 thread groups of 64 float4 units), until it has <= 64 units.
+    Padded slab rows (cslab != C, the stem) keep all rows in one tile."""
+    if splits == 0:
+        return 64, 64
+    units_max = 64 if splits > 8 else 1 << 30
+    TC = min(64, _pow2ceil(K))
+    if cslab != C:
+        assert R <= 64 and (taps * cslab) % 4 == 0, (R, taps, cslab)
+        cols4 = taps * cslab // 4
+        while TC > 1 and (TC * cols4 * splits > OPT_TILE_LOADS or TC * cols4 > units_max):
+            TC //= 2
+        assert TC * cols4 <= units_max, (R, K, splits, cslab)
+        return R, TC
+    assert C % 4 == 0, C
+    TR = min(64, _pow2ceil(R))
+    while (TR * TC // 4) * splits > OPT_TILE_LOADS or TR * TC // 4 > units_max:
+        if TC >= TR and TC > 1:
+            TC //= 2
+        elif TR > 4:
+            TR //= 2
+        else:
+            break
+    assert TR * TC // 4 <= units_max, (R, K, splits)
+    return TR, TC
+
 
 @dataclass
 class LRSchedule:
@@ -259,6 +300,7 @@ class Engine:
         from ..parallel.dist import gpu_shared_by_ranks
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")
+        self.opt_fused = bool(tune.get("opt_fused"))
         # (never on a GPU shared by several ranks: its grids need every CU to themselves)
         ok = pm != 0 and not gpu_shared_by_ranks() and _persist.supported(self)
         self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
@@ -353,6 +395,7 @@ class Engine:
             segs.append(rec)
         seg_arr = np.array(segs, dtype=SEG_DTYPE)
         assert SEG_DTYPE.itemsize == self.nat.param_seg_bytes()
+        self.seg_arr, self.seg_names = seg_arr, [s.name for s in ps.train_slots]
         self.segs = torch.from_numpy(seg_arr.view(np.uint8).copy()).to(self.device)
         self.nseg = len(segs)
         # OHWI transpose tiles (ohwi_pack): ceil(taps*C/64) x ceil(K/64) per weight
@@ -1248,22 +1291,68 @@ class Engine:
 
         self._emit_optimizer(plan)
 
-    def _emit_optimizer(self, plan):
+    def _sgd_tiles_work(self, slabs):
+        """The work map of the one-launch optimizer (csrc/optim.hip sgd_tiles_kernel): per
+        parameter segment its slab (split-K partials still to be summed, or none: the
+        gradient is in `grad`) and its first workgroup; weights with bf16 copies or slabs
+        go in tiles of their HWIO master (opt_tile), other tensors in 1024-element chunks."""
+        work = np.zeros(self.nseg, dtype=OPTW_DTYPE)
+        blk = []
+        gptr = self.grad.data_ptr()
+        for i, (rec, name) in enumerate(zip(self.seg_arr, self.seg_names)):
+            d = slabs.get(name)
+            taps, C, K = int(rec["kh"] * rec["kw"]), int(rec["C"]), int(rec["K"])
+            tiled = d is not None or rec["bf_ohwi"] >= 0 or rec["bf_hwio"] >= 0
+            part, splits, kslab, cslab = 0, 0, 0, 0
+            if d is not None:
+                part, grad, splits, kslab, Kv, dtaps, cslab, Cv = d
+                assert (grad, Kv, dtaps, Cv) == (gptr + 4 * int(rec["offset"]), K, taps, C), name
+                assert kslab >= K and cslab >= C and part % 16 == 0, name
+            tr = tc = 0
+            if tiled:
+                assert taps * C * K == rec["numel"], name
+                tr, tc = opt_tile(taps * C, K, splits, cslab or C, C, taps)
+                n = _ceil(taps * C, tr) * _ceil(K, tc)
+            else:
+                n = _ceil(int(rec["numel"]), 1024)
+            work[i] = (part, len(blk), splits, kslab, cslab, int(tiled), tr, tc)
+            blk += [i] * n
+        assert OPTW_DTYPE.itemsize == self.nat.opt_work_bytes()
+        assert not set(slabs) - set(self.seg_names), "slab without a parameter segment"
+        wt = torch.from_numpy(work.view(np.uint8).copy()).to(self.device)
+        bt = torch.tensor(blk, dtype=torch.int32, device=self.device)
+        self._keep += [wt, bt]
+        return wt, bt, len(blk)
+
+    def _emit_optimizer(self, plan, fused_slabs=None):
         """Optimizer segment (fused SGD-momentum + wd + bf16 re-pack, global_step += 1)
-        and the `cost` segment (1/2 sum v^2 of the weights)."""
+        and the `cost` segment (1/2 sum v^2 of the weights).  fused_slabs (a dict, the
+        persistent step): ONE sgd_tiles launch that also sums those weights' slabs."""
         spec = self.spec
         sp = self.scalars.data_ptr()
         b2 = plan.size()
         s = self.sched
-        plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
-                             self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
-                             s.warm_from, s.warm_to, list(s.bounds), list(s.values),
-                             self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
-                             int(self.use_momentum), self.segs.data_ptr(), self.nseg,
-                             self.wbf.data_ptr(), sp + 8, 1)
-        plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
-                       self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles, self.wbf.data_ptr(),
-                       self.gstep.data_ptr())   # + global_step += 1
+        if fused_slabs is not None:
+            assert not self.stem_s2d
+            wt, bt, nblk = self._sgd_tiles_work(fused_slabs)
+            if not hasattr(self, "opt_ticket"):
+                self.opt_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+            plan.sgd_tiles(self.params.master.data_ptr(), self.grad.data_ptr(),
+                           self.mom.data_ptr(), s.init, s.warm_steps, s.warm_from, s.warm_to,
+                           list(s.bounds), list(s.values), self.gstep.data_ptr(), self.momentum,
+                           self.wd, 1.0, int(self.use_momentum), self.segs.data_ptr(),
+                           wt.data_ptr(), bt.data_ptr(), nblk, self.wbf.data_ptr(), sp + 8,
+                           self.opt_ticket.data_ptr())   # + global_step += 1
+        else:
+            plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
+                                 self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
+                                 s.warm_from, s.warm_to, list(s.bounds), list(s.values),
+                                 self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
+                                 int(self.use_momentum), self.segs.data_ptr(), self.nseg,
+                                 self.wbf.data_ptr(), sp + 8, 1)
+            plan.ohwi_pack(self.params.master.data_ptr(), self.segs.data_ptr(),
+                           self.ohwi_tile0.data_ptr(), self.nseg, self.ohwi_tiles,
+                           self.wbf.data_ptr(), self.gstep.data_ptr())   # + global_step += 1
         if self.stem_s2d:
             plan.stem_s2d_pack(self.stem_master, self.stem_w4.data_ptr(), spec.stem.cout)
         self._t_opt_end = plan.timing_point("opt_end")
@@ -1345,8 +1434,14 @@ class Engine:
         # every CU (nothing can overlap it): ONE grouped reduce of all the slabs, then
         # (world > 1) ONE all-reduce of the whole gradient -- the per-bucket launches of
         # the per-layer plan only pay off when they overlap a backward (bs16: 6 reduce
-        # launches 32 us vs 1)
-        self._emit_reduce(plan, [n for (_, _, names) in self.buckets for n in names])
+        # launches 32 us vs 1).  With nothing to all-reduce and opt_fused, the slabs are
+        # summed by the optimizer launch itself (sgd_tiles).
+        all_names = [n for (_, _, names) in self.buckets for n in names]
+        slabs = None
+        if self.opt_fused and not self.reduce_buckets:
+            slabs = {n: self._pending.pop(n) for n in all_names if n in self._pending}
+        else:
+            self._emit_reduce(plan, all_names)
         for bi, (lo, hi, names) in enumerate(self.buckets):
             self._mark(plan, *names)
             self._flushed.add(bi)
@@ -1357,7 +1452,24 @@ class Engine:
         self._join_comm(plan)
         self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
-        self._emit_optimizer(plan)
+        self._emit_optimizer(plan, fused_slabs=(slabs or {}) if self.opt_fused else None)
+        if slabs:
+            # not part of the step: the slab sums alone, for callers that want this
+            # step's gradient without the update (forward_backward)
+            b4 = plan.size()
+            self._pending.update(slabs)
+            self._emit_reduce(plan, list(slabs))
+            self.seg["gsum"] = (b4, plan.size())
+
+    def forward_backward(self, st=None):
+        """Forward + backward of the current batch with `grad` complete and no update
+        (the persistent step on one GPU otherwise leaves its weight-gradient slabs to
+        the optimizer launch)."""
+        st = torch.cuda.current_stream().cuda_stream if st is None else st
+        self._run("fwd", st)
+        self._run_bwd(st)
+        if "gsum" in self.seg:
+            self._run("gsum", st)
 
     def persist_error(self) -> bool:
         """Whether a persistent launch's barrier wait ever timed out (diagnostics)."""

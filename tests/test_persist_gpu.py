@@ -15,8 +15,8 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-def _engine(monkeypatch, spec, N, gpu, persist, input_mode="nhwc", slices=-1):
-    monkeypatch.setenv("DTR_TUNE", f"persist={persist},persist_slices={slices}")
+def _engine(monkeypatch, spec, N, gpu, persist, input_mode="nhwc", slices=-1, opt_fused=1):
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist},persist_slices={slices},opt_fused={opt_fused}")
     eng = Engine(spec, N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu,
                  input_mode=input_mode, use_graph=False)
     assert eng.persist == (persist == 1)
@@ -84,8 +84,7 @@ def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N, slices):
     store.master.copy_(ep.params.master)
     store.stats.copy_(ep.params.stats)
     st = torch.cuda.current_stream().cuda_stream
-    ep._run("fwd", st)
-    ep._run_bwd(st)
+    ep.forward_backward(st)
     torch.cuda.synchronize()
     assert not ep.persist_error()
     model = TorchResNet(spec, store, emulate_bf16=True)
@@ -120,8 +119,7 @@ def test_persistent_step_within_bf16_noise_deep(gpu, monkeypatch, size, N):
         out[emu] = (xent.item(), store.master.grad.detach().clone())
     st = torch.cuda.current_stream().cuda_stream
     for e in (ep, er):
-        e._run("fwd", st)
-        e._run_bwd(st)
+        e.forward_backward(st)
     torch.cuda.synchronize()
     assert not ep.persist_error()
     (x_emu, g_emu), (_, g_32) = out[True], out[False]
@@ -145,8 +143,7 @@ def test_persistent_step_is_deterministic(gpu, monkeypatch):
     st = torch.cuda.current_stream().cuda_stream
     out = []
     for _ in range(3):
-        eng._run("fwd", st)
-        eng._run_bwd(st)
+        eng.forward_backward(st)
         torch.cuda.synchronize()
         out.append(eng.grad.clone())
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
@@ -203,8 +200,7 @@ def test_persistent_step_bitwise_under_concurrent_load(gpu, monkeypatch, slices)
     imgs, labels = _batch(spec, N, gpu)
     eng.set_batch(imgs, labels)
     st = torch.cuda.current_stream()
-    eng._run("fwd", st.cuda_stream)
-    eng._run_bwd(st.cuda_stream)
+    eng.forward_backward(st.cuda_stream)
     torch.cuda.synchronize()
     ref = eng.grad.clone()
     noise = torch.cuda.Stream(device=gpu)
@@ -214,8 +210,47 @@ def test_persistent_step_bitwise_under_concurrent_load(gpu, monkeypatch, slices)
             torch.cuda._sleep(20000 * (i + 1))   # one CU busy for ~10-60 us
             for _ in range(2):
                 big.add_(1.0)
-        eng._run("fwd", st.cuda_stream)
-        eng._run_bwd(st.cuda_stream)
+        eng.forward_backward(st.cuda_stream)
         torch.cuda.synchronize()
         assert not eng.persist_error()
         assert torch.equal(eng.grad, ref), f"run {i}: gradient differs under concurrent load"
+
+
+@pytest.mark.parametrize("N", [16, 128])
+def test_fused_optimizer_matches_unfused(gpu, monkeypatch, N):
+    """opt_fused (ONE sgd_tiles launch: slab sums + SGD-momentum + both bf16 copies +
+    global_step) vs the grouped reduce + sgd_pack + ohwi_pack launches
+    from the same weights on the same batch: after one step the gradients are equal bit
+    for bit (N = 128: 32-split slabs, summed in the grouped reduce's order), weights,
+    momenta and the bf16 copies agree to fp32 rounding (the update's fma contraction),
+    and the ticket re-arms (global_step counts every step)."""
+    spec = cifar_spec(20)
+    ef = _engine(monkeypatch, spec, N, gpu, 1, input_mode="cifar_u8", opt_fused=1)
+    eu = _engine(monkeypatch, spec, N, gpu, 1, input_mode="cifar_u8", opt_fused=0)
+    assert "gsum" in ef.seg and "gsum" not in eu.seg
+    eu.params.master.copy_(ef.params.master)
+    eu.params.stats.copy_(ef.params.stats)
+    eu.repack()
+    for e in (ef, eu):
+        e.fill_synthetic(0)
+    for e in (ef, eu):
+        e.step()
+    torch.cuda.synchronize()
+    assert not ef.persist_error() and not eu.persist_error()
+    mf, mu = ef.metrics(reduce=False), eu.metrics(reduce=False)
+    assert mf["global_step"] == mu["global_step"] == 1
+    assert mf["lr"] == mu["lr"]
+    print("rel grad", _rel(ef.grad, eu.grad), "master", _rel(ef.params.master, eu.params.master),
+          "mom", _rel(ef.mom, eu.mom), "wbf", _rel(ef.wbf, eu.wbf))
+    assert torch.equal(ef.grad, eu.grad)   # the grouped reduce's summation order
+    assert _rel(ef.params.master, eu.params.master) < 1e-6
+    assert _rel(ef.mom, eu.mom) < 1e-5
+    assert _rel(ef.wbf, eu.wbf) < 1e-3
+    # (later steps drift apart: a deep bf16 network amplifies the last-bit differences of
+    # the N = 128 slab sums) -- the step counter and the ticket keep counting
+    for _ in range(2):
+        ef.step()
+    torch.cuda.synchronize()
+    assert ef.metrics(reduce=False)["global_step"] == 3
+    assert ef.opt_ticket.item() == 0
+    assert torch.isfinite(ef.params.master).all()
