@@ -473,8 +473,8 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
 // dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N, P,
 // classes, kpad, update_moving, wgrad_wgs]; floats = [grad_scale, momentum, eps].
 static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::vector<float> f) {
-  if (p.size() != 16 || n.size() != 8 || f.size() != 3)
-    throw std::invalid_argument("prn: 16 pointers, 8 ints, 3 floats");
+  if (p.size() != 20 || n.size() != 8 || f.size() != 3)
+    throw std::invalid_argument("prn: 20 pointers, 8 ints, 3 floats");
   PrnArgs a{};
   a.blocks = P<const PrnBlock>(p[0]);
   a.bns = P<const PrnBn>(p[1]);
@@ -492,6 +492,10 @@ static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::ve
   a.dpool = P<float>(p[13]);
   a.dx0 = P<bf16>(p[14]);
   a.items = P<const PrnItem>(p[15]);
+  a.loss_sum = P<float>(p[16]);
+  a.correct = P<float>(p[17]);
+  a.dbias = P<float>(p[18]);
+  a.dense_grad = P<float>(p[19]);
   a.nblocks = n[0];
   a.nitems = n[1];
   a.N = n[2];
@@ -507,7 +511,8 @@ static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::ve
     throw std::invalid_argument("prn: unsupported shape");
   if (mode == 0) return [a](hipStream_t s) { prn_forward(a, s); };
   if (mode == 1) return [a, wgs](hipStream_t s) { prn_backward(a, wgs, s); };
-  throw std::invalid_argument("prn: mode 0 (forward) or 1 (backward)");
+  if (mode == 2) return [a](hipStream_t s) { prn_head(a, s); };
+  throw std::invalid_argument("prn: mode 0 (forward), 1 (backward) or 2 (head folds)");
 }
 
 // bn_bwd_apply with the finalize fused in: fin = [acc, gamma, dgamma, dbeta, coef]

@@ -1590,6 +1590,95 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
   return true;
 }
 
+// The head's batch folds in one workgroup, launched on the main stream right after the
+// backward launch: the loss / precision / bias-gradient folds of
+// softmax_xent_reduce_kernel (head.hip, same thread mapping and order) and the dense
+// weight gradient pooled^T x dlogits (bf16 operands staged in LDS, fp32 sums over the
+// images in order).  These were a side-stream softmax_xent_reduce + conv_wgrad pair
+// whose fork and join events cost ~11 us per step between the launches.  (Run by the
+// backward launch's first weight-gradient workgroup instead, this code perturbed the
+// register allocation of the whole backward kernel: 76 -> 272 B of scratch per lane,
+// +55 us per step.)
+__device__ void prn_head_fold(const PrnArgs& a, char* smem, int tid) {
+  const int N = a.N, ld = a.kpad, classes = a.classes;
+  // every operand into LDS with one round of 16-byte loads: the fp32 gradient rows and
+  // the per-image (loss, correct) pairs of the softmax workspace, pooled [N][64] and
+  // dlogits [N][ld] (bf16); rows of 64 and ld (% 16) elements are whole 16-B chunks,
+  // the pair block goes in 8-byte pieces
+  float* red = reinterpret_cast<float*>(smem);           // [4][64]
+  float* sw = red + 256;                                  // [N][ld] + [N][2]
+  bf16* sp = reinterpret_cast<bf16*>(sw + ((N * ld + 2 * N + 3) & ~3));   // 16-B aligned
+  bf16* sd = sp + N * 64;
+  for (int i = tid; i < N * ld / 4; i += PT)
+    reinterpret_cast<f32x4*>(sw)[i] = ldg(reinterpret_cast<const f32x4*>(a.ws) + i);
+  for (int i = tid; i < N; i += PT)
+    reinterpret_cast<float2*>(sw + N * ld)[i] = ldg(reinterpret_cast<const float2*>(a.ws + N * ld) + i);
+  for (int i = tid; i < N * 8; i += PT)
+    reinterpret_cast<uint4*>(sp)[i] = ldg(reinterpret_cast<const uint4*>(a.pooled) + i);
+  for (int i = tid; i < N * ld / 8; i += PT)
+    reinterpret_cast<uint4*>(sd)[i] = ldg(reinterpret_cast<const uint4*>(a.dlogits) + i);
+  __syncthreads();
+  const int lane = tid & 63, q = tid >> 6;
+  if (q < 4) {   // bias gradient: thread (class, row slice q) sums rows q, q + 4, ...
+    float t = 0.f;
+    if (lane < classes) {
+#pragma unroll 8
+      for (int r = q; r < N; r += 4) t += sw[r * ld + lane];
+    }
+    red[q * 64 + lane] = t;
+  } else if (q == 4) {   // loss and precision
+    const float* rs = sw + N * ld;
+    float l = 0.f, k = 0.f;
+    for (int r = lane; r < N; r += 64) {
+      l += rs[2 * r];
+      k += rs[2 * r + 1];
+    }
+    l = wave_sum(l);
+    k = wave_sum(k);
+    if (lane == 0) {
+      stg(a.loss_sum, l);
+      stg(a.correct, k);
+    }
+  }
+  // dense weight gradient: thread (f = tid % 64, image chunk tid / 64 of 8) holds 16
+  // classes' sums in registers over its images (the dlogits row is a broadcast LDS read),
+  // the 8 chunk partials are added in chunk order through LDS.  (One thread per output
+  // over all images ran 10-14 us: ~2.5k LDS instructions queued on this one CU.)
+  static_assert(PT == 512, "8 image chunks of 64 threads");
+  float* part = reinterpret_cast<float*>(sd + ((N * ld + 7) & ~7));   // [8][64][16]
+  {
+    const int f = tid & 63, c = tid >> 6;
+    const int n0 = (N * c) >> 3, n1 = (N * (c + 1)) >> 3;
+    for (int k0 = 0; k0 < classes; k0 += 16) {   // ld % 16 == 0: k0 + 15 < ld
+      float acc[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      for (int n = n0; n < n1; ++n) {
+        const float x = (float)sp[n * 64 + f];
+        const bf16* drow = sd + n * ld + k0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] += x * (float)drow[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) part[(c * 64 + f) * 16 + j] = acc[j];
+      __syncthreads();
+      for (int o = tid; o < 64 * 16; o += PT) {
+        const int ff = o >> 4, j = o & 15;
+        if (k0 + j < classes) {
+          float t = part[ff * 16 + j];
+#pragma unroll
+          for (int cc = 1; cc < 8; ++cc) t += part[(cc * 64 + ff) * 16 + j];
+          stg(a.dense_grad + ff * classes + k0 + j, t);   // HWIO [64][classes]
+        }
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (q == 0 && lane < classes)
+    stg(a.dbias + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
+}
+
 template <int P>
 __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1612,6 +1701,11 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
     run_item(it, smem, wave, lane);
   }
+}
+
+__global__ void __launch_bounds__(PT, 1) prn_head_kernel(PrnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  prn_head_fold(a, smem, threadIdx.x);
 }
 
 // ---- host ------------------------------------------------------------------------------
@@ -1646,6 +1740,17 @@ void prn_forward(const PrnArgs& a, hipStream_t s) {
   if (a.P == 1) hipLaunchKernelGGL(prn_fwd_kernel<1>, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
   else if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_fwd_kernel<4>, dim3(a.N * 4), dim3(PT), LDS_TOTAL, s, b);
+  DTR_CHECK_LAUNCH();
+}
+
+void prn_head(const PrnArgs& a, hipStream_t s) {
+  if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad) || a.N > 240 || !a.dense_grad ||
+      !a.loss_sum || !a.correct || !a.dbias)
+    throw std::invalid_argument("prn_head: unsupported shape or missing outputs");
+  const size_t lds = 1024 + 32 + (size_t)a.N * ((64 + a.kpad) * sizeof(bf16) + (a.kpad + 2) * sizeof(float)) +
+                    8 * 64 * 16 * sizeof(float);
+  if (lds > LDS_TOTAL) throw std::invalid_argument("prn_head: batch too large for LDS");
+  hipLaunchKernelGGL(prn_head_kernel, dim3(1), dim3(PT), lds, s, a);
   DTR_CHECK_LAUNCH();
 }
 

@@ -279,6 +279,11 @@ struct PrnArgs {
   bf16* dlogits;             // [N][kpad]
   float* ws;                 // softmax_xent workspace: [N][kpad] gradient rows, then [N][2]
   float* dpool;              // [N][64] fp32: average-pool gradient per channel (dact)
+  // the head's batch folds (prn_head):
+  float* loss_sum;           // sum of the per-image losses
+  float* correct;            // number of correct top-1 predictions
+  float* dbias;              // [classes] dense bias gradient
+  float* dense_grad;         // [64][classes] fp32 dense weight gradient (HWIO)
   bf16* dx0;                 // backward: gradient of the stem output [N][32][32][16]
   const PrnItem* items;      // backward weight-gradient items, in readiness order
   int nitems;
@@ -294,6 +299,8 @@ bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
 void prn_forward(const PrnArgs& a, hipStream_t s);
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);
+// the head's batch folds (loss, precision, dense bias + weight gradients), one workgroup
+void prn_head(const PrnArgs& a, hipStream_t s);
 // item kind of a conv (stage of its output, kernel size, stride; stem = 8 input channels)
 int prn_item_kind(int cin, int cout, int ksize, int stride);
 

@@ -253,6 +253,22 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
     const int r0 = (t / tc_n) * TR, c0 = (t - (t / tc_n) * tc_n) * TC;
     const int nr = min(TR, R - r0), nc = min(TC, K - c0);   // valid extent
     const bool slab = ow.part != nullptr;
+    const int lc = __builtin_ctz(TC);                         // TC: a power of two
+    // this thread's elements' master, momentum and (no slab) gradient, loaded before
+    // the slab sums so the two rounds of loads overlap (TR * TC <= 16 x 256)
+    constexpr int EPT = 16;
+    float wr[EPT], mr[EPT], gr[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int q = tid + j * 256, rl = q >> lc, cl = q & (TC - 1);
+      wr[j] = mr[j] = gr[j] = 0.f;
+      if (q < TR * TC && rl < nr && cl < nc) {
+        const long e = sg.offset + (long)(r0 + rl) * K + c0 + cl;
+        wr[j] = w[e];
+        if (use_momentum) mr[j] = mom[e];
+        if (!slab) gr[j] = g[e];
+      }
+    }
     if (slab) {
       // slab columns: the tile's rows (cslab == C: column n = row r, nr % 4 == 0) or,
       // for padded rows (the stem: C = 3 in rows of cslab; one row tile), all of them
@@ -308,23 +324,21 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
     }
     __syncthreads();         // gt and lr_s
     const float lr = lr_s;
-#pragma unroll 4
-    for (int q = tid; q < TR * TC; q += 256) {
-      const int rl = q / TC, cl = q - rl * TC;
-      if (rl < nr && cl < nc) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int q = tid + j * 256, rl = q >> lc, cl = q & (TC - 1);
+      if (q < TR * TC && rl < nr && cl < nc) {
         const int r = r0 + rl, co = c0 + cl;
         const long e = sg.offset + (long)r * K + co;
-        float gv;
+        float gv = gr[j];
         if (slab) {
           gv = gt[cl][rl];
           g[e] = gv;
-        } else {
-          gv = g[e];
         }
-        float wv = w[e];
+        float wv = wr[j];
         gv = gv * grad_scale + wd * wv;
         if (use_momentum) {
-          const float a = momentum * mom[e] + gv;
+          const float a = momentum * mr[j] + gv;
           mom[e] = a;
           wv -= lr * a;
         } else {

@@ -1371,10 +1371,10 @@ class Engine:
 
     def _build_persist_plan(self):
         """The persistent small-batch step (train/persist.py): input, ONE forward launch;
-        the head's batch folds and the dense weight gradient on the side stream; ONE
-        backward launch (dgrad chain + BN backward on one workgroup per image, weight
-        gradients on the remaining CUs); the grouped slab reduces and bucket all-reduces;
-        the optimizer."""
+        ONE backward launch (dgrad chain + BN backward on the image row-slice workgroups,
+        the weight gradients on the remaining CUs); the head's batch folds; on one GPU
+        the optimizer launch (sum of the weight-gradient slabs included), else the
+        grouped slab reduce, ONE all-reduce and the optimizer."""
         plan, spec, N = self.plan, self.spec, self.N
         self.seg = {}
         for e in self.bns.values():
@@ -1404,32 +1404,11 @@ class Engine:
         self._side_q, self._side_blocks = [], 0
         self._main_wgrad = False
         self._reduce_main = True   # the slab reduces run on the main stream
-        sp = self.scalars.data_ptr()
-        F = spec.dense_in
-        off, spl, pps = self.wg_off["dense"]
-        dpart = self.wg_part.data_ptr() + 4 * off
-        self._pending[self.dense_name] = (dpart, self.dense_grad, spl, self.kpad,
-                                          spec.num_classes, 1, F, F)
         self._produced.add(self.dense_name)
-        side = self.fork_wgrad
-        if side:   # the head's batch folds + the dense wgrad overlap the backward launch
-            ev = plan.new_event()
-            plan.record(ev)
-            plan.use_stream(1)
-            plan.wait(ev)
-        plan.softmax_xent_reduce(self.xent_ws.data_ptr(), self.kpad, N, spec.num_classes, sp,
-                                 sp + 4, self.dense_bias_grad)
-        plan.conv_wgrad(self.dlogits.data_ptr(), self.pooled.data_ptr(), 0, 0, dpart,
-                        self._dense_geom(N), spl, pps)
-        if side:
-            plan.use_stream(0)
         plan.prn(1, ptrs, ints, floats)
-        if side:
-            ev = plan.new_event()
-            plan.use_stream(1)
-            plan.record(ev)
-            plan.use_stream(0)
-            plan.wait(ev)
+        # the head's batch folds (loss, precision, dense bias and weight gradients): one
+        # workgroup on the main stream -- no side stream, no fork/join events
+        plan.prn(2, ptrs, ints, floats)
         # every slab is complete when the backward launch ends, and that launch holds
         # every CU (nothing can overlap it): ONE grouped reduce of all the slabs, then
         # (world > 1) ONE all-reduce of the whole gradient -- the per-bucket launches of

@@ -232,6 +232,10 @@ class PersistStep:
                 eng.labels.data_ptr(), eng.pooled.data_ptr(), eng.dlogits.data_ptr(),
                 eng.xent_ws.data_ptr(), self.dpool.data_ptr(), self.dx0.data_ptr(),
                 self.item_dev.data_ptr()]
+        # backward / head-fold launches: the head's batch folds' outputs (loss, precision,
+        # dense bias and weight gradients; prn_head)
+        sp = eng.scalars.data_ptr()
+        ptrs += [0, 0, 0, 0] if fwd else [sp, sp + 4, eng.dense_bias_grad, eng.dense_grad]
         ints = [self.nblocks, len(self.items), eng.N, self.P_fwd if fwd else self.P,
                 spec.num_classes, eng.kpad, 1,
                 self.wgrad_wgs]
