@@ -26,6 +26,8 @@ def run(acc, size, N):
     torch.cuda.synchronize()
     stats = {n: (b.mean.clone(), b.rstd.clone()) for n, b in eng.bns.items()}
     eng._run("bwd", st)
+    if "gsum" in eng.seg:   # persistent step on one GPU: the slab sums
+        eng._run("gsum", st)
     torch.cuda.synchronize()
     grads = {s.name: eng.grad[s.offset:s.offset + s.numel].clone() for s in eng.params.train_slots}
     return stats, grads, eng.scalars[0].item()

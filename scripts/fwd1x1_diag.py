@@ -28,6 +28,8 @@ def run(mode):
     acts = {f"X{i}": t.float().clone() for i, t in enumerate(eng.X)}
     bn = {n: (b.mean.clone(), b.rstd.clone(), b.scale.clone()) for n, b in eng.bns.items()}
     eng._run("bwd", st)
+    if "gsum" in eng.seg:   # persistent step on one GPU: the slab sums
+        eng._run("gsum", st)
     torch.cuda.synchronize()
     return spec, acts, bn, eng.grad.clone(), eng.scalars[0].item()
 

@@ -40,8 +40,7 @@ def _make(spec, N, gpu, wd=2e-4):
 def _grads(spec, N, gpu):
     eng, imgs, labels, ref_store = _make(spec, N, gpu)
     st = torch.cuda.current_stream().cuda_stream
-    eng._run("fwd", st)
-    eng._run("bwd", st)
+    eng.forward_backward(st)
     torch.cuda.synchronize()
     out = {}
     for emu in (True, False):
@@ -187,8 +186,7 @@ def test_bn_accumulator_mode_matches_partials(gpu, monkeypatch):
         monkeypatch.setenv("DTR_TUNE", f"bn_acc={mode},persist=0")
         eng, _, _, _ = _make(spec, 64, gpu)
         st = torch.cuda.current_stream().cuda_stream
-        eng._run("fwd", st)
-        eng._run("bwd", st)
+        eng.forward_backward(st)
         torch.cuda.synchronize()
         res[mode] = (eng.scalars[0].item(), eng.grad.clone(), eng.params.stats.clone())
     (l0, g0, s0), (l1, g1, s1) = res["0"], res["1"]
@@ -207,8 +205,7 @@ def test_fused_head_matches_unfused(gpu, monkeypatch):
         eng, _, _, _ = _make(spec, 64, gpu)
         assert eng._head_fused == (mode == "1")
         st = torch.cuda.current_stream().cuda_stream
-        eng._run("fwd", st)
-        eng._run("bwd", st)
+        eng.forward_backward(st)
         torch.cuda.synchronize()
         res[mode] = (eng.scalars[:2].clone(), eng.grad.clone(), eng.params.stats.clone())
     (s0, g0, t0), (s1, g1, t1) = res["0"], res["1"]
@@ -230,8 +227,7 @@ def test_bn_backward_apply_recompute_matches_separate_apply(gpu, monkeypatch):
         monkeypatch.setenv("DTR_TUNE", f"bap_maxc={mode},persist=0")
         eng, _, _, _ = _make(spec, 8, gpu)
         st = torch.cuda.current_stream().cuda_stream
-        eng._run("fwd", st)
-        eng._run("bwd", st)
+        eng.forward_backward(st)
         torch.cuda.synchronize()
         res[mode] = (eng.scalars[0].item(), eng.grad.clone(), eng.params.stats.clone(),
                      eng.n_bap)

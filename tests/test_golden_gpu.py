@@ -74,8 +74,7 @@ def test_full_depth_training_step_from_trained_weights(gpu, trained):
     labels = torch.randint(0, 10, (N,), device=gpu)
     eng.set_batch(imgs, labels)
     st = torch.cuda.current_stream().cuda_stream
-    eng._run("fwd", st)
-    eng._run("bwd", st)
+    eng.forward_backward(st)
     torch.cuda.synchronize()
 
     ref = {}

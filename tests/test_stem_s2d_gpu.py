@@ -75,8 +75,7 @@ def _engine(spec, monkeypatch, gpu, s2d, imgs, labels, master, stats):
         eng.repack()
     eng.set_batch(imgs, labels)
     st = torch.cuda.current_stream().cuda_stream
-    eng._run("fwd", st)
-    eng._run("bwd", st)
+    eng.forward_backward(st)
     torch.cuda.synchronize()
     return eng
 
