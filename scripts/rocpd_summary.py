@@ -34,7 +34,7 @@ def main():
     rows = c.execute("select name, start, end, duration, grid_x, grid_y, grid_z, lds_size, "
                      "vgpr_count, accum_vgpr_count, stream_id from kernels order by start").fetchall()
     # one optimizer launch per step: the window starts after the (K+1)-th-from-last one
-    opt = [i for i, r in enumerate(rows) if "sgd_pack_kernel" in r[0]]
+    opt = [i for i, r in enumerate(rows) if "sgd_pack_kernel" in r[0] or "sgd_tiles_kernel" in r[0]]
     if len(opt) < steps + 1:
         raise SystemExit(f"found {len(opt)} optimizer launches, need > {steps}")
     lo, hi = opt[-steps - 1] + 1, opt[-1] + 1
