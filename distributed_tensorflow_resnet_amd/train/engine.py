@@ -989,20 +989,25 @@ class Engine:
                 self._mark(plan, *names)
                 self._flushed.add(bi)
 
-    def _emit_allreduce(self, plan, lo: int, hi: int, side_dep: bool):
+    def _emit_allreduce(self, plan, lo: int, hi: int, side_dep: bool, on_main: bool = False):
         """Fork the comm stream off the main stream (and, with ``side_dep``, off the
         side stream, where the bucket's split-K reduces ran) at the bucket's ready
         point and all-reduce grad[lo:hi) there (bf16 exchange: cast kernels on the
-        comm stream around a bf16 all-reduce), while the compute streams continue."""
-        evs = [plan.new_event()]
-        plan.record(evs[0])
-        if side_dep:
-            evs.append(plan.new_event())
-            plan.use_stream(1)
-            plan.record(evs[1])
-        plan.use_stream(2)
-        for ev in evs:
-            plan.wait(ev)
+        comm stream around a bf16 all-reduce), while the compute streams continue.
+        ``on_main``: on the main stream itself, no fork and no join (the persistent
+        step: nothing is left to overlap, and each event costs ~5 us between launches)."""
+        if on_main:
+            assert not side_dep
+        else:
+            evs = [plan.new_event()]
+            plan.record(evs[0])
+            if side_dep:
+                evs.append(plan.new_event())
+                plan.use_stream(1)
+                plan.record(evs[1])
+            plan.use_stream(2)
+            for ev in evs:
+                plan.wait(ev)
         n = hi - lo
         g = self.grad.data_ptr() + 4 * lo
         if self.grad_bf16 is not None:
@@ -1013,12 +1018,13 @@ class Engine:
         else:
             plan.all_reduce(self.comm, g, n, self.nat.COMM_F32)
         self._n_allreduce += 1
+        self._comm_forks += 0 if on_main else 1
         self._allreduce_bytes += n * (2 if self.grad_bf16 is not None else 4)
         plan.use_stream(0)
 
     def _join_comm(self, plan):
         """The optimizer (main stream) waits for every bucket's all-reduce."""
-        if self.comm is None or not self._n_allreduce:
+        if self.comm is None or not self._comm_forks:
             return
         ev = plan.new_event()
         plan.use_stream(2)
@@ -1061,7 +1067,7 @@ class Engine:
         self.seg = {}
         for e in self.bns.values():
             e.pending = None
-        self._n_allreduce, self._allreduce_bytes = 0, 0
+        self._n_allreduce, self._allreduce_bytes, self._comm_forks = 0, 0, 0
         b0 = plan.size()
         self._t_fwd0 = plan.timing_point("fwd_begin")
         # the step's BN accumulators start at zero: cleared by the CIFAR augmentation
@@ -1379,7 +1385,7 @@ class Engine:
         self.seg = {}
         for e in self.bns.values():
             e.pending = None
-        self._n_allreduce, self._allreduce_bytes = 0, 0
+        self._n_allreduce, self._allreduce_bytes, self._comm_forks = 0, 0, 0
         self._head_fused = False
         b0 = plan.size()
         self._t_fwd0 = plan.timing_point("fwd_begin")
@@ -1426,7 +1432,7 @@ class Engine:
             self._flushed.add(bi)
         if self.comm is not None:
             self._emit_allreduce(plan, min(b[0] for b in self.buckets),
-                                 max(b[1] for b in self.buckets), side_dep=False)
+                                 max(b[1] for b in self.buckets), side_dep=False, on_main=True)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
         self._join_comm(plan)
         self._t_joined = plan.timing_point("allreduce_joined")

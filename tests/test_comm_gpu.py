@@ -51,7 +51,10 @@ def test_native_comm_single_rank_is_identity(gpu, monkeypatch, persist):
     names = eng.plan.names()
     assert names.count("all_reduce") == info["allreduce_ops"]
     streams = eng.plan.op_streams()
-    assert all(streams[i] == 2 for i, n in enumerate(names) if n == "all_reduce")
+    # per-layer plan: on the comm stream, overlapping the backward; persistent step: on
+    # the main stream (nothing left to overlap; no fork/join events)
+    want = 2 if persist == "0" else 0
+    assert all(streams[i] == want for i, n in enumerate(names) if n == "all_reduce")
     for _ in range(3):
         ref.step()
         eng.step()
