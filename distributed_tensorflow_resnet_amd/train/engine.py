@@ -301,6 +301,7 @@ class Engine:
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")
         self.opt_fused = bool(tune.get("opt_fused"))
+        self.opt_fused_layer = bool(tune.get("opt_fused_layer"))
         # (never on a GPU shared by several ranks: its grids need every CU to themselves)
         ok = pm != 0 and not gpu_shared_by_ranks() and _persist.supported(self)
         self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
@@ -1295,7 +1296,7 @@ class Engine:
         self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
 
-        self._emit_optimizer(plan)
+        self._emit_optimizer(plan, fused_slabs={} if self.opt_fused_layer else None)
 
     def _sgd_tiles_work(self, slabs):
         """The work map of the one-launch optimizer (csrc/optim.hip sgd_tiles_kernel): per
@@ -1339,7 +1340,6 @@ class Engine:
         b2 = plan.size()
         s = self.sched
         if fused_slabs is not None:
-            assert not self.stem_s2d
             wt, bt, nblk = self._sgd_tiles_work(fused_slabs)
             if not hasattr(self, "opt_ticket"):
                 self.opt_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)

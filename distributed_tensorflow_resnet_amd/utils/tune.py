@@ -59,6 +59,9 @@ ENGINE = {
     "opt_fused": (1, "the persistent step's optimizer as ONE launch (split-K slab sums on "
                      "one GPU, SGD-momentum, both bf16 weight copies: sgd_tiles) instead of "
                      "the grouped slab reduce + sgd_pack + ohwi_pack"),
+    "opt_fused_layer": (0, "the launch-per-layer plan's optimizer as ONE sgd_tiles launch too "
+                           "(SGD-momentum + both bf16 copies; its weight gradients are already "
+                           "summed) instead of sgd_pack + ohwi_pack"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 
