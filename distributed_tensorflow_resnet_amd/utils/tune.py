@@ -61,7 +61,9 @@ ENGINE = {
                      "the grouped slab reduce + sgd_pack + ohwi_pack"),
     "opt_fused_layer": (0, "the launch-per-layer plan's optimizer as ONE sgd_tiles launch too "
                            "(SGD-momentum + both bf16 copies; its weight gradients are already "
-                           "summed) instead of sgd_pack + ohwi_pack"),
+                           "summed) instead of sgd_pack + ohwi_pack; off: ImageNet RN50 176 us vs "
+                           "98 + 44 us (scalar 4-byte accesses over 25.5 M weights), steps within "
+                           "noise (10.54-10.59 ms either way), CIFAR per-layer 1.262 vs 1.267 ms"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 
