@@ -570,8 +570,17 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// fp64 accumulator replicas per BatchNorm of the persistent kernels (the per-layer
+// kernels use BN_ACC_REP; the engine sizes every BN's block for the larger count).  Each
+// workgroup adds into replica blockIdx % REP; after the barrier every workgroup reads all
+// REP replicas of its channels.  Same-box A/B, step ms bs128 / bs16
+// (profiles/cifar_persist_variants.md): 1 replica 1.058 / 0.657 (same-address atomics
+// serialise), 2: 0.887 / 0.594, 4: 0.850 / 0.595, 8: 0.862 / 0.597, 16: 0.879 / 0.627
+// (the combine's reads grow).
+constexpr int PRN_ACC_REP = 4;
+
 // Per-channel sums over this slice of two per-value quantities f(t, r, x1, x2), added to
-// a BN's fp64 accumulator replicas acc [BN_ACC_REP][2][C] (memory-side atomics; exact, so
+// a BN's fp64 accumulator replicas acc [PRN_ACC_REP][2][C] (memory-side atomics; exact, so
 // order-independent).  Folding: xor-shuffles over the 16 pixel lanes, then the waves that
 // hold each channel through LDS `red` [8 waves][128] in a fixed order.
 template <int S, int P, typename F>
@@ -625,24 +634,24 @@ __device__ __forceinline__ void bn_sums(F f, float* red, double* acc, int wave, 
         v1 += red[w * 128 + c];
         v2 += red[w * 128 + 64 + c];
       }
-    double* p = acc + (long)(blockIdx.x % BN_ACC_REP) * 2 * G::C + c;
+    double* p = acc + (long)(blockIdx.x % PRN_ACC_REP) * 2 * G::C + c;
     atomic_add_g(p, (double)v1);
     atomic_add_g(p + G::C, (double)v2);
   }
 }
 
-// After the barrier: the channel's two sums from the BN_ACC_REP replicas (sc1 loads,
+// After the barrier: the channel's two sums from the PRN_ACC_REP replicas (sc1 loads,
 // replicas added in a fixed order)
 __device__ __forceinline__ void acc_read(const double* acc, int C, int c, double& s1, double& s2) {
-  double a[BN_ACC_REP], b[BN_ACC_REP];
+  double a[PRN_ACC_REP], b[PRN_ACC_REP];
 #pragma unroll
-  for (int r = 0; r < BN_ACC_REP; ++r) {
+  for (int r = 0; r < PRN_ACC_REP; ++r) {
     a[r] = ld_sc1_d(acc + (long)r * 2 * C + c);
     b[r] = ld_sc1_d(acc + (long)r * 2 * C + C + c);
   }
   s1 = s2 = 0.0;
 #pragma unroll
-  for (int r = 0; r < BN_ACC_REP; ++r) {
+  for (int r = 0; r < PRN_ACC_REP; ++r) {
     s1 += a[r];
     s2 += b[r];
   }
@@ -1713,6 +1722,7 @@ static long long* g_prn_probe = nullptr;
 void prn_set_probe(long long* p) { g_prn_probe = p; }
 
 size_t prn_lds_bytes() { return LDS_TOTAL; }
+int prn_acc_rep() { return PRN_ACC_REP; }
 
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad) {
   return N >= 1 && (P == 1 || P == 2 || P == 4) && N * P <= 256 && nblocks >= 3 && nblocks % 3 == 0 &&

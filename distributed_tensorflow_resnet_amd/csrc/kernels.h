@@ -297,6 +297,7 @@ enum { PRN_THREADS = 512 };
 void prn_set_probe(long long* p);   // diagnostics (scripts/prn_probe.py); nullptr = off
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
+int prn_acc_rep();   // fp64 accumulator replicas per BatchNorm of the persistent kernels
 void prn_forward(const PrnArgs& a, hipStream_t s);
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);
 // the head's batch folds (loss, precision, dense bias + weight gradients), one workgroup

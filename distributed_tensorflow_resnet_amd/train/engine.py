@@ -521,7 +521,9 @@ class Engine:
         # the CIFAR direct convs: ~4 us per consumer prologue at 512 tiles).  All the
         # replicas live in one buffer zeroed by one memset at the start of the step.
         self.bn_acc_on = self.bn_bacc_on = bool(tune.get("bn_acc"))
-        rep = self.nat.bn_acc_rep()
+        # (each BN's block holds the larger of the per-layer and the persistent kernels'
+        # replica counts; a kernel uses the first replicas of the block)
+        rep = max(self.nat.bn_acc_rep(), self.nat.prn_acc_rep())
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
         # (+ N x 64 doubles and 64 more: the persistent step's average-pool sums and its
         # barrier counters / readiness line, zeroed with the accumulators at the start of
