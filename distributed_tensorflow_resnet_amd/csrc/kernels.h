@@ -12,7 +12,12 @@ namespace dtr {
 
 typedef __bf16 bf16;
 
-constexpr int BN_ACC_REP = 8;   // fp64 accumulator replicas per BatchNorm (one per XCD)
+// fp64 accumulator replicas per BatchNorm of the per-layer kernels (replica =
+// blockIdx % REP: two XCDs each).  Same-box A/B, ImageNet RN50 bs128 / per-layer CIFAR
+// bs128 step ms (profiles/bn_acc_replicas.md): 2: 10.48 / 1.429, 4: 10.47 / 1.298,
+// 8: 10.54 / 1.267, 16: 10.72 / 1.266 -- 4 for the ImageNet headline (the per-layer
+// CIFAR path only runs above 240 images per rank; the persistent step uses its own count)
+constexpr int BN_ACC_REP = 4;
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1 };
 
@@ -118,7 +123,7 @@ struct GemmArgs {
   BnBwdFin bfin;            // with bnb_part: finalize in-kernel
   // Accumulator mode of STATS / BNB: instead of (or beside) the per-tile partials,
   // every workgroup adds its tile's sums into [BN_ACC_REP][2][Ncol] fp64 replicas
-  // (replica = blockIdx.x % BN_ACC_REP, one per XCD) with memory-side atomics, so
+  // (replica = blockIdx.x % BN_ACC_REP) with memory-side atomics, so
   // a consumer reads 2 x BN_ACC_REP values per channel instead of combining every
   // tile partial.  The buffers are zeroed once per step.
   double* stat_acc;         // STATS: sum y, sum y^2
