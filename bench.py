@@ -264,10 +264,14 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
     if eng.persist_error():
         raise SystemExit(f"bench.py: rank {ctx.rank}: a persistent-step barrier wait timed "
                          "out (workgroups not co-resident?) -- the measurement is invalid")
+    # (the persistent step has no side stream: its weight gradients run inside the
+    # backward launch)
     extra = {"dtype": "bf16", "device": torch.cuda.get_device_name(device),
-             "graph": use_graph, "wgrad_stream": eng.fork_wgrad, "comm": eng.comm_info(),
+             "graph": use_graph, "wgrad_stream": bool(eng.fork_wgrad and not eng.persist),
+             "comm": eng.comm_info(),
              "step_path": ("persistent (P fwd/bwd = %d/%d)" % (eng.prn.P_fwd, eng.prn.P)
                            if eng.persist else "per-layer plan"),
+             "persist_off_reason": eng.persist_reason or None,
              "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
     return ctx, elapsed, m, extra, phases
 

@@ -471,10 +471,10 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
 // Persistent small-batch CIFAR step (cifar_persist.hip).  mode 0: forward launch, 1:
 // backward launch.  ptrs = [blocks, bns, x_in, stem_w, pool_acc, bar, err, dense_w,
 // dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N, P,
-// classes, kpad, update_moving, wgrad_wgs]; floats = [grad_scale, momentum, eps].
+// classes, kpad, update_moving, wgrad_wgs, fault_bar]; floats = [grad_scale, momentum, eps].
 static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::vector<float> f) {
-  if (p.size() != 20 || n.size() != 8 || f.size() != 3)
-    throw std::invalid_argument("prn: 20 pointers, 8 ints, 3 floats");
+  if (p.size() != 20 || n.size() != 9 || f.size() != 3)
+    throw std::invalid_argument("prn: 20 pointers, 9 ints, 3 floats");
   PrnArgs a{};
   a.blocks = P<const PrnBlock>(p[0]);
   a.bns = P<const PrnBn>(p[1]);
@@ -504,6 +504,7 @@ static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::ve
   a.kpad = n[5];
   a.update_moving = n[6];
   const int wgs = n[7];
+  a.fault_bar = n[8];
   a.grad_scale = f[0];
   a.momentum = f[1];
   a.eps = f[2];
@@ -1185,6 +1186,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("prn_set_probe", [](ptr_t p) { prn_set_probe(P<long long>(p)); },
         "diagnostics: image 0 of the persistent launches records (tag, wall clock) pairs here");
   m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, slices, blocks, classes, kpad)");
+  m.def("prn_check", &prn_check, "every host-side limit of the persistent step (N, slices, forward slices, "
+        "blocks, classes, kpad), co-residency included: '' or the reason it is unsupported");
   m.def("prn_item_kind", &prn_item_kind, "weight-gradient item kind of a conv (cin, cout, k, stride)");
   m.def("prn_struct_bytes", []() {
     return std::vector<int>{(int)sizeof(PrnBn), (int)sizeof(PrnBlock), (int)sizeof(PrnItem)};

@@ -867,6 +867,10 @@ __device__ __forceinline__ void probe(Ctx& x, int tag) {
 
 __device__ __forceinline__ bool wait_fwd(Ctx& x) {
   ++x.nbar;
+  if (x.a->fault_bar == (int)x.nbar && blockIdx.x == 0) {   // tests: a lost workgroup
+    if (threadIdx.x == 0) __hip_atomic_store(x.a->err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
   return grid_wait(x.a->bar, x.nbar * x.slices, x.a->err, x.m.flag);
 }
 // Backward: slice workgroup 0 republishes every completed barrier as a count in its own
@@ -1742,6 +1746,39 @@ static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS
                   wg_lds(16, 8, 1, 32) <= LDS_TOTAL,
               "weight-gradient LDS");
 
+static size_t prn_head_lds(int N, int kpad) {
+  return 1024 + 32 + (size_t)N * ((64 + kpad) * sizeof(bf16) + (kpad + 2) * sizeof(float)) +
+         8 * 64 * 16 * sizeof(float);
+}
+
+// workgroups of `kern` (PT threads, `lds` bytes) the device keeps resident at once
+template <typename K>
+static long resident_blocks(K kern, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, PT, lds) != hipSuccess) return -1;
+  return (long)per_cu * cu_count();
+}
+
+std::string prn_check(int N, int P, int P_fwd, int nblocks, int classes, int kpad) {
+  if (!prn_supported(N, P, nblocks, classes, kpad) || !prn_supported(N, P_fwd, nblocks, classes, kpad))
+    return "unsupported shape (slices 1/2/4, N x slices <= 256, 3n blocks, classes <= kpad <= 64)";
+  const int cus = cu_count();
+  if (N * P_fwd > cus) return "forward grid (N x slices) exceeds the CUs";
+  if (N * P + 1 > cus) return "backward grid (N x slices + weight-gradient workgroups) exceeds the CUs";
+  if (N > 240 || prn_head_lds(N, kpad) > LDS_TOTAL) return "head folds: batch too large for LDS";
+  // co-residency: every workgroup of a grid must be resident at once (grid barriers)
+  const long rf = P_fwd == 1 ? resident_blocks(prn_fwd_kernel<1>, LDS_TOTAL)
+                  : P_fwd == 2 ? resident_blocks(prn_fwd_kernel<2>, LDS_TOTAL)
+                               : resident_blocks(prn_fwd_kernel<4>, LDS_TOTAL);
+  const long rb = P == 1 ? resident_blocks(prn_bwd_kernel<1>, LDS_TOTAL)
+                  : P == 2 ? resident_blocks(prn_bwd_kernel<2>, LDS_TOTAL)
+                           : resident_blocks(prn_bwd_kernel<4>, LDS_TOTAL);
+  if (rf < 0 || rb < 0) return "occupancy query failed";
+  if (rf < (long)N * P_fwd) return "forward grid not co-resident (occupancy API)";
+  if (rb < (long)N * P + 1) return "backward grid not co-resident (occupancy API)";
+  return "";
+}
+
 void prn_forward(const PrnArgs& a, hipStream_t s) {
   if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad) || a.N * a.P > cu_count())
     throw std::invalid_argument("prn_forward: unsupported shape (N x P <= CUs, 3n blocks, <= 64 classes)");
@@ -1757,8 +1794,7 @@ void prn_head(const PrnArgs& a, hipStream_t s) {
   if (!prn_supported(a.N, a.P, a.nblocks, a.classes, a.kpad) || a.N > 240 || !a.dense_grad ||
       !a.loss_sum || !a.correct || !a.dbias)
     throw std::invalid_argument("prn_head: unsupported shape or missing outputs");
-  const size_t lds = 1024 + 32 + (size_t)a.N * ((64 + a.kpad) * sizeof(bf16) + (a.kpad + 2) * sizeof(float)) +
-                    8 * 64 * 16 * sizeof(float);
+  const size_t lds = prn_head_lds(a.N, a.kpad);
   if (lds > LDS_TOTAL) throw std::invalid_argument("prn_head: batch too large for LDS");
   hipLaunchKernelGGL(prn_head_kernel, dim3(1), dim3(PT), lds, s, a);
   DTR_CHECK_LAUNCH();

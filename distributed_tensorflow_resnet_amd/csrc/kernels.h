@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "tune.h"
 
 namespace dtr {
@@ -297,10 +299,16 @@ struct PrnArgs {
   float momentum, eps;
   int update_moving;
   long long* probe = nullptr;   // diagnostics: workgroup 0's (tag, wall clock) phase stamps
+  int fault_bar = -1;        // tests only (DTR_PRN_FAULT_BAR): forward workgroup 0 abandons the
+                             // launch at this barrier, as a lost workgroup would; -1 off
 };
 enum { PRN_THREADS = 512 };
 void prn_set_probe(long long* p);   // diagnostics (scripts/prn_probe.py); nullptr = off
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
+// Every host-side limit of the three persistent launches at once (forward at P_fwd slices,
+// backward at P, the head folds), including co-residency from the occupancy API: "" when
+// the step is supported, else the reason.  The engine calls it once when it builds the plan.
+std::string prn_check(int N, int P, int P_fwd, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
 int prn_acc_rep();   // fp64 accumulator replicas per BatchNorm of the persistent kernels
 void prn_forward(const PrnArgs& a, hipStream_t s);

@@ -15,6 +15,7 @@ import contextlib
 import datetime
 import faulthandler
 import os
+import socket
 import sys
 import threading
 import time
@@ -118,14 +119,47 @@ def engine_streams(device: torch.device):
     return _STREAMS[key]
 
 
-def gpu_shared_by_ranks() -> bool:
-    """Whether this node's ranks are folded onto fewer GPUs than ranks (the one-GPU
-    rehearsals).  Kernels that need every workgroup co-resident (the persistent CIFAR
-    step) must not run then: two processes' grids interleaved on one device could each
-    hold part of the CUs and wait for the rest forever."""
-    n = torch.cuda.device_count()
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    return n > 0 and local_world > n
+def device_identity(index: int) -> str:
+    """Physical identity of visible device `index` on this host: its PCI location, else
+    its UUID, else (neither exposed) the visible-device masks plus the ordinal -- so ranks
+    that each see one GPU through HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES (ordinal 0
+    everywhere) still differ."""
+    props = torch.cuda.get_device_properties(index)
+    pci = tuple(getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if all(v is not None for v in pci) and any(pci):
+        return "pci:%x:%x:%x" % pci
+    uid = str(getattr(props, "uuid", "") or "")
+    if uid.strip("0-") and uid.lower() not in ("none",):
+        return f"uuid:{uid}"
+    vis = "|".join(os.environ.get(k, "") for k in
+                   ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
+    return f"ord:{vis}|{index}"
+
+
+def ranks_on_device(store, rank: int, world: int, ident: str, tag: str = "dev") -> int:
+    """How many ranks of this job (this one included) run on the physical device `ident`
+    of this host: every rank publishes (hostname, identity) through the c10d store and
+    reads the others' (blocking until each rank has published -- every rank calls this
+    at the same point, the engine build)."""
+    mine = f"{socket.gethostname()}|{ident}"
+    store.set(f"dtr/{tag}/{rank}", mine)
+    return sum(1 for r in range(world)
+               if (mine if r == rank else bytes(store.get(f"dtr/{tag}/{r}")).decode()) == mine)
+
+
+def gpu_shared_by_ranks(ctx=None, device_index: int | None = None) -> bool:
+    """Whether another rank of this job runs on this rank's physical GPU (the one-GPU
+    rehearsals that fold ranks onto one device).  Kernels that need every workgroup
+    co-resident (the persistent CIFAR step) must not run then: two processes' grids
+    interleaved on one device could each hold part of the CUs and wait for the rest
+    forever.  Decided from the devices' physical identities (device_identity) exchanged
+    through the c10d store, not from rank / device counts: launchers that hand every
+    rank one GPU by visible-device masks see one device per process."""
+    if ctx is None or not getattr(ctx, "active", False) or torch.cuda.device_count() == 0:
+        return False
+    idx = torch.cuda.current_device() if device_index is None else device_index
+    store = dist.distributed_c10d._get_default_store()
+    return ranks_on_device(store, ctx.rank, ctx.world_size, device_identity(idx)) > 1
 
 
 class DistContext:

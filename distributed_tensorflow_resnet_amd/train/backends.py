@@ -67,7 +67,13 @@ class GPUBackend:
     def synchronize(self):
         torch.cuda.synchronize()
 
+    def check_health(self):
+        """Raise (engine.PersistentStepError) if a persistent launch failed: called before
+        every checkpoint save, so a half-computed step never reaches a checkpoint."""
+        self.engine.check_health()
+
     def state_tensors(self):
+        self.check_health()
         return state_to_tf(self.engine.params, self.engine.mom, self.global_step)
 
     def load_state(self, tensors):
@@ -170,6 +176,9 @@ class CPUBackend:
         return dict(self._last)
 
     def synchronize(self):
+        pass
+
+    def check_health(self):
         pass
 
     def state_tensors(self):

@@ -27,9 +27,13 @@ from ..utils.flags import build_parser, warn_unsupported
 from ..utils.records import EventWriter
 from . import hooks as H
 from .backends import make_backend
-from .engine import cifar_lr_schedule, imagenet_lr_schedule, scaled
+from .engine import PersistentStepError, cifar_lr_schedule, imagenet_lr_schedule, scaled
 from .evaluator import SidecarEvaluator, make_inference
 from .session import TrainingSession, run_training
+
+
+# written into --train_dir when a persistent CIFAR launch failed: restarts use the per-layer plan
+PERSIST_FAULT_MARKER = "persist_fault"
 
 
 class Prefetcher:
@@ -121,6 +125,13 @@ def main(argv=None, kind: str = "cifar") -> int:
         return 0
 
     # ---------------------------------------------------------------- train
+    # a previous attempt's persistent CIFAR step failed (a grid barrier timed out): this
+    # attempt runs the launch-per-layer plan (every rank reads the same marker, and the
+    # engine agrees the choice over c10d anyway)
+    if flags.train_dir and os.path.exists(os.path.join(flags.train_dir, PERSIST_FAULT_MARKER)):
+        os.environ["DTR_TUNE"] = ",".join(filter(None, [os.environ.get("DTR_TUNE", ""), "persist=0"]))
+        H.log(f"persistent step disabled: {PERSIST_FAULT_MARKER} in {flags.train_dir} "
+              "(a previous attempt's grid barrier timed out)")
     dev = None
     if device == "gpu":
         local = local_device_index()
@@ -188,7 +199,17 @@ def main(argv=None, kind: str = "cifar") -> int:
                            is_chief=is_chief, rank=rank, feeder=feeder)
     t0 = time.time()
     steps0 = sess.global_step
-    final = run_training(sess)
+    try:
+        final = run_training(sess)
+    except PersistentStepError as e:
+        # fail the job, not the model: no checkpoint of this state is written (the session
+        # skips the hooks' end() on an exception); the launcher (--max_restarts) restarts
+        # from the last good checkpoint and the marker puts the restart on the per-layer plan
+        H.log(f"FATAL: {e}; exiting with code {H.StepWatchdogHook.EXIT_CODE} for a restart")
+        if flags.train_dir and is_chief:
+            with open(os.path.join(flags.train_dir, PERSIST_FAULT_MARKER), "w") as fh:
+                fh.write(f"{e}\n")
+        return H.StepWatchdogHook.EXIT_CODE
     dt = time.time() - t0
     if is_chief:
         H.log(f"training done: global_step={final}, {final - steps0} steps in {dt:.1f}s")

@@ -68,6 +68,13 @@ OPTW_DTYPE = np.dtype([   # csrc/optim.h OptWork
 OPT_TILE_LOADS = 2048   # a sgd_tiles workgroup's slab loads: <= 8 16-byte loads per thread
 
 
+class PersistentStepError(RuntimeError):
+    """A persistent CIFAR launch's grid barrier timed out (csrc/cifar_persist.hip: every
+    wait is bounded, a timed-out workgroup sets the error flag and exits).  The step's
+    results are invalid; the driver exits with code 3 so parallel/launch.py restarts the
+    job from the last good checkpoint, on the per-layer plan."""
+
+
 def _pow2ceil(x: int) -> int:
     return 1 << max(0, (int(x) - 1).bit_length())
 
@@ -302,9 +309,21 @@ class Engine:
         self.persist_slices = tune.get("persist_slices")
         self.opt_fused = bool(tune.get("opt_fused"))
         self.opt_fused_layer = bool(tune.get("opt_fused_layer"))
-        # (never on a GPU shared by several ranks: its grids need every CU to themselves)
-        ok = pm != 0 and not gpu_shared_by_ranks() and _persist.supported(self)
-        self.persist = ok and (pm == 1 or self.N <= _persist.AUTO_MAX_BATCH)
+        # why the persistent step is off ("" = on); never on a GPU shared by several ranks
+        # (its grids need every CU to themselves), and the same choice on EVERY rank (the
+        # two plans issue different collectives)
+        if pm == 0:
+            reason = "tune persist=0"
+        elif pm != 1 and self.N > _persist.AUTO_MAX_BATCH:
+            reason = f"per-rank batch {self.N} > {_persist.AUTO_MAX_BATCH} (auto)"
+        elif gpu_shared_by_ranks(self.dist, didx):
+            reason = "GPU shared by several ranks"
+        else:
+            reason = _persist.check(self)
+        if self.dist is not None and self.dist.active and not self.dist._agree(reason == ""):
+            reason = reason or "another rank cannot run the persistent step"
+        self.persist_reason = reason
+        self.persist = reason == ""
         self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
@@ -1459,8 +1478,28 @@ class Engine:
             self._run("gsum", st)
 
     def persist_error(self) -> bool:
-        """Whether a persistent launch's barrier wait ever timed out (diagnostics)."""
+        """Whether a persistent launch's barrier wait ever timed out (synchronises)."""
         return self.prn is not None and bool(self.prn.err.item())
+
+    def check_health(self, err_word: float | None = None):
+        """Raise PersistentStepError when a persistent launch's grid barrier timed out:
+        its workgroups exited early, so that step's gradient, weights and BN statistics
+        are garbage and must neither reach a checkpoint nor keep training.  `err_word`:
+        the flag slot (scalars[4]) if the caller has read the scalars already."""
+        if self.prn is None:
+            return
+        if err_word is None:
+            bad = bool(self.prn.err.item())
+        else:
+            bad = err_word != 0.0
+        if bad:
+            raise PersistentStepError(
+                "a persistent-step grid barrier timed out (workgroups not co-resident or lost); "
+                f"the step's results are invalid (err={int(self.prn.err.item())})")
+
+    def clear_persist_error(self):
+        if self.prn is not None:
+            self.prn.err.zero_()
 
     # ------------------------------------------------------------------ running
     def repack(self):
@@ -1666,6 +1705,7 @@ class Engine:
             self._run("cost", torch.cuda.current_stream().cuda_stream)
             self._cost_at = self._steps_run
         v = self.scalars.detach().cpu().tolist()
+        self.check_health(v[4])
         loss_sum, correct, lr, l2 = v[0], v[1], v[2], v[3]
         if reduce and self.dist is not None and self.world > 1:
             t = torch.tensor([loss_sum, correct], device=self.device)

@@ -11,8 +11,13 @@ publishes anyway), grid barriers only where BatchNorm needs batch statistics (ex
 atomic sums), and the CUs beyond the slices compute the weight gradients (fp32 slabs per
 image group) while the backward's dgrad chain continues.  The step is then:
 
-    [augment] -> prn forward -> (side: softmax-xent batch folds, dense wgrad)
-              -> prn backward -> grouped slab reduces (+ bucket all-reduces) -> optimizer
+    [augment] -> prn forward -> prn backward -> prn head folds (loss, precision, dense
+              gradients: one workgroup) -> one GPU: sgd_tiles (the weight-gradient slab
+              sums + SGD-momentum + both bf16 weight copies, ONE launch)
+                                         | world > 1: grouped slab reduce -> all-reduce
+                                           of the whole gradient -> optimizer
+
+all on the main stream (5 launches on one GPU).
 
 Selected by the engine (tune ``persist``: -1 auto = per-rank batch <= AUTO_MAX_BATCH on a supported
 CIFAR spec, 0 off, 1 on when supported).
@@ -20,6 +25,7 @@ CIFAR spec, 0 off, 1 on when supported).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -66,31 +72,42 @@ def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:
     return 2 if 8 * N <= 3 * cus else 1
 
 
-def supported(eng) -> bool:
-    """Whether the persistent kernels cover this engine's network and batch."""
+def check(eng) -> str:
+    """'' when the persistent kernels cover this engine's network, batch and device, else
+    the reason they do not: the network shape here, every host-side limit of the three
+    launches (slices, grids within the CUs, the head folds' LDS) and the co-residency of
+    both grids by the occupancy API in one native predicate (prn_check)."""
     spec, nat = eng.spec, eng.nat
     if not spec.dataset.startswith("cifar") or spec.maxpool or eng.stem_s2d:
-        return False
+        return "not a CIFAR network"
     if spec.image_h != 32 or spec.image_w != 32 or spec.dense_in != 64:
-        return False
+        return "not a 32x32 CIFAR ResNet v2"
     st = spec.stem
     if (st.kh, st.kw, st.stride, st.cout) != (3, 3, 1, 16) or st.cin > 8:
-        return False
+        return "stem is not 3x3/1 -> 16"
     nb = len(spec.blocks)
     if nb % 3 or any(b.kind != "building" for b in spec.blocks):
-        return False
+        return "not 3 stages of building blocks"
     n = nb // 3
     for i, b in enumerate(spec.blocks):
         stage = i // n
         if b.cout != 16 << stage or b.ho != 32 >> stage:
-            return False
+            return "stage widths are not 16/32/64"
         first = i % n == 0
         if (b.proj is not None) != first or b.stride != (2 if first and stage else 1):
-            return False
+            return "projection / stride layout is not the CIFAR v2 one"
     cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
     P = slices_for(eng.N, cus, eng.persist_slices)
     # (at least 16 CUs left for the weight-gradient workgroups)
-    return eng.N * P + 16 <= cus and bool(nat.prn_supported(eng.N, P, nb, spec.num_classes, eng.kpad))
+    if eng.N * P + 16 > cus:
+        return f"{eng.N} x {P} slices leave fewer than 16 CUs for the weight gradients"
+    return str(nat.prn_check(eng.N, P, fwd_slices_for(eng.N, cus, eng.persist_slices), nb,
+                             spec.num_classes, eng.kpad))
+
+
+def supported(eng) -> bool:
+    """Whether the persistent kernels cover this engine's network and batch."""
+    return check(eng) == ""
 
 
 def _stage(b) -> int:
@@ -122,7 +139,11 @@ class PersistStep:
         self.cus = torch.cuda.get_device_properties(dev).multi_processor_count
         self.P = slices_for(N, self.cus, eng.persist_slices)          # backward
         self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
-        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # barrier-timeout flag: slot 4 of the engine's scalars, so the host read of the
+        # logged metrics (Engine.metrics) sees it at no extra cost; never cleared by the
+        # kernels (Engine.clear_persist_error)
+        self.err = eng.scalars[4:5].view(torch.int32)
+        self.fault_bar = int(os.environ.get("DTR_PRN_FAULT_BAR", "-1"))
         self.dpool = torch.zeros((N, 64), device=dev)
         self.dx0 = torch.empty_like(eng.X[0])
         # per-block backward gradients published to the weight-gradient workgroups
@@ -238,6 +259,6 @@ class PersistStep:
         ptrs += [0, 0, 0, 0] if fwd else [sp, sp + 4, eng.dense_bias_grad, eng.dense_grad]
         ints = [self.nblocks, len(self.items), eng.N, self.P_fwd if fwd else self.P,
                 spec.num_classes, eng.kpad, 1,
-                self.wgrad_wgs]
+                self.wgrad_wgs, self.fault_bar if fwd else -1]
         floats = [1.0 / eng.global_batch, bn_decay, bn_eps]
         return ptrs, ints, floats

@@ -55,3 +55,30 @@ def test_imagenet_driver_gpu_synthetic(gpu, tmp_path):
              "--batch_size", "32", "--train_steps", "6", "--log_every", "3"])
     assert r.returncode == 0, r.stderr[-4000:]
     assert "training precision" in r.stdout
+
+
+def test_persistent_fault_fails_job_and_restart_falls_back(gpu, tmp_path):
+    """A persistent CIFAR launch whose grid barrier times out must fail the job, not the
+    model: DTR_PRN_FAULT_BAR makes forward workgroup 0 abandon the
+    launch at its 3rd barrier (a lost workgroup; the others time out at the next one).
+    The first metrics read raises, the CLI exits 3 WITHOUT writing a checkpoint of the
+    broken step and leaves the fault marker; the launcher's restart resumes from the
+    last good checkpoint on the per-layer plan and finishes."""
+    td = str(tmp_path / "train")
+    common = ["--device", "gpu", "--synthetic", "--resnet_size", "8", "--batch_size", "16",
+              "--train_dir", td, "--log_every", "1", "--save_checkpoint_steps", "1"]
+    r = run(["resnet_cifar_main.py", "--train_steps", "2"] + common)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-2")
+    r = run(["-m", "distributed_tensorflow_resnet_amd.parallel.launch", "--nproc", "1",
+             "--max_restarts", "1", "--master_port", "29634", "resnet_cifar_main.py",
+             "--train_steps", "4"] + common, env={"DTR_PRN_FAULT_BAR": "3"})
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "grid barrier timed out" in out and "exiting with code 3" in out, out[-4000:]
+    assert "[launch] a rank failed with exit code 3" in out
+    assert "persistent step disabled" in out
+    assert os.path.exists(os.path.join(td, "persist_fault"))
+    # the broken step 3 never reached a checkpoint: both attempts resumed from step 2
+    assert out.count("(global_step=2)") == 2, out[-4000:]
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-4")

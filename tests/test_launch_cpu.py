@@ -59,25 +59,43 @@ def test_start_and_stop_background_run(tmp_path):
 
 
 def test_gpu_shared_by_ranks(monkeypatch):
-    """Ranks folded onto fewer GPUs than ranks (one-GPU rehearsals) must switch the
-    persistent CIFAR step off: its grids need every CU of the device to themselves."""
+    """Ranks on one physical GPU (one-GPU rehearsals) must switch the persistent CIFAR
+    step off -- its grids need every CU of the device to themselves -- and ranks that
+    each see one GPU through a visible-device mask (ordinal 0 everywhere) must not be
+    mistaken for sharing: the decision comes from physical device identities
+    exchanged through the c10d store."""
+    import types
+
     import torch
+    import torch.distributed as dist
 
-    from distributed_tensorflow_resnet_amd.parallel.dist import gpu_shared_by_ranks
+    from distributed_tensorflow_resnet_amd.parallel import dist as D
 
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
-    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
-    assert gpu_shared_by_ranks()
-    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
-    assert not gpu_shared_by_ranks()
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
-    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
-    assert not gpu_shared_by_ranks()
-    monkeypatch.delenv("LOCAL_WORLD_SIZE")
-    monkeypatch.setenv("WORLD_SIZE", "16")
-    assert gpu_shared_by_ranks()
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
-    assert not gpu_shared_by_ranks()
+    # identities: PCI location first, then the UUID, then the visible masks + ordinal
+    props = types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x15, pci_device_id=0, uuid="abc")
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    assert D.device_identity(0) == "pci:0:15:0"
+    props = types.SimpleNamespace(uuid="GPU-1234")
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    assert D.device_identity(0) == "uuid:GPU-1234"
+    props = types.SimpleNamespace(uuid="00000000-0000-0000-0000-000000000000")
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
+    a = D.device_identity(0)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    assert D.device_identity(0) != a          # one GPU per rank by mask: distinct
+
+    # counting over a store: ranks 0 and 1 share GPU "x", rank 2 has "y"
+    store = dist.HashStore()
+    store.set("dtr/t/1", f"{D.socket.gethostname()}|x")
+    store.set("dtr/t/2", f"{D.socket.gethostname()}|y")
+    assert D.ranks_on_device(store, 0, 3, "x", tag="t") == 2
+    store = dist.HashStore()
+    store.set("dtr/u/0", f"{D.socket.gethostname()}|x")
+    store.set("dtr/u/1", "otherhost|y")
+    assert D.ranks_on_device(store, 2, 3, "y", tag="u") == 1   # same id on another host
+    # no process group: never shared
+    assert not D.gpu_shared_by_ranks(None)
 
 
 def test_persistent_slice_selection():
