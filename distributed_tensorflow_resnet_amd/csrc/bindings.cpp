@@ -1283,6 +1283,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_fin_version", &set_fin_version,
         "BN finalize kernel variant: 0 = LDS tree, 2 = per-channel one-round, 1 = auto (default)");
   m.def("bn_acc_rep", []() { return BN_ACC_REP; }, "fp64 accumulator replicas per BatchNorm");
+  m.def("prn_bar_words", &prn_bar_words, "32-bit words of the persistent step's barrier region (128-B aligned)");
   m.def("prn_acc_rep", &prn_acc_rep, "fp64 accumulator replicas per BatchNorm (persistent kernels)");
   m.def("pfin_cap", &pfin_cap, "max partials a consumer prologue combines for C channels");
   m.def("bn_bwd_tiles", &bn_bwd_tiles);

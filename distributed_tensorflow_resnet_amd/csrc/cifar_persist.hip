@@ -207,24 +207,64 @@ __device__ __forceinline__ int opaque_s(int v) {
 }
 
 // ---- grid barrier ---------------------------------------------------------------------
-// Every wave drains its stores / atomics, then lane 0 arrives.  The caller issues its
-// prefetches (waves 1-7) and waits (grid_wait).
-__device__ __forceinline__ void grid_arrive(unsigned* bar) {
+// Arrival counters sharded over PRN_SHARDS cache lines: workgroup b adds to line b % 8 (one
+// XCD per line under round-robin placement), and the waiters poll all 8 lines with ONE
+// 8-lane load.  One shared counter serialises its arrivals at the memory side (~12 ns
+// each) and its pollers contend with them: microbench/bn_barrier.hip, profiles/bn_barrier.md
+// -- a BN barrier (sums, drain, arrive, wait, sums read) at 128 workgroups 3.94 -> 2.72 us,
+// at 256 8.85 -> 4.86 us, at 64 2.31 -> 2.07 us.
+constexpr int PRN_SHARDS = 8, PRN_LINE = 32;   // 32 words = one 128-B line per shard
+// bar layout (words): forward shards at PRN_FWD + 32 s, backward shards at PRN_BWD + 32 s,
+// the backward readiness count at PRN_READY, the weight-gradient item queue at PRN_QUEUE
+// (each on its own line; PRN_BAR_WORDS in all, zeroed every step)
+constexpr int PRN_FWD = 0, PRN_BWD = PRN_SHARDS * PRN_LINE, PRN_READY = 2 * PRN_SHARDS * PRN_LINE,
+              PRN_QUEUE = PRN_READY + PRN_LINE, PRN_BAR_WORDS = PRN_QUEUE + PRN_LINE;
+
+// Every wave drains its stores / atomics, then lane 0 arrives on its shard.  The caller
+// issues its prefetches (waves 1-7) and waits (grid_wait).
+__device__ __forceinline__ void grid_arrive(unsigned* bar, int shards) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(bar + (blockIdx.x % shards) * PRN_LINE, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wait until `target` arrivals; lane 0 of wave 0 polls every SLEEP x 64 clocks (the
-// weight-gradient workgroups poll 8x less often: ~190 of them on one counter line slow
-// the slices' arrives).  Returns false when the wait timed out (*err set): the caller
-// exits.
-template <int SLEEP = 1>
-__device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* err, int* flag) {
+// Wait until barrier k (1-based) of `nsl` arriving workgroups is complete: shard s holds
+// k x (the arrivers b < nsl with b % 8 == s).  Lanes 0-7 of wave 0 poll their shard every
+// 64 clocks.  Returns false when the wait timed out (*err set): the caller exits.
+__device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned k, unsigned nsl, int shards,
+                                          int* err, int* flag) {
+  if ((int)threadIdx.x < shards) {
+    const unsigned sh = threadIdx.x;
+    const unsigned target = k * ((nsl + shards - 1 - sh) / shards);
+    const unsigned* p = bar + sh * PRN_LINE;
+    const long long t0 = wall_clock64();
+    int ok = 1;
+    for (;;) {
+      const bool done = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (__builtin_amdgcn_ballot_w64(!done) == 0) break;   // every shard complete
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > kSpinTicks) {
+        if (sh == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    if (sh == 0) *flag = ok;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*flag) != 0;   // uniform: no divergent region after
+}
+
+// Wait until the single counter `ctr` reaches `target` (the weight-gradient workgroups on
+// the readiness line; they poll 8x less often: ~190 pollers on one line slow its writer).
+template <int SLEEP = 8>
+__device__ __forceinline__ bool count_wait(unsigned* ctr, unsigned target, int* err, int* flag) {
   if (threadIdx.x == 0) {
     const long long t0 = wall_clock64();
     int ok = 1;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(SLEEP);
       if (wall_clock64() - t0 > kSpinTicks) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -235,7 +275,7 @@ __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned target, int* e
     *flag = ok;
   }
   __syncthreads();
-  return __builtin_amdgcn_readfirstlane(*flag) != 0;   // uniform: no divergent region after
+  return __builtin_amdgcn_readfirstlane(*flag) != 0;
 }
 
 // ---- weights: global -> registers (waves 1-7) -> LDS -----------------------------------
@@ -871,16 +911,14 @@ __device__ __forceinline__ bool wait_fwd(Ctx& x) {
     if (threadIdx.x == 0) __hip_atomic_store(x.a->err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
   }
-  return grid_wait(x.a->bar, x.nbar * x.slices, x.a->err, x.m.flag);
+  return grid_wait(x.a->bar + PRN_FWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
 }
-// Backward: slice workgroup 0 republishes every completed barrier as a count in its own
-// cache line (bar + PRN_READY, 256 B away): the ~190 weight-gradient workgroups poll that
-// line instead of the arrival counter the slices' atomics go to.
-constexpr int PRN_READY = 64;
-constexpr int PRN_QUEUE = 96;   // the weight-gradient item queue (its own 128-B line)
+// Backward: slice workgroup 0 republishes every completed barrier as a count on its own
+// line (bar + PRN_READY): the ~190 weight-gradient workgroups poll that line instead of
+// the arrival shards the slices' atomics go to.
 __device__ __forceinline__ bool wait_bwd(Ctx& x) {
   ++x.nbar;
-  const bool ok = grid_wait(x.a->bar + 1, x.nbar * x.slices, x.a->err, x.m.flag);
+  const bool ok = grid_wait(x.a->bar + PRN_BWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
   if (ok && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(x.a->bar + PRN_READY, x.nbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ok;
@@ -960,7 +998,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   if constexpr (P > 1) publish<S, P, 1>(hr, B.h1 + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, hr, B.bn2, wave, lane);
   probe(x, 4);
-  grid_arrive(a.bar);
+  grid_arrive(a.bar + PRN_FWD, a.shards);
   publish<S, P, P == 1 ? 0 : 2>(hr, B.h1 + img_o, x.kslice, wave, lane);
   probe(x, 5);
   {
@@ -984,7 +1022,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   if constexpr (P > 1) publish<S, P, 1>(xr, B.out + img_o, x.kslice, wave, lane);
   fwd_sums<S, P>(x, xr, bi_next, wave, lane);
   probe(x, 10);
-  grid_arrive(a.bar);
+  grid_arrive(a.bar + PRN_FWD, a.shards);
   publish<S, P, P == 1 ? 0 : 2>(xr, B.out + img_o, x.kslice, wave, lane);
   probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
@@ -1044,7 +1082,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     round_acc<0, P, false>(xr, acc, xr);
     if constexpr (P > 1) publish<0, P, 1>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
-    grid_arrive(a.bar);
+    grid_arrive(a.bar + PRN_FWD, a.shards);
     publish<0, P, P == 1 ? 0 : 2>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
     WLoad LP{};
@@ -1138,7 +1176,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
       atomic_add_g(a.pool_acc + (long)x.img * 64 + tid, (double)v);
     }
   }
-  grid_arrive(a.bar);
+  grid_arrive(a.bar + PRN_FWD, a.shards);
   if (!wait_fwd(x)) return;
   if (x.kslice != 0) return;
   float* pool_s = x.m.tbl2;          // [0, 64) pooled, [64, 128) dp, [128, 192) g
@@ -1319,7 +1357,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     publish<S, P, 1>(da, B.da2 + img_o, x.kslice, wave, lane);
   bwd_sums<S, P>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
   probe(x, 4);
-  grid_arrive(a.bar + 1);
+  grid_arrive(a.bar + PRN_BWD, a.shards);
   // dout for the conv2 / projection weight gradients and the neighbours' residual rows:
   // stored after this arrive (its drain overlaps the wait), drained by the next one
   publish<S, P>(dout, B.dout + img_o, x.kslice, wave, lane);
@@ -1362,7 +1400,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     publish<SI, P, 1>(da, B.da1 + img_i, x.kslice, wave, lane);
   bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
-  grid_arrive(a.bar + 1);
+  grid_arrive(a.bar + PRN_BWD, a.shards);
   // dh1 for the conv1 weight gradient, from its halo (HA, intact until the next block
   // stages its own): stored after this arrive, drained by the next one
   halo_to_global<S, P>(x.m.ha, B.dh1 + img_o, x.kslice);
@@ -1563,7 +1601,7 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
       for (int r = 0; r < 4; ++r) dp[t][r] = (bf16)dps[(cb * 16 + 4 * (lane >> 4) + r) & 63];
     }
     bwd_sums<2, P>(x, dp, xs, x.m.tbl, fb, wave, lane);
-    grid_arrive(a.bar + 1);
+    grid_arrive(a.bar + PRN_BWD, a.shards);
     bn_prefetch_bwd(ld_const(a.bns + (fb)), 64, x.bnr);
     bn_prefetch_tab(ld_const(a.bns + (BL.bn2)), 64, x.ftr);
     if (!wait_bwd(x)) return false;
@@ -1598,7 +1636,7 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
   probe(x, 200);
   // ---- the stem output's gradient: published for the stem's weight gradient ----
   publish<0, P>(dout, a.dx0 + (long)x.img * 1024 * 16, x.kslice, wave, lane);
-  grid_arrive(a.bar + 1);
+  grid_arrive(a.bar + PRN_BWD, a.shards);
   if (blockIdx.x == 0) wait_bwd(x);   // publishes the stem item's readiness
   return true;
 }
@@ -1711,7 +1749,7 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     const int i = __builtin_amdgcn_readfirstlane(*slot);
     if (i >= a.nitems) return;
     const PrnItem& it = ld_const(a.items + i);
-    if (!grid_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
+    if (!count_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
     run_item(it, smem, wave, lane);
   }
 }
@@ -1726,6 +1764,7 @@ static long long* g_prn_probe = nullptr;
 void prn_set_probe(long long* p) { g_prn_probe = p; }
 
 size_t prn_lds_bytes() { return LDS_TOTAL; }
+int prn_bar_words() { return PRN_BAR_WORDS; }
 int prn_acc_rep() { return PRN_ACC_REP; }
 
 bool prn_supported(int N, int P, int nblocks, int classes, int kpad) {
@@ -1745,6 +1784,8 @@ int prn_item_kind(int cin, int cout, int ksize, int stride) {
 static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS_TOTAL &&
                   wg_lds(16, 8, 1, 32) <= LDS_TOTAL,
               "weight-gradient LDS");
+
+static int prn_shards() { return tune(T_PRN_SHARDS) == 1 ? 1 : PRN_SHARDS; }
 
 static size_t prn_head_lds(int N, int kpad) {
   return 1024 + 32 + (size_t)N * ((64 + kpad) * sizeof(bf16) + (kpad + 2) * sizeof(float)) +
@@ -1784,6 +1825,7 @@ void prn_forward(const PrnArgs& a, hipStream_t s) {
     throw std::invalid_argument("prn_forward: unsupported shape (N x P <= CUs, 3n blocks, <= 64 classes)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
+  b.shards = prn_shards();
   if (a.P == 1) hipLaunchKernelGGL(prn_fwd_kernel<1>, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
   else if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_fwd_kernel<4>, dim3(a.N * 4), dim3(PT), LDS_TOTAL, s, b);
@@ -1808,6 +1850,7 @@ void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
     throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
+  b.shards = prn_shards();
   if (a.P == 1) hipLaunchKernelGGL(prn_bwd_kernel<1>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   else if (a.P == 2) hipLaunchKernelGGL(prn_bwd_kernel<2>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_bwd_kernel<4>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);

@@ -275,9 +275,10 @@ struct PrnArgs {
   const bf16* x_in;          // [N][32][32][8] input images (channels 3..7 zero)
   const bf16* stem_w;        // OHWI [16][3][3][8]
   double* pool_acc;          // [N][64] fp64 average-pool sums (zeroed every step)
-  unsigned* bar;             // [128]: barrier counters (forward, backward) at 0, 1; the backward
-                             // readiness count at 64, the weight-gradient item queue at 96 --
-                             // zeroed every step
+  unsigned* bar;             // [prn_bar_words()], 128-B aligned: sharded arrival counters
+                             // (forward, backward), the backward readiness count and the
+                             // weight-gradient item queue, each on its own lines -- zeroed
+                             // every step (cifar_persist.hip PRN_FWD .. PRN_QUEUE)
   int* err;                  // set when a barrier wait times out
   const bf16* dense_w;       // [64][kpad] bf16 HWIO
   const float* dense_b;
@@ -299,6 +300,7 @@ struct PrnArgs {
   float momentum, eps;
   int update_moving;
   long long* probe = nullptr;   // diagnostics: workgroup 0's (tag, wall clock) phase stamps
+  int shards = 8;            // arrival-counter shards (tune prn_shards: 1 or 8)
   int fault_bar = -1;        // tests only (DTR_PRN_FAULT_BAR): forward workgroup 0 abandons the
                              // launch at this barrier, as a lost workgroup would; -1 off
 };
@@ -310,6 +312,7 @@ bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
 // the step is supported, else the reason.  The engine calls it once when it builds the plan.
 std::string prn_check(int N, int P, int P_fwd, int nblocks, int classes, int kpad);
 size_t prn_lds_bytes();
+int prn_bar_words();   // barrier / readiness / queue words of PrnArgs::bar (zeroed every step)
 int prn_acc_rep();   // fp64 accumulator replicas per BatchNorm of the persistent kernels
 void prn_forward(const PrnArgs& a, hipStream_t s);
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);

@@ -81,6 +81,9 @@ const TuneEntry kTable[T_COUNT] = {
      "off: 0.88-1.0 us per K tile (2x the MFMA bound) plus ~11 us of exposed prologue, first "
      "DMA and epilogue per workgroup -- 478-621 TF/s vs the 4-wave ring's 558-679 "
      "(profiles/imagenet_ring8.md)"},
+    {"prn_shards", 8,
+     "arrival-counter shards (one 128-B line each, workgroup b on b % shards) of the persistent "
+     "CIFAR step's grid barriers: 8 or 1 (profiles/bn_barrier.md)"},
 };
 
 std::atomic<long> g_val[T_COUNT];

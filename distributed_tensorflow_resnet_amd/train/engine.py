@@ -544,13 +544,14 @@ class Engine:
         # replica counts; a kernel uses the first replicas of the block)
         rep = max(self.nat.bn_acc_rep(), self.nat.prn_acc_rep())
         tot = sum(4 * rep * b.spec.channels for b in self.bns.values())
-        # (+ N x 64 doubles and 64 more: the persistent step's average-pool sums and its
-        # barrier counters / readiness line, zeroed with the accumulators at the start of
-        # every step -- train/persist.py)
+        # (+ N x 64 doubles and the barrier region: the persistent step's average-pool sums
+        # and its sharded barrier counters / readiness line / item queue (128-B aligned lines),
+        # zeroed with the accumulators at the start of every step -- train/persist.py)
         base = max(_ceil(tot, 2) * 2, 2)
-        self.bn_acc = torch.zeros(base + 64 * N + 64, dtype=torch.float64, device=dev)
+        bar_d = _ceil(self.nat.prn_bar_words(), 2) + 16   # + up to 128 B of alignment
+        self.bn_acc = torch.zeros(base + 64 * N + bar_d, dtype=torch.float64, device=dev)
         self.prn_pool = self.bn_acc.data_ptr() + 8 * base
-        self.prn_bar = self.bn_acc.data_ptr() + 8 * (base + 64 * N)
+        self.prn_bar = _ceil(self.bn_acc.data_ptr() + 8 * (base + 64 * N), 128) * 128
         off = 0
         for b in self.bns.values():
             n = 2 * rep * b.spec.channels
