@@ -33,6 +33,11 @@ COMMON_FLAGS = [
 ]
 
 
+# per-file extra flags (none at present; e.g. ["-mllvm", "-amdgpu-mfma-vgpr-form=1"] keeps
+# a one-wave-per-SIMD kernel's MFMA accumulators in arch VGPRs, profiles/imagenet_wide.md)
+FILE_FLAGS: dict = {}
+
+
 def _sources():
     """Device code (*.hip), host-only C++ (*.cpp except the bindings), bindings."""
     hips = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
@@ -78,6 +83,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     objs = []
     for src in hips + [binding]:
         flags = bind_flags if src == binding else COMMON_FLAGS
+        flags = flags + FILE_FLAGS.get(os.path.basename(src), [])
         digest = _file_digest(src, hdr + " ".join(flags))
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         stamp = obj + ".sha1"

@@ -1243,18 +1243,6 @@ PYBIND11_MODULE(_C, m) {
     g.Kdim = c.kh * c.kw * (mode == MODE_FWD ? c.C : c.K);
     return conv_gemm_uses_ring(g, mode);
   }, "whether conv_gemm(mode, geom) (no BN+ReLU prologue) runs the LDS-DMA ring loop");
-  m.def("conv_ring8_covers", [](int mode, std::vector<int> geom) {
-    GemmArgs g{};
-    g.g = geom_from(geom);
-    const ConvGeom& c = g.g;
-    g.M = mode == MODE_FWD ? c.N * c.Ho * c.Wo : c.N * c.H * c.W;
-    g.Ncol = mode == MODE_FWD ? c.K : c.C;
-    g.Kdim = c.kh * c.kw * (mode == MODE_FWD ? c.C : c.K);
-    return conv_gemm_uses_ring8(g, mode);
-  }, "whether conv_gemm(mode, geom) (no prologue, accumulator-mode BN sums) runs the 8-wave "
-     "256x128 ring (conv_ring8.hip)");
-  m.def("set_ring8_probe", [](ptr_t p) { set_ring8_probe(P<long long>(p)); },
-        "diagnostics: conv_ring8 workgroup 0 writes its timeline (53 wall-clock stamps) to p");
   m.def("set_direct_probe", [](ptr_t p) { set_direct_probe(P<long long>(p)); },
         "diagnostics: direct-conv workgroups write 4 wall-clock stamps each to p (0 = off)");
   m.def("set_wgrad_direct", &set_wgrad_direct,

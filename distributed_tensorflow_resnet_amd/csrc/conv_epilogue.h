@@ -8,9 +8,8 @@ namespace dtr {
 
 enum { F_PRE = 1, F_STATS = 2, F_BNB = 4, F_ABWD = 8 };
 
-// The epilogue's thread index: 256 threads per tile.  The 512-thread 8-wave ring kernel
-// (conv_ring8.hip) runs two epilogues side by side, one per 128-row half of its
-// 256-row tile (waves 0-3 and 4-7, the same barriers in lockstep), each on its own LDS.
+// The epilogue's thread index: 256 threads per tile (a 512-thread kernel may run two
+// epilogues side by side, one per half of its tile, each on its own LDS, with SYNC_ALL).
 __device__ __forceinline__ int ep_tid() { return (int)(threadIdx.x & 255); }
 
 // Epilogue staging: PR rows of the fp32 tile at a time -- the whole tile when
@@ -321,7 +320,7 @@ __device__ __forceinline__ bool splitk_combine(const GemmArgs& args, f32x4 (&acc
 // row stores with bias / residual / accumulate, BN statistics (STATS), BN
 // backward sums (BNB) and the optional last-arriver finalize.  Entered after a
 // workgroup barrier (the caller's LDS is dead).
-// SYNC_ALL (the two side-by-side epilogues of conv_ring8.hip): every phase runs, rows
+// SYNC_ALL (two side-by-side epilogues of a 512-thread kernel): every phase runs, rows
 // past M included (as no-ops), so both halves pass the same barriers; the caller then
 // uses accumulator-mode BN statistics / sums only (no per-tile partial rows, no
 // last-arriver finalize).

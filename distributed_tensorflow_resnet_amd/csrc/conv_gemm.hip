@@ -668,40 +668,6 @@ static void launch_nbuf(const GemmArgs& a0, hipStream_t s) {
     if constexpr (BN >= 64) {
       const bool ring = BM == 128 && (BN == 128 || (BN == 64 && WM == 4)) && (FLAGS & F_PRE) == 0 &&
                         conv_ring_covers(a, MODE);
-      if constexpr (BN == 128) {
-        if (ring && conv_ring8_covers(a, MODE)) {   // deep K: 8-wave 256 x 128 ring
-          dim3 g8((a.M + 255) / 256, (a.Ncol + 127) / 128, a.par ? 4 : 1);
-          const long tiles8 = (long)g8.x * g8.y;
-          // one workgroup per CU: split only while the slices still fit in one round of
-          // the CUs (the 14x14 grid's 196 tiles run unsplit; 2 slices would be 392
-          // workgroups, a second round 53 % full)
-          int S = 1;
-          const int kt8 = (a.Kdim + 63) / 64;
-          while (!a.par && S * 2 <= tune(T_SPLITK) && tiles8 * S * 2 <= cu_count() &&
-                 kt8 / (S * 2) >= 8)
-            S *= 2;
-          const size_t need = (size_t)S * tiles8 * 256 * 128 * sizeof(float);
-          if (g_sk_query) {
-            if (S > 1) {
-              g_sk_query->bytes = need;
-              g_sk_query->tiles = (size_t)tiles8;
-            }
-            return;
-          }
-          float* part = a.sk_part;
-          unsigned* cnt = a.sk_cnt;
-          const bool ok = part != nullptr ? true
-                                           : splitk_workspace(need, (size_t)tiles8, s, &part, &cnt);
-          if (S > 1 && ok) {
-            a.ksplit = S;
-            a.sk_part = part;
-            a.sk_cnt = cnt;
-            g8.z = S;
-          }
-          conv_ring8(a, MODE, FLAGS, g8, s);
-          return;
-        }
-      }
       if (ring || conv_gemm_fast(a, MODE)) {
         const long tiles = (long)grid.x * grid.y;
         const int S = a.par ? 1 : pick_ksplit(tiles, (a.Kdim + 63) / 64);
@@ -830,18 +796,6 @@ bool conv_gemm_uses_ring(const GemmArgs& a0, int mode) {
     a.Kdim = ((g.kh + 1) >> 1) * ((g.kw + 1) >> 1) * g.K;
   }
   return conv_ring_covers(a, mode);
-}
-
-bool conv_gemm_uses_ring8(const GemmArgs& a0, int mode) {
-  if (conv_direct_covers(a0, mode)) return false;
-  GemmArgs a = a0;
-  if (mode == MODE_DGRAD && parity_dgrad(a)) {
-    const ConvGeom& g = a.g;
-    a.par = 1;
-    a.M = g.N * ((g.H + 1) >> 1) * ((g.W + 1) >> 1);
-    a.Kdim = ((g.kh + 1) >> 1) * ((g.kw + 1) >> 1) * g.K;
-  }
-  return conv_ring8_covers(a, mode);
 }
 
 size_t conv_gemm_splitk_need(const GemmArgs& a, int mode, size_t* tiles) {

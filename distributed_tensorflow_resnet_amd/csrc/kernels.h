@@ -136,7 +136,6 @@ struct GemmArgs {
   ConvGeom g;
   int M, Ncol, Kdim;
   long long* probe = nullptr;   // direct conv: per-workgroup phase timestamps (diagnostics)
-  long long* kprobe = nullptr;  // ring8: workgroup 0's phase / K-tile timeline (diagnostics)
   int wt = 0;                   // epilogue output stores write-through (sc1): tune wt_store
   // split-K (conv_gemm FAST loop; set by the launcher): gridDim.z = ksplit slices of the
   // K tiles; each slice publishes its fp32 tile to sk_part, the last arriver of the tile
@@ -207,12 +206,6 @@ int conv_gemm_bm(int M, int Ncol);
 // caller's grid (split-K / parity set up by the caller, conv_gemm.hip)
 bool conv_ring_covers(const GemmArgs& a, int mode);
 void conv_ring(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
-// 8-wave 256 x 128 tile, 3-stage ring for the deep-K (>= 1152) convs (conv_ring8.hip)
-bool conv_ring8_covers(const GemmArgs& a, int mode);
-void conv_ring8(const GemmArgs& a, int mode, int flags, dim3 grid, hipStream_t s);
-size_t conv_ring8_lds();
-bool conv_gemm_uses_ring8(const GemmArgs& a, int mode);   // (parity classes resolved)
-void set_ring8_probe(long long* p);   // diagnostics: workgroup 0's timeline (nullptr = off)
 bool conv_gemm_uses_ring(const GemmArgs& a, int mode);
 int conv_gemm_bn(int M, int Ncol);   // column tile of the kernel conv_gemm() picks
 

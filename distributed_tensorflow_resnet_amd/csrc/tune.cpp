@@ -76,11 +76,6 @@ const TuneEntry kTable[T_COUNT] = {
     {"ring_kt_dgrad", 4,
      "ring dgrads from this many 64-deep K tiles (the 4-tile 14x14 1024->256 dgrad: 75.8 -> "
      "68.8 us on the ring)"},
-    {"ring8", 0,
-     "8-wave 256x128-tile 3-stage LDS-DMA ring (conv_ring8.hip) for the 3x3 convs with K >= 1024; "
-     "off: 0.88-1.0 us per K tile (2x the MFMA bound) plus ~11 us of exposed prologue, first "
-     "DMA and epilogue per workgroup -- 478-621 TF/s vs the 4-wave ring's 558-679 "
-     "(profiles/imagenet_ring8.md)"},
     {"prn_shards", 8,
      "arrival-counter shards (one 128-B line each, workgroup b on b % shards) of the persistent "
      "CIFAR step's grid barriers: 8 or 1 (profiles/bn_barrier.md)"},

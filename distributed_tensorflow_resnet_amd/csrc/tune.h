@@ -35,7 +35,6 @@ enum TuneId : int {
   T_RING,              // LDS-DMA ring implicit GEMM (conv_ring.hip) for eligible convs
   T_RING_KT,           // ... forward convs with K loops of at least this many 64-deep tiles
   T_RING_KT_DGRAD,     // ... dgrads with K loops of at least this many tiles
-  T_RING8,             // 8-wave 256x128 3-stage ring for the deep-K convs (conv_ring8.hip)
   T_PRN_SHARDS,        // arrival-counter shards of the persistent CIFAR step's grid barriers
   T_COUNT
 };

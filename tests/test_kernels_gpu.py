@@ -759,80 +759,6 @@ def test_ring_conv_matches_register_loop_and_reference(gpu, mode, N, H, C, K, k,
     torch.testing.assert_close(sums[1], sums[0], rtol=2e-3, atol=2e-2)
 
 
-RING8_CASES = [
-    # mode, N, H, C, K, k, s
-    ("fwd", 32, 14, 256, 256, 3, 1),      # M = 6272: the last tile's second half is empty
-    ("fwd", 64, 28, 128, 128, 3, 1),      # M = 50176 = 196 tiles of 256
-    ("fwd", 32, 28, 128, 128, 3, 2),      # stride-2 transition
-    ("fwd", 128, 7, 512, 512, 3, 1),      # split-K (25 x 4 tiles)
-    ("dgrad", 32, 14, 256, 256, 3, 1),
-    ("dgrad", 128, 14, 256, 256, 3, 2),   # stride 2: output-parity classes
-    ("dgrad", 128, 7, 512, 512, 3, 1),    # split-K
-]
-
-
-@pytest.mark.parametrize("mode,N,H,C,K,k,s", RING8_CASES)
-def test_ring8_conv_matches_ring_and_reference(gpu, mode, N, H, C, K, k, s):
-    """8-wave 256x128 3-stage ring (conv_ring8.hip) == the 4-wave 128x128 ring (tune
-    ring8=0) to fp32 summation order and == the fp32 reference, with the fused
-    epilogues in accumulator mode (forward: residual + BN statistics into the fp64
-    replicas; dgrad: BN-backward sums + accumulate-into-output); both epilogue halves,
-    rows past M, split-K and parity classes."""
-    torch.manual_seed(23)
-    nat = fn.native()
-    dflt = {t[0]: t[1] for t in nat.tune_table()}
-    g = fn.ConvGeom(N, H, H, C, K, k, k, s)
-    fwd = mode == "fwd"
-    nat.tune_set("ring8", 1)   # (off by default: profiles/imagenet_ring8.md)
-    try:
-        assert nat.conv_ring8_covers(0 if fwd else 1, g.as_list())
-    finally:
-        nat.tune_set("ring8", dflt["ring8"])
-    if fwd:
-        x = torch.randn(N, H, H, C, device=gpu).to(BF)
-        w = (torch.randn(K, k, k, C, device=gpu) / math.sqrt(k * k * C)).to(BF)
-        res = torch.randn(N, g.Ho, g.Wo, K, device=gpu).to(BF)
-        tiles, _ = fn.stat_tiles(N * g.Ho * g.Wo, K)
-    else:
-        dy = torch.randn(N, g.Ho, g.Wo, K, device=gpu).to(BF)
-        w = (torch.randn(k, k, C, K, device=gpu) / math.sqrt(k * k * K)).to(BF)
-        x = torch.randn(N, H, H, C, device=gpu).to(BF)
-        base = torch.randn(N, H, H, C, device=gpu).to(BF)
-        mean, rstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
-        sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
-    outs, sums = [], []
-    for r8 in (0, 1):
-        nat.tune_set("ring8", r8)
-        try:
-            for _ in range(2):   # repeated launches (split-K tickets are reset)
-                if fwd:
-                    acc = torch.zeros(8 * 2 * K, device=gpu, dtype=torch.float64)
-                    part = torch.zeros(tiles * 2 * K, device=gpu)
-                    out = fn.conv2d_fwd(x, w, s, residual=res, stat_part=part, fin=[acc])
-                    red = acc.view(8, 2, K).sum(0)
-                else:
-                    bacc = torch.zeros(8 * 2 * C, device=gpu, dtype=torch.float64)
-                    part = torch.zeros((N * H * H // 64 + 1) * 2 * C, device=gpu)
-                    out = base.clone()
-                    fn.conv2d_dgrad(dy, w, tuple(x.shape), s, out=out, accumulate=True,
-                                    bnb=(x, mean, rstd, sc, sh, part), bfin=[bacc])
-                    red = bacc.view(8, 2, C).sum(0)
-            torch.cuda.synchronize()
-        finally:
-            nat.tune_set("ring8", dflt["ring8"])
-        outs.append(out.float())
-        sums.append(red.float())
-    if fwd:
-        want = ref.conv2d(x.float(), w.float().permute(1, 2, 3, 0), s) + res.float()
-    else:
-        xt = torch.zeros(N, H, H, C, device=gpu, requires_grad=True)
-        ref.conv2d(xt, w.float(), s).backward(dy.float())
-        want = xt.grad + base.float()
-    assert _rel(outs[1], outs[0]) < 2e-3
-    assert _rel(outs[1], want) < 1e-2
-    torch.testing.assert_close(sums[1], sums[0], rtol=2e-3, atol=2e-2)
-
-
 @pytest.mark.parametrize("N,H,C,K,k,s", [(4, 28, 128, 128, 3, 1), (8, 14, 256, 256, 3, 2),
                                          (4, 56, 256, 128, 1, 1), (16, 7, 512, 512, 3, 1),
                                          (2, 14, 1024, 2048, 1, 2)])
