@@ -471,10 +471,11 @@ static Launch mk_head_fused(ptr_t x, std::vector<ptr_t> bn, float momentum, floa
 // Persistent small-batch CIFAR step (cifar_persist.hip).  mode 0: forward launch, 1:
 // backward launch.  ptrs = [blocks, bns, x_in, stem_w, pool_acc, bar, err, dense_w,
 // dense_b, labels, pooled, dlogits, ws, dpool, dx0, items]; ints = [nblocks, nitems, N, P,
-// classes, kpad, update_moving, wgrad_wgs, fault_bar]; floats = [grad_scale, momentum, eps].
+// classes, kpad, update_moving, wgrad_wgs, fault_bar, overlap, bucket of stage 0, 1, 2];
+// floats = [grad_scale, momentum, eps].
 static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::vector<float> f) {
-  if (p.size() != 20 || n.size() != 9 || f.size() != 3)
-    throw std::invalid_argument("prn: 20 pointers, 9 ints, 3 floats");
+  if (p.size() != 20 || n.size() != 13 || f.size() != 3)
+    throw std::invalid_argument("prn: 20 pointers, 13 ints, 3 floats");
   PrnArgs a{};
   a.blocks = P<const PrnBlock>(p[0]);
   a.bns = P<const PrnBn>(p[1]);
@@ -505,6 +506,8 @@ static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::ve
   a.update_moving = n[6];
   const int wgs = n[7];
   a.fault_bar = n[8];
+  a.overlap = n[9];
+  for (int i = 0; i < 3; ++i) a.bucket_of_stage[i] = n[10 + i];
   a.grad_scale = f[0];
   a.momentum = f[1];
   a.eps = f[2];
@@ -514,6 +517,10 @@ static Launch mk_prn(int mode, std::vector<ptr_t> p, std::vector<int> n, std::ve
   if (mode == 1) return [a, wgs](hipStream_t s) { prn_backward(a, wgs, s); };
   if (mode == 2) return [a](hipStream_t s) { prn_head(a, s); };
   throw std::invalid_argument("prn: mode 0 (forward), 1 (backward) or 2 (head folds)");
+}
+
+static Launch mk_prn_bucket_wait(ptr_t bar, int bucket, long long target, ptr_t err) {
+  return [=](hipStream_t s) { prn_bucket_wait(P<unsigned>(bar), bucket, (unsigned)target, P<int>(err), s); };
 }
 
 // bn_bwd_apply with the finalize fused in: fin = [acc, gamma, dgamma, dbeta, coef]
@@ -1183,6 +1190,7 @@ PYBIND11_MODULE(_C, m) {
         "whether bn_bwd_apply_acc (finalize fused into the apply) covers (M, C)");
   def_op(m, plan, "head_fused", mk_head_fused);
   def_op(m, plan, "prn", mk_prn);
+  def_op(m, plan, "prn_bucket_wait", mk_prn_bucket_wait);
   m.def("prn_set_probe", [](ptr_t p) { prn_set_probe(P<long long>(p)); },
         "diagnostics: image 0 of the persistent launches records (tag, wall clock) pairs here");
   m.def("prn_supported", &prn_supported, "whether the persistent CIFAR step covers (N, slices, blocks, classes, kpad)");

@@ -150,6 +150,17 @@ __device__ __forceinline__ void stg(T* p, T v) {
 #endif
 }
 
+// 4-byte write-through store (global_store_dword ... sc1): read by another agent-scope
+// consumer before this kernel ends (overlap mode)
+__device__ __forceinline__ void st_sc1_f32(float* p, float v) {
+#if __HIP_DEVICE_COMPILE__
+  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ bf16x8 lds16(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 __device__ __forceinline__ double ld_sc1_d(const double* p) {
@@ -218,7 +229,18 @@ constexpr int PRN_SHARDS = 8, PRN_LINE = 32;   // 32 words = one 128-B line per 
 // the backward readiness count at PRN_READY, the weight-gradient item queue at PRN_QUEUE
 // (each on its own line; PRN_BAR_WORDS in all, zeroed every step)
 constexpr int PRN_FWD = 0, PRN_BWD = PRN_SHARDS * PRN_LINE, PRN_READY = 2 * PRN_SHARDS * PRN_LINE,
-              PRN_QUEUE = PRN_READY + PRN_LINE, PRN_BAR_WORDS = PRN_QUEUE + PRN_LINE;
+              PRN_QUEUE = PRN_READY + PRN_LINE, PRN_BUCKET = PRN_QUEUE + PRN_LINE,
+              PRN_NBUCKET = 3, PRN_BAR_WORDS = PRN_BUCKET + PRN_NBUCKET * PRN_LINE;
+constexpr unsigned PRN_BUCKET_RELEASED = 0x40000000u;   // a timed-out launch releases the waiters
+
+// a timed-out wait: flag the error and release the comm stream's bucket waiters (they
+// would otherwise wait for counts the exiting workgroups never reach)
+__device__ __forceinline__ void prn_fail(unsigned* bar, int* err) {
+  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int b = 0; b < PRN_NBUCKET; ++b)
+    __hip_atomic_store(bar + PRN_BUCKET + b * PRN_LINE, PRN_BUCKET_RELEASED, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Every wave drains its stores / atomics, then lane 0 arrives on its shard.  The caller
 // issues its prefetches (waves 1-7) and waits (grid_wait).
@@ -233,8 +255,9 @@ __device__ __forceinline__ void grid_arrive(unsigned* bar, int shards) {
 // Wait until barrier k (1-based) of `nsl` arriving workgroups is complete: shard s holds
 // k x (the arrivers b < nsl with b % 8 == s).  Lanes 0-7 of wave 0 poll their shard every
 // 64 clocks.  Returns false when the wait timed out (*err set): the caller exits.
-__device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned k, unsigned nsl, int shards,
-                                          int* err, int* flag) {
+__device__ __forceinline__ bool grid_wait(unsigned* base, int off, unsigned k, unsigned nsl,
+                                          int shards, int* err, int* flag) {
+  unsigned* bar = base + off;
   if ((int)threadIdx.x < shards) {
     const unsigned sh = threadIdx.x;
     const unsigned target = k * ((nsl + shards - 1 - sh) / shards);
@@ -246,7 +269,7 @@ __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned k, unsigned ns
       if (__builtin_amdgcn_ballot_w64(!done) == 0) break;   // every shard complete
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > kSpinTicks) {
-        if (sh == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sh == 0) prn_fail(base, err);
         ok = 0;
         break;
       }
@@ -260,14 +283,16 @@ __device__ __forceinline__ bool grid_wait(unsigned* bar, unsigned k, unsigned ns
 // Wait until the single counter `ctr` reaches `target` (the weight-gradient workgroups on
 // the readiness line; they poll 8x less often: ~190 pollers on one line slow its writer).
 template <int SLEEP = 8>
-__device__ __forceinline__ bool count_wait(unsigned* ctr, unsigned target, int* err, int* flag) {
+__device__ __forceinline__ bool count_wait(unsigned* base, int off, unsigned target, int* err,
+                                           int* flag) {
   if (threadIdx.x == 0) {
+    const unsigned* ctr = base + off;
     const long long t0 = wall_clock64();
     int ok = 1;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(SLEEP);
       if (wall_clock64() - t0 > kSpinTicks) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prn_fail(base, err);
         ok = 0;
         break;
       }
@@ -801,9 +826,9 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, 
     tbl[256 + c] = pr.rstd;
     tbl[320 + c] = pr.scale;
     tbl[384 + c] = pr.shift;
-    if (blockIdx.x == 0) {
-      stg(bn.dbeta + c, sg);
-      stg(bn.dgamma + c, sgx);
+    if (blockIdx.x == 0) {   // (write-through: the overlap mode's comm stream reads them
+      st_sc1_f32(bn.dbeta + c, sg);   //  while this launch still runs)
+      st_sc1_f32(bn.dgamma + c, sgx);
     }
   }
   __syncthreads();
@@ -892,6 +917,7 @@ struct Ctx {
   int pc;            // probe stamps written
   BnRegs bnr;        // prefetched BN parameters of the next combine
   BnRegs ftr;        // backward: prefetched forward table of the next BN-backward sums
+  unsigned* mark;    // overlap mode, workgroup 0: bucket line its next arrive counts on
 };
 
 // diagnostics: workgroup 0's lane 0 records (tag, wall clock) pairs (prn_set_probe)
@@ -911,14 +937,23 @@ __device__ __forceinline__ bool wait_fwd(Ctx& x) {
     if (threadIdx.x == 0) __hip_atomic_store(x.a->err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
   }
-  return grid_wait(x.a->bar + PRN_FWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
+  return grid_wait(x.a->bar, PRN_FWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
 }
 // Backward: slice workgroup 0 republishes every completed barrier as a count on its own
 // line (bar + PRN_READY): the ~190 weight-gradient workgroups poll that line instead of
 // the arrival shards the slices' atomics go to.
+// backward arrive; workgroup 0 then also counts a finished bucket of BatchNorm gradients
+// (x.mark), ordered after the arrive's drain of its write-through dgamma / dbeta stores
+__device__ __forceinline__ void arrive_bwd(Ctx& x) {
+  grid_arrive(x.a->bar + PRN_BWD, x.a->shards);
+  if (x.mark != nullptr) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(x.mark, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x.mark = nullptr;
+  }
+}
 __device__ __forceinline__ bool wait_bwd(Ctx& x) {
   ++x.nbar;
-  const bool ok = grid_wait(x.a->bar + PRN_BWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
+  const bool ok = grid_wait(x.a->bar, PRN_BWD, x.nbar, x.slices, x.a->shards, x.a->err, x.m.flag);
   if (ok && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(x.a->bar + PRN_READY, x.nbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ok;
@@ -1049,6 +1084,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
   x.nbar = 0;
   x.slices = (unsigned)(a.N * P);
   x.pc = 0;
+  x.mark = nullptr;
   const int tid = threadIdx.x;
   probe(x, 0);
 
@@ -1357,7 +1393,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     publish<S, P, 1>(da, B.da2 + img_o, x.kslice, wave, lane);
   bwd_sums<S, P>(x, da, hs, x.m.tbl, B.bn2, wave, lane);
   probe(x, 4);
-  grid_arrive(a.bar + PRN_BWD, a.shards);
+  arrive_bwd(x);
   // dout for the conv2 / projection weight gradients and the neighbours' residual rows:
   // stored after this arrive (its drain overlaps the wait), drained by the next one
   publish<S, P>(dout, B.dout + img_o, x.kslice, wave, lane);
@@ -1400,7 +1436,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
     publish<SI, P, 1>(da, B.da1 + img_i, x.kslice, wave, lane);
   bwd_sums<SI, P>(x, da, xs, x.m.tbl, B.bn1, wave, lane);
   probe(x, 10);
-  grid_arrive(a.bar + PRN_BWD, a.shards);
+  arrive_bwd(x);
   // dh1 for the conv1 weight gradient, from its halo (HA, intact until the next block
   // stages its own): stored after this arrive, drained by the next one
   halo_to_global<S, P>(x.m.ha, B.dh1 + img_o, x.kslice);
@@ -1415,6 +1451,10 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   NbrBwd q;
   bwd_nbr_issue<SI, P>(nb, B.da1 + img_i, B.x + img_i, PROJ ? nullptr : B.dout + img_o, q);
   bn_bwd_table(ld_const(a.bns + (B.bn1)), x.bnr, GI::C, (float)a.N * GI::R * GI::R, x.m.tbl2);
+  // a stage's first block is the last one the backward reaches: its BN1 gradient completes
+  // the stage's BatchNorm gradients (overlap mode: counted on the stage's bucket line)
+  if (PROJ && a.overlap && blockIdx.x == 0 && a.bucket_of_stage[S] >= 0)
+    x.mark = a.bar + PRN_BUCKET + a.bucket_of_stage[S] * PRN_LINE;
   if constexpr (PROJ) bwd_apply<SI, P, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   else bwd_apply<SI, P, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   if (has_prev) load_regs<SI, P>(hs, Bn.h1 + img_i, x.kslice, wave, lane);   // previous block's BN2 input
@@ -1431,7 +1471,7 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
 // fragments by the transposed read ds_read_b64_tr_b16 (conv_wgrad_direct.hip's scheme);
 // waves = WT tile groups x (8 / WT) pixel slices, summed in LDS in a fixed order.
 template <int CO, int CI, int KSZ, int STR, int RO, int WT>
-__device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wave, int lane) {
+__device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wave, int lane, bool wt) {
   constexpr int RI = RO * STR, W2 = RI + 2, OFF = KSZ == 1 ? 1 : 0;
   constexpr int KN = KSZ * KSZ * CI, NB = (KN + 15) / 16, MB = CO / 16;
   constexpr int TILES = MB * NB, TPW = TILES / WT, WKS = NW / WT;
@@ -1522,9 +1562,15 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
     for (int t = 0; t < TPW; ++t) {
       const int tile = tg * TPW + t, mb = tile / NB, nb = tile - mb * NB;
       const int n = nb * 16 + li;
-      if (n < KN)
+      if (n < KN) {
+        if (wt) {   // overlap mode: read by the comm stream while the launch runs
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stg(it.part + (long)(mb * 16 + 4 * gq + i) * KN + n, acc[t][i]);
+          for (int i = 0; i < 4; ++i) st_sc1_f32(it.part + (long)(mb * 16 + 4 * gq + i) * KN + n, acc[t][i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) stg(it.part + (long)(mb * 16 + 4 * gq + i) * KN + n, acc[t][i]);
+        }
+      }
     }
   }
   __syncthreads();
@@ -1536,17 +1582,17 @@ __host__ __device__ constexpr int wg_lds(int co, int ci, int str, int ro) {
   return ro * ro * co * 2 + (ro * str + 2) * (ro * str + 2) * ci * 2 + 512;
 }
 
-__device__ __forceinline__ void run_item(const PrnItem& it, char* smem, int wave, int lane) {
+__device__ __forceinline__ void run_item(const PrnItem& it, char* smem, int wave, int lane, bool wt) {
   switch (it.kind) {
-    case 0: wgrad_item<16, 16, 3, 1, 32, 1>(it, smem, wave, lane); break;   // stage-0 3x3
-    case 1: wgrad_item<32, 32, 3, 1, 16, 2>(it, smem, wave, lane); break;   // stage-1 3x3
-    case 2: wgrad_item<64, 64, 3, 1, 8, 8>(it, smem, wave, lane); break;    // stage-2 3x3
-    case 3: wgrad_item<32, 16, 3, 2, 16, 2>(it, smem, wave, lane); break;   // 3x3/2 16->32
-    case 4: wgrad_item<64, 32, 3, 2, 8, 8>(it, smem, wave, lane); break;    // 3x3/2 32->64
-    case 5: wgrad_item<16, 16, 1, 1, 32, 1>(it, smem, wave, lane); break;   // 1x1 16->16
-    case 6: wgrad_item<32, 16, 1, 2, 16, 2>(it, smem, wave, lane); break;   // 1x1/2 16->32
-    case 7: wgrad_item<64, 32, 1, 2, 8, 8>(it, smem, wave, lane); break;    // 1x1/2 32->64
-    case 8: wgrad_item<16, 8, 3, 1, 32, 1>(it, smem, wave, lane); break;    // stem 8->16
+    case 0: wgrad_item<16, 16, 3, 1, 32, 1>(it, smem, wave, lane, wt); break;   // stage-0 3x3
+    case 1: wgrad_item<32, 32, 3, 1, 16, 2>(it, smem, wave, lane, wt); break;   // stage-1 3x3
+    case 2: wgrad_item<64, 64, 3, 1, 8, 8>(it, smem, wave, lane, wt); break;    // stage-2 3x3
+    case 3: wgrad_item<32, 16, 3, 2, 16, 2>(it, smem, wave, lane, wt); break;   // 3x3/2 16->32
+    case 4: wgrad_item<64, 32, 3, 2, 8, 8>(it, smem, wave, lane, wt); break;    // 3x3/2 32->64
+    case 5: wgrad_item<16, 16, 1, 1, 32, 1>(it, smem, wave, lane, wt); break;   // 1x1 16->16
+    case 6: wgrad_item<32, 16, 1, 2, 16, 2>(it, smem, wave, lane, wt); break;   // 1x1/2 16->32
+    case 7: wgrad_item<64, 32, 1, 2, 8, 8>(it, smem, wave, lane, wt); break;    // 1x1/2 32->64
+    case 8: wgrad_item<16, 8, 3, 1, 32, 1>(it, smem, wave, lane, wt); break;    // stem 8->16
     default: break;
   }
 }
@@ -1570,6 +1616,7 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
   x.nbar = 0;
   x.slices = (unsigned)nsl;
   x.pc = 0;
+  x.mark = nullptr;
   probe(x, 0);
   const int nb = a.nblocks;
   const PrnBlock& BL = ld_const(a.blocks + (nb - 1));
@@ -1601,7 +1648,7 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
       for (int r = 0; r < 4; ++r) dp[t][r] = (bf16)dps[(cb * 16 + 4 * (lane >> 4) + r) & 63];
     }
     bwd_sums<2, P>(x, dp, xs, x.m.tbl, fb, wave, lane);
-    grid_arrive(a.bar + PRN_BWD, a.shards);
+    arrive_bwd(x);
     bn_prefetch_bwd(ld_const(a.bns + (fb)), 64, x.bnr);
     bn_prefetch_tab(ld_const(a.bns + (BL.bn2)), 64, x.ftr);
     if (!wait_bwd(x)) return false;
@@ -1636,7 +1683,7 @@ __device__ __forceinline__ bool prn_bwd_slices(const PrnArgs& a, char* smem, int
   probe(x, 200);
   // ---- the stem output's gradient: published for the stem's weight gradient ----
   publish<0, P>(dout, a.dx0 + (long)x.img * 1024 * 16, x.kslice, wave, lane);
-  grid_arrive(a.bar + PRN_BWD, a.shards);
+  arrive_bwd(x);
   if (blockIdx.x == 0) wait_bwd(x);   // publishes the stem item's readiness
   return true;
 }
@@ -1749,8 +1796,30 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
     const int i = __builtin_amdgcn_readfirstlane(*slot);
     if (i >= a.nitems) return;
     const PrnItem& it = ld_const(a.items + i);
-    if (!count_wait<8>(a.bar + PRN_READY, (unsigned)it.ready, a.err, flag)) return;
-    run_item(it, smem, wave, lane);
+    if (!count_wait<8>(a.bar, PRN_READY, (unsigned)it.ready, a.err, flag)) return;
+    run_item(it, smem, wave, lane, a.overlap != 0);
+    if (a.overlap && it.bucket >= 0) {   // the slab's write-through stores drained, then counted
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add(a.bar + PRN_BUCKET + it.bucket * PRN_LINE, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// comm-stream bucket wait (overlap mode): lane 0 polls the bucket line (bounded)
+__global__ void __launch_bounds__(64) prn_bucket_wait_kernel(unsigned* bar, int bucket, unsigned target,
+                                                            int* err) {
+  if (threadIdx.x != 0) return;
+  const unsigned* ctr = bar + PRN_BUCKET + bucket * PRN_LINE;
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > kSpinTicks) {
+      __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
   }
 }
 
@@ -1839,6 +1908,13 @@ void prn_head(const PrnArgs& a, hipStream_t s) {
   const size_t lds = prn_head_lds(a.N, a.kpad);
   if (lds > LDS_TOTAL) throw std::invalid_argument("prn_head: batch too large for LDS");
   hipLaunchKernelGGL(prn_head_kernel, dim3(1), dim3(PT), lds, s, a);
+  DTR_CHECK_LAUNCH();
+}
+
+void prn_bucket_wait(unsigned* bar, int bucket, unsigned target, int* err, hipStream_t s) {
+  if (bucket < 0 || bucket >= PRN_NBUCKET || bar == nullptr || err == nullptr)
+    throw std::invalid_argument("prn_bucket_wait: bucket 0..2, bar and err required");
+  hipLaunchKernelGGL(prn_bucket_wait_kernel, dim3(1), dim3(64), 0, s, bar, bucket, target, err);
   DTR_CHECK_LAUNCH();
 }
 

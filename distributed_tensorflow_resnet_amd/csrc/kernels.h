@@ -260,6 +260,9 @@ struct PrnItem {             // backward weight-gradient work item: one conv x o
   int kind;                  // conv shape class (prn_item_kind)
   int img0, nimg;
   int ready;                 // backward barrier arrivals (x slices) after which dy is complete
+  int bucket;                // overlap mode: all-reduce bucket whose counter counts this item
+                             // (its slab stored write-through), -1 none
+  int pad_;
 };
 struct PrnArgs {
   const PrnBlock* blocks;
@@ -294,6 +297,12 @@ struct PrnArgs {
   int update_moving;
   long long* probe = nullptr;   // diagnostics: workgroup 0's (tag, wall clock) phase stamps
   int shards = 8;            // arrival-counter shards (tune prn_shards: 1 or 8)
+  // overlap mode (world > 1): each weight-gradient item's slab is stored write-through
+  // and counted on its bucket's line of `bar` (PRN_BUCKET), and slice workgroup 0 counts
+  // the bucket's BatchNorm gradients there once its last BN backward is stored, so the
+  // comm stream's slab reduce + all-reduce of a bucket start while the backward runs
+  int overlap = 0;
+  int bucket_of_stage[3] = {-1, -1, -1};   // stage 0..2 -> bucket (overlap mode)
   int fault_bar = -1;        // tests only (DTR_PRN_FAULT_BAR): forward workgroup 0 abandons the
                              // launch at this barrier, as a lost workgroup would; -1 off
 };
@@ -311,6 +320,10 @@ void prn_forward(const PrnArgs& a, hipStream_t s);
 void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s);
 // the head's batch folds (loss, precision, dense bias + weight gradients), one workgroup
 void prn_head(const PrnArgs& a, hipStream_t s);
+// comm-stream wait (overlap mode): one wave polls bar[PRN_BUCKET + 32 b] until it reaches
+// `target` (bounded: 2 s, then *err), so the launches behind it on that stream start once
+// bucket b's gradients are complete
+void prn_bucket_wait(unsigned* bar, int bucket, unsigned target, int* err, hipStream_t s);
 // item kind of a conv (stage of its output, kernel size, stride; stem = 8 input channels)
 int prn_item_kind(int cin, int cout, int ksize, int stride);
 

@@ -324,10 +324,15 @@ class Engine:
             reason = reason or "another rank cannot run the persistent step"
         self.persist_reason = reason
         self.persist = reason == ""
+        # world > 1 (or a forced communicator): the gradient buckets' reduces and
+        # all-reduces overlap the persistent backward launch (tune persist_overlap)
+        self.persist_overlap = (self.persist and self.comm is not None
+                                and bool(tune.get("persist_overlap")))
         self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
+        self._device_deps: dict[int, int] = {}   # stream check: device-side waits (op -> producer op)
         self.reduce_buckets = self.world > 1 or self.comm is not None
         if self.reduce_buckets:
             if not bucket_mb:
@@ -363,7 +368,8 @@ class Engine:
             self.bucket_sched = schedule_buckets(self.buckets, self.ready_index)
         else:
             self.bucket_sched = []
-        errs = check_plan(self.plan, self.seg, barriers=[i for i, _, _ in self.bucket_sched])
+        errs = check_plan(self.plan, self.seg, barriers=[i for i, _, _ in self.bucket_sched],
+                          device_deps=self._device_deps)
         if errs:   # fork/join structure of the three streams (race check)
             raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
         self.graph = None
@@ -1055,7 +1061,7 @@ class Engine:
         plan.use_stream(0)
         plan.wait(ev)
 
-    def _emit_reduce(self, plan, names):
+    def _emit_reduce(self, plan, names, stream: int | None = None):
         descs = [self._pending.pop(n) for n in names if n in self._pending]
         if not descs:
             return
@@ -1066,7 +1072,9 @@ class Engine:
             chunk += self.nat.wgrad_reduce_chunks(sp, K, taps, C)
         t = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
         self._keep.append(t)
-        plan.use_stream(1 if self.fork_wgrad and not self._reduce_main else 0)
+        if stream is None:
+            stream = 1 if self.fork_wgrad and not self._reduce_main else 0
+        plan.use_stream(stream)
         plan.wgrad_reduce_grouped(t.data_ptr(), len(descs), chunk, 1.0)
         st = self.spec.stem
         sc = self.convs[st.name]
@@ -1433,6 +1441,11 @@ class Engine:
         self._main_wgrad = False
         self._reduce_main = True   # the slab reduces run on the main stream
         self._produced.add(self.dense_name)
+        if self.prn.overlap:
+            self._emit_persist_overlap(plan, ptrs, ints, floats)
+            self.seg["bwd"] = (b1, plan.size())
+            self._emit_optimizer(plan, fused_slabs={} if self.opt_fused else None)
+            return
         plan.prn(1, ptrs, ints, floats)
         # the head's batch folds (loss, precision, dense bias and weight gradients): one
         # workgroup on the main stream -- no side stream, no fork/join events
@@ -1467,6 +1480,43 @@ class Engine:
             self._pending.update(slabs)
             self._emit_reduce(plan, list(slabs))
             self.seg["gsum"] = (b4, plan.size())
+
+    def _emit_persist_overlap(self, plan, ptrs, ints, floats):
+        """World > 1: the persistent backward launch on the main stream, and on the comm
+        stream (forked before it): the head's batch folds, then per gradient bucket, in
+        the order the backward completes them (persist.bucket_ranges), a one-wave wait
+        for the bucket's line in the launch's barrier region to reach its count, the
+        bucket's grouped slab reduce, and its all-reduce -- all while the backward still
+        runs on the CUs left out of its grid.  The optimizer joins the comm stream.  The
+        stream check takes each bucket wait as ordered after the backward launch
+        (device_deps): the launch publishes the bucket's completion through that line."""
+        from .persist import bucket_ranges
+
+        fork = plan.new_event()
+        plan.record(fork)
+        plan.use_stream(2)
+        plan.wait(fork)
+        plan.prn(2, ptrs, ints, floats)        # head folds (loss, precision, dense grads)
+        plan.use_stream(0)
+        bwd_op = plan.size()
+        plan.prn(1, ptrs, ints, floats)        # backward: dgrad chain + weight gradients
+        err = self.prn.err.data_ptr()
+        for b, (lo, hi, names) in enumerate(bucket_ranges(self)):
+            plan.use_stream(2)                 # (_emit_reduce/_emit_allreduce end on main)
+            self._device_deps[plan.size()] = bwd_op
+            plan.prn_bucket_wait(self.prn_bar, b, self.prn.bucket_target(b), err)
+            self._emit_reduce(plan, names, stream=2)
+            plan.use_stream(2)
+            self._mark(plan, *names)
+            self._emit_allreduce(plan, lo, hi, side_dep=False, on_main=True)
+        for bi in range(len(self.buckets)):
+            self._flushed.add(bi)
+        join = plan.new_event()
+        plan.use_stream(2)
+        plan.record(join)
+        plan.use_stream(0)
+        plan.wait(join)
+        self._t_bwd_done = self._t_joined = plan.timing_point("allreduce_joined")
 
     def forward_backward(self, st=None):
         """Forward + backward of the current batch with `grad` complete and no update

@@ -36,7 +36,14 @@ PRN_BLOCK = np.dtype([(k, "<u8") for k in ("x", "h1", "out", "w1f", "w2f", "wpf"
                                            "wpb", "dout", "dh1", "da2", "da1")] +
                      [(k, "<i4") for k in ("stage", "stride", "bn1", "bn2")])
 PRN_ITEM = np.dtype([(k, "<u8") for k in ("dy", "x", "scale", "shift", "part")] +
-                    [(k, "<i4") for k in ("kind", "img0", "nimg", "ready")])
+                    [(k, "<i4") for k in ("kind", "img0", "nimg", "ready", "bucket", "pad_")])
+# overlap mode (world > 1): CUs left out of the backward grid for the comm stream's bucket
+# waits, slab reduces and RCCL all-reduces, which run while the backward does
+OVERLAP_RESERVE_CUS = 16
+# all-reduce buckets of the overlap mode, in the order the backward completes them:
+# stage 2 (64 channels) + the final BN + dense, stage 1, stage 0 + the stem
+BUCKET_OF_STAGE = (2, 1, 0)
+
 # every supported per-rank batch (MI355X, CIFAR RN50 step vs the per-layer engine: bs16
 # 0.660 vs 0.915 ms, bs32 0.722 vs 0.962, bs64 0.837 vs 1.085, bs96 1.034 vs 1.272, bs128
 # (1 slice) 1.101 vs 1.261)
@@ -110,6 +117,28 @@ def supported(eng) -> bool:
     return check(eng) == ""
 
 
+def bucket_ranges(eng):
+    """Overlap-mode all-reduce buckets as contiguous ranges of the flat gradient (TF
+    variable order: each block's parameters together, the final BN and dense last):
+    [(lo, hi, slot names)] in BUCKET_OF_STAGE order -- bucket 0 the last stage's blocks +
+    the final BN + dense, bucket 1 the middle stage, bucket 2 the stem + the first stage."""
+    spec = eng.spec
+    nps = len(spec.blocks) // 3
+    stage_of = {spec.stem.name: 0, spec.final_bn.name: 2, "dense": 2}
+    for i, b in enumerate(spec.blocks):
+        for layer in list(b.convs) + list(b.bns) + ([b.proj] if b.proj is not None else []):
+            stage_of[layer.name] = i // nps
+    out = [[None, None, []] for _ in BUCKET_OF_STAGE]
+    for s in eng.params.train_slots:
+        r = out[BUCKET_OF_STAGE[stage_of[s.name.rsplit("/", 1)[0]]]]
+        r[0] = s.offset if r[0] is None else min(r[0], s.offset)
+        r[1] = s.offset + s.numel if r[1] is None else max(r[1], s.offset + s.numel)
+        r[2].append(s.name)
+    for lo, hi, names in out:   # contiguous: the slots of a bucket tile [lo, hi)
+        assert sum(sl.numel for sl in eng.params.train_slots if sl.name in set(names)) == hi - lo
+    return [tuple(r) for r in out]
+
+
 def _stage(b) -> int:
     return int(math.log2(b.cout // 16))
 
@@ -139,6 +168,7 @@ class PersistStep:
         self.cus = torch.cuda.get_device_properties(dev).multi_processor_count
         self.P = slices_for(N, self.cus, eng.persist_slices)          # backward
         self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
+        self.overlap = bool(getattr(eng, "persist_overlap", False))
         # barrier-timeout flag: slot 4 of the engine's scalars, so the host read of the
         # logged metrics (Engine.metrics) sees it at no extra cost; never cleared by the
         # kernels (Engine.clear_persist_error)
@@ -193,16 +223,17 @@ class PersistStep:
             c = eng.convs[name]
             size = 4 if c.spec.cout == 16 else max(1, math.ceil(N / 4))
             return [(g0, min(size, N - g0)) for g0 in range(0, N, size)]
-        convs = []   # (name, dy, x, bn scale, bn shift, ready)
+        convs = []   # (name, dy, x, bn scale, bn shift, ready, stage)
         for j, i in enumerate(range(nb - 1, -1, -1)):
             b = blocks[i]
             bn1, bn2 = eng.bns[b.bns[0].name], eng.bns[b.bns[1].name]
             d_out, d_h1 = self.dout[i].data_ptr(), self.dh1[i].data_ptr()
-            convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 3))
+            st = _stage(b)
+            convs.append((b.convs[1].name, d_out, eng.H1[i].data_ptr(), bn2, 2 * j + 3, st))
             if b.proj is not None:
-                convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 3))
-            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 4))
-        convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 2))
+                convs.append((b.proj.name, d_out, eng.X[i].data_ptr(), bn1, 2 * j + 3, st))
+            convs.append((b.convs[0].name, d_h1, eng.X[i].data_ptr(), bn1, 2 * j + 4, st))
+        convs.append((spec.stem.name, self.dx0.data_ptr(), eng.x_in.data_ptr(), None, 2 * nb + 2, 0))
         tot = 0
         self.part_off, self.splits = {}, {}
         for name, *_ in convs:
@@ -213,7 +244,9 @@ class PersistStep:
             tot += self.splits[name] * s.cout * s.kh * s.kw * c.cin
         self.part = torch.empty(max(tot, 1), device=eng.device)
         items = []
-        for name, dy, x, bn, ready in convs:
+        self.stage_of = {name: st for name, *_, st in convs}
+        self.bucket_items = [0] * len(BUCKET_OF_STAGE)
+        for name, dy, x, bn, ready, st in convs:
             c = eng.convs[name]
             s = c.spec
             kind = nat.prn_item_kind(c.cin, s.cout, s.kh, s.stride)
@@ -226,11 +259,20 @@ class PersistStep:
                     r["scale"], r["shift"] = bn.scale.data_ptr(), bn.shift.data_ptr()
                 r["part"] = self.part.data_ptr() + 4 * (self.part_off[name] + gi * slab)
                 r["kind"], r["img0"], r["nimg"], r["ready"] = kind, g0, gn, ready
+                r["bucket"] = BUCKET_OF_STAGE[st] if self.overlap else -1
+                if self.overlap:
+                    self.bucket_items[BUCKET_OF_STAGE[st]] += 1
                 items.append(r)
         self.items = np.array(items, dtype=PRN_ITEM)
         self.item_dev = self._dev(self.items)
-        self.wgrad_wgs = max(1, min(self.cus - N * self.P, len(items)))
+        reserve = OVERLAP_RESERVE_CUS if self.overlap else 0
+        self.wgrad_wgs = max(1, min(self.cus - N * self.P - reserve, len(items)))
         self.convs = [c[0] for c in convs]
+
+    def bucket_target(self, b: int) -> int:
+        """Count bucket b's line reaches when its gradients are complete (overlap mode):
+        one per weight-gradient item of its convs + slice workgroup 0's BatchNorm mark."""
+        return self.bucket_items[b] + 1
 
     def pending(self):
         """_pending entries (grouped-reduce descriptors) of every conv's slabs."""
@@ -259,6 +301,7 @@ class PersistStep:
         ptrs += [0, 0, 0, 0] if fwd else [sp, sp + 4, eng.dense_bias_grad, eng.dense_grad]
         ints = [self.nblocks, len(self.items), eng.N, self.P_fwd if fwd else self.P,
                 spec.num_classes, eng.kpad, 1,
-                self.wgrad_wgs, self.fault_bar if fwd else -1]
+                self.wgrad_wgs, self.fault_bar if fwd else -1, int(self.overlap and not fwd)]
+        ints += list(BUCKET_OF_STAGE) if self.overlap else [-1, -1, -1]
         floats = [1.0 / eng.global_batch, bn_decay, bn_eps]
         return ptrs, ints, floats

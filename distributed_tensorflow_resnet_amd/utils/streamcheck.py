@@ -37,6 +37,13 @@ R4  collectives: an all-reduce (or a host split point, `barriers`: an index
     plan, on every stream -- the bucket it reads is complete, whichever stream
     produced its gradients.
 
+Device-side dependencies (`device_deps` {op: producer op}): a launch that waits on the
+device for a producer launch on another stream to publish its part (the persistent
+backward's bucket counters: engine.py `_emit_persist_overlap`, the one-wave
+`prn_bucket_wait` kernel) orders everything after it on its stream after the producer,
+as far as this structural check is concerned -- the producer's kernel publishes that
+bucket complete (write-through stores drained before the count) while it still runs.
+
 Op encoding (`Plan.op_kinds` / `op_streams` / `op_events`): kind 0 launch,
 1 record, 2 wait, 3 timing probe (ignored); stream 0 main, 1 side, 2 comm.
 """
@@ -52,7 +59,8 @@ _COLLECTIVES = ("all_reduce",)
 def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Sequence[int],
                      segments: Iterable[Tuple[str, int, int]],
                      names: Sequence[str] | None = None,
-                     barriers: Sequence[int] = ()) -> List[str]:
+                     barriers: Sequence[int] = (),
+                     device_deps: Dict[int, int] | None = None) -> List[str]:
     """Return a list of human-readable violations (empty = ordering is sound).
 
     ``barriers``: plan indices where the host runs a collective on the main
@@ -108,6 +116,14 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
                 clock[s] = [max(x, y) for x, y in zip(clock[s], src[1])]
                 forked[s] = forked[s] or src[2]
             elif k == LAUNCH:
+                dep = (device_deps or {}).get(i)
+                if dep is not None:
+                    if not (a <= dep < i) or kinds[dep] != LAUNCH or streams[dep] == s:
+                        errs.append(f"{seg}: device dependency of {op(i)} on {op(dep)} is not "
+                                    f"an earlier launch of this segment on another stream")
+                    else:
+                        t = streams[dep]
+                        clock[s][t] = max(clock[s][t], dep)
                 if s != 0 and not forked[s] and not reported_fork[s]:
                     errs.append(f"{seg}: stream-{s} {op(i)} before any fork from the main "
                                 f"stream (R2)")
@@ -125,8 +141,9 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
     return errs
 
 
-def check_plan(plan, segments: Dict[str, Tuple[int, int]], barriers: Sequence[int] = ()) -> List[str]:
+def check_plan(plan, segments: Dict[str, Tuple[int, int]], barriers: Sequence[int] = (),
+               device_deps: Dict[int, int] | None = None) -> List[str]:
     """`check_plan_order` over a native `_C.Plan` and the engine's {name: (a, b)}."""
     return check_plan_order(plan.op_kinds(), plan.op_streams(), plan.op_events(),
                             [(k, a, b) for k, (a, b) in segments.items()], plan.names(),
-                            barriers=barriers)
+                            barriers=barriers, device_deps=device_deps)

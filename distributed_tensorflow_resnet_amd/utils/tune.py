@@ -56,6 +56,10 @@ ENGINE = {
     "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (backward: 4 "
                            "up to 32 images, 2 up to 64, else 1; forward: 4 up to 32, 2 while "
                            "2N <= 3/4 of the CUs, else 1), 1, 2 or 4 for both"),
+    "persist_overlap": (1, "world > 1: the persistent step's gradient buckets (stage 3 + head, "
+                           "stage 2, stage 1 + stem) are slab-reduced and all-reduced on the comm "
+                           "stream while the backward launch still runs (16 CUs left out of its "
+                           "grid), instead of one reduce + one all-reduce after it"),
     "opt_fused": (1, "the persistent step's optimizer as ONE launch (split-K slab sums on "
                      "one GPU, SGD-momentum, both bf16 weight copies: sgd_tiles) instead of "
                      "the grouped slab reduce + sgd_pack + ohwi_pack"),

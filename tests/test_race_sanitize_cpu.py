@@ -166,6 +166,26 @@ def test_streamcheck_comm_stream_sound_and_races():
     assert any("(R2)" in x for x in errs), errs
 
 
+def test_streamcheck_device_dependency_orders_bucket_wait():
+    """Persistent overlap plan: the comm stream's bucket all-reduce is ordered after the
+    backward launch on the main stream by a device-side counter wait, not an event."""
+    # main: fwd, record e0 | comm: wait e0, head | main: bwd (4) | comm: bucket wait (5),
+    # all_reduce (6), record e1 | main: wait e1, optimizer
+    ops = [(LAUNCH, 0, -1), (RECORD, 0, 0), (WAIT, 2, 0), (LAUNCH, 2, -1), (LAUNCH, 0, -1),
+           (LAUNCH, 2, -1), (LAUNCH, 2, -1), (RECORD, 2, 1), (WAIT, 0, 1), (LAUNCH, 0, -1)]
+    k, s, e = _plan(ops)
+    seg = [("bwd", 0, len(k))]
+    names = _names(len(k), [6])
+    assert check_plan_order(k, s, e, seg, names=names, device_deps={5: 4}) == []
+    # without the declared dependency the all-reduce races the backward: R4
+    errs = check_plan_order(k, s, e, seg, names=names)
+    assert any("(R4)" in x and "all_reduce" in x for x in errs), errs
+    # a dependency on a later op, on an op of the same stream, or on a non-launch is refused
+    for dep in ({5: 6}, {5: 3}, {5: 1}):
+        errs = check_plan_order(k, s, e, seg, names=names, device_deps=dep)
+        assert any("device dependency" in x for x in errs), (dep, errs)
+
+
 def test_streamcheck_host_split_needs_join():
     """gloo rehearsal: the host all-reduces between Plan.run calls at a split index;
     a side-stream launch queued before the split but joined only later is a race
