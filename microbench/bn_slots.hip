@@ -76,12 +76,13 @@ __device__ __forceinline__ u32x4 ld_wt_b128(const u32x4* base, int idx) {
   return __builtin_amdgcn_raw_buffer_load_b128(rs, idx * 16, 0, 16);
 }
 
-enum Mode { ATOM = 0, SLOT = 1, INT = 2, INT1 = 3 };
+enum Mode { ATOM = 0, SLOT = 1, INT = 2, INT1 = 3, INT2 = 4 };
 constexpr int NBAR = 2000;
 struct Acc {   // per barrier: fp64 [4][2][CMAX] or fixed-point u64 [4][2][CMAX]
   union {
     double d[4][2][CMAX];
     unsigned long long q[4][2][CMAX];
+    unsigned long long q2[4][4][CMAX];   // INT2: [rep][s1 hi, s1 lo, s2 hi, s2 lo][c]
   };
 };
 __device__ __forceinline__ unsigned long long ld_agent_q(const unsigned long long* p) {
@@ -93,6 +94,18 @@ __device__ __forceinline__ unsigned long long fx(float v) {
 }
 __device__ __forceinline__ double unfx(unsigned long long w, unsigned n) {
   return (double)((long long)(w - n) >> CBITS) / (double)(1 << FRAC);
+}
+// INT2: v * 2^60 split into hi * 2^46 + lo (0 <= lo < 2^46), each word (part << 9) + 1
+__device__ __forceinline__ void fx2(float v, unsigned long long& hi, unsigned long long& lo) {
+  const double d = ldexp((double)v, 60);
+  const double h = floor(ldexp(d, -46));
+  const double l = rint(d - ldexp(h, 46));
+  hi = ((unsigned long long)(long long)h << CBITS) + 1ull;
+  lo = ((unsigned long long)(long long)l << CBITS) + 1ull;
+}
+__device__ __forceinline__ double unfx2(unsigned long long hi, unsigned long long lo, unsigned n) {
+  return ldexp((double)((long long)(hi - n) >> CBITS), -14) +
+         ldexp((double)((long long)(lo - n) >> CBITS), -60);
 }
 
 template <int MODE>
@@ -111,7 +124,71 @@ __global__ void __launch_bounds__(NT, 1) bar_kernel(Ctl* c, Acc* accs, int iters
     if (do_sums < 0) continue;
     const float s1 = x + (float)blockIdx.x, s2 = x * x;
     Acc* A = accs + (it - 1);
-    if (MODE == INT || MODE == INT1) {
+    if (MODE == INT2) {
+      if (tid < ch) {
+        unsigned long long h1, l1, h2, l2;
+        fx2(s1, h1, l1);
+        fx2(s2, h2, l2);
+        unsigned long long* p = &A->q2[blockIdx.x % 4][0][tid];
+        __hip_atomic_fetch_add(p, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p + CMAX, l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p + 2 * CMAX, h2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p + 3 * CMAX, l2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const long long t0 = wall_clock64();
+      int fail = 0;
+      if (tid < 4) {
+        const unsigned want = (unsigned)((G - tid + 3) / 4);
+        for (;;) {
+          const bool done = (unsigned)(ld_agent_q(&A->q2[tid][0][0]) & ((1u << CBITS) - 1)) == want;
+          if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > kSpinTicks) {
+            fail = 1;
+            break;
+          }
+        }
+      }
+      if (fail) flag[1] = 1;
+      __syncthreads();
+      if (tid < ch) {
+        unsigned long long w[16];
+        for (;;) {
+          bool done = true;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[4 * r + j] = ld_agent_q(&A->q2[r][j][tid]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const unsigned want = (unsigned)((G - r + 3) / 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) done = done && (unsigned)(w[4 * r + j] & ((1u << CBITS) - 1)) == want;
+          }
+          if (done) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > kSpinTicks) {
+            fail = 1;
+            break;
+          }
+        }
+        unsigned long long h1 = 0, l1 = 0, h2 = 0, l2 = 0;
+        unsigned n = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          h1 += w[4 * r];
+          l1 += w[4 * r + 1];
+          h2 += w[4 * r + 2];
+          l2 += w[4 * r + 3];
+          n += (unsigned)((G - r + 3) / 4);
+        }
+        tbl[tid] = unfx2(h1, l1, n);
+        tbl[CMAX + tid] = unfx2(h2, l2, n);
+        if (fail) flag[1] = 1;
+      }
+      __syncthreads();
+      ok = flag[1] == 0;
+    } else if (MODE == INT || MODE == INT1) {
       if (tid < ch) {
         unsigned long long* p = &A->q[blockIdx.x % 4][0][tid];
         __hip_atomic_fetch_add(p, fx(s1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -313,7 +390,7 @@ int main() {
               prop.name, prop.multiProcessorCount);
   std::printf("us per barrier (median of 5 launches of 2000 barriers, minus the work alone), 512-thread "
               "workgroups, one per CU. `microbench/bn_slots.hip`.\n\n");
-  std::printf("| workgroups | channels | work | atom | slot | int | int1 |\n|---|---|---|---|---|---|---|\n");
+  std::printf("| workgroups | channels | work | atom | slot | int | int1 | int2 |\n|---|---|---|---|---|---|---|---|\n");
   for (int G : {16, 64, 128, 256}) {
     for (int ch : {16, 64}) {
       for (int work : {0, 400}) {
@@ -323,8 +400,11 @@ int main() {
         const float s = per_barrier<SLOT>(c, accs, G, work, ch, &bs);
         const float q = per_barrier<INT>(c, accs, G, work, ch, &bi);
         const float q1 = per_barrier<INT1>(c, accs, G, work, ch, &bi1);
-        bad = ba || bs || bi || bi1;
-        std::printf("| %d | %d | %d | %.2f | %.2f | %.2f | %.2f |%s%s%s%s\n", G, ch, work, a, s, q, q1,
+        bool bi2 = false;
+        const float q2 = per_barrier<INT2>(c, accs, G, work, ch, &bi2);
+        bad = ba || bs || bi || bi1 || bi2;
+        std::printf("| %d | %d | %d | %.2f | %.2f | %.2f | %.2f | %.2f |%s%s%s%s%s\n", G, ch, work, a, s, q, q1, q2,
+                    bi2 ? " int2-FAIL" : "",
                     ba ? " atom-FAIL" : "", bs ? " slot-FAIL" : "", bi ? " int-FAIL" : "",
                     bi1 ? " int1-FAIL" : "");
         std::fflush(stdout);
