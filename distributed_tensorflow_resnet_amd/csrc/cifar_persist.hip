@@ -310,9 +310,12 @@ struct WLoad {
   int dgrad, cin, cout; // dgrad: rows = ci of HWIO [tap][ci][co], k = tap * cout + co
 };
 
+// (the thread id is taken opaque in both: otherwise each stage loop hoists the per-thread
+// addresses of every weight unit out of its loop and keeps them live across the blocks --
+// the backward kernels' VGPR spills)
 template <int NR>
 __device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
-  const int t = (int)threadIdx.x - 64;
+  const int t = opaque_v((int)threadIdx.x) - 64;
   if (t < 0 || L.src == nullptr) return;
   const int upr = L.K / 8, units = L.rows * upr;
 #pragma unroll
@@ -335,7 +338,7 @@ __device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
 template <int NR>
 __device__ __forceinline__ void w_store(const WLoad& L, const bf16x8 (&r)[NR], bf16* wl) {
   if (L.src == nullptr) return;
-  const int tid = threadIdx.x, t = tid - 64;
+  const int tid = opaque_v((int)threadIdx.x), t = tid - 64;
   const int upr = L.K / 8, units = L.rows * upr;
   if (t >= 0) {
 #pragma unroll
