@@ -599,13 +599,13 @@ static Launch mk_sgd_tiles(ptr_t master, ptr_t grad, ptr_t mom, float init,
                            std::vector<long long> bounds, std::vector<float> vals, ptr_t gstep,
                            float momentum, float wd, float grad_scale, int use_momentum,
                            ptr_t segs, ptr_t work, ptr_t blk_seg, int nblocks, ptr_t bf,
-                           ptr_t lr_out, ptr_t ticket) {
+                           ptr_t lr_out, ptr_t ticket, ptr_t gin, ptr_t gout, int pack) {
   const LrSchedule sc = make_sched(init, warm_steps, warm_from, warm_to, bounds, vals);
   return [=](hipStream_t s) {
     sgd_tiles(P<float>(master), P<float>(grad), P<float>(mom), sc, P<long long>(gstep),
               momentum, wd, grad_scale, use_momentum, P<const ParamSeg>(segs),
               P<const OptWork>(work), P<const int>(blk_seg), nblocks, P<bf16>(bf),
-              P<float>(lr_out), P<unsigned>(ticket), s);
+              P<float>(lr_out), P<unsigned>(ticket), P<const bf16>(gin), P<bf16>(gout), pack, s);
   };
 }
 

@@ -35,10 +35,15 @@ struct OptWork {
 };
 // blk_seg[b] = the segment of workgroup b; ticket: a zero-initialised int the last
 // workgroup resets after its global_step += 1 (every workgroup has read the step).
+// gin (no slabs): the gradient read as bf16 from gin (the bf16 all-reduce's result; the
+// fp32 grad is written from it).  pack: no update -- the gradient (slab sums or grad) is
+// only written out, as bf16 to gout (or, gout null, as fp32 to grad): the all-reduce's
+// input in one launch instead of a grouped reduce plus a cast.
 void sgd_tiles(float* master, float* grad, float* mom, const LrSchedule& s, long long* gstep,
                float momentum, float wd, float grad_scale, int use_momentum,
                const ParamSeg* segs, const OptWork* work, const int* blk_seg, int nblocks,
-               bf16* bf, float* lr_out, unsigned* ticket, hipStream_t st);
+               bf16* bf, float* lr_out, unsigned* ticket, const bf16* gin, bf16* gout, int pack,
+               hipStream_t st);
 void step_increment(long long* gstep, hipStream_t s);
 int l2_workspace_floats();
 void l2_half_sum(const float* v, long n, float* ws, float* out, hipStream_t s);

@@ -226,12 +226,19 @@ void ohwi_pack(const float* master, const ParamSeg* segs, const long long* tile0
 //   3. the bf16 tile transposed through LDS into the OHWI copy (written along ci).
 // Other tensors (BN gamma/beta, biases) go in 1024-element chunks.  The rate comes from
 // global_step; the last workgroup to finish (by ticket) does global_step += 1.
+// World > 1 (optim.h): `pack` launches stop after the gradient (written as the bf16
+// all-reduce input `gout`, or to grad), and the update launch then reads it back from
+// `gin` (the all-reduced bf16).
+// MODE 0: update (gradient from slabs / grad); 1: pack; 2: update from gin.
+template <int MODE>
 __global__ void __launch_bounds__(256)
 sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict__ mom,
                  LrSchedule sched, long long* gstep, float momentum, float wd,
                  float grad_scale, int use_momentum, const ParamSeg* __restrict__ segs,
                  const OptWork* __restrict__ work, const int* __restrict__ blk_seg,
-                 bf16* __restrict__ bf, float* __restrict__ lr_out, unsigned* ticket) {
+                 bf16* __restrict__ bf, float* __restrict__ lr_out, unsigned* ticket,
+                 const bf16* __restrict__ gin, bf16* __restrict__ gout) {
+  constexpr bool pack = MODE == 1, from_gin = MODE == 2;
   __shared__ float gt[64][65];   // summed gradient tile [co][r]
   __shared__ bf16 bt[64][66];    // updated bf16 tile [r][co]
   __shared__ f32x4 red[256];     // split-group partials
@@ -264,9 +271,11 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
       wr[j] = mr[j] = gr[j] = 0.f;
       if (q < TR * TC && rl < nr && cl < nc) {
         const long e = sg.offset + (long)(r0 + rl) * K + c0 + cl;
-        wr[j] = w[e];
-        if (use_momentum) mr[j] = mom[e];
-        if (!slab) gr[j] = g[e];
+        if constexpr (!pack) {
+          wr[j] = w[e];
+          if (use_momentum) mr[j] = mom[e];
+        }
+        if (!slab) gr[j] = from_gin ? (float)gin[e] : g[e];
       }
     }
     if (slab) {
@@ -334,6 +343,12 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
         if (slab) {
           gv = gt[cl][rl];
           g[e] = gv;
+        } else if constexpr (from_gin) {
+          g[e] = gv;
+        }
+        if constexpr (pack) {
+          if (gout) gout[e] = (bf16)gv;
+          continue;
         }
         float wv = wr[j];
         gv = gv * grad_scale + wd * wv;
@@ -349,7 +364,7 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
         bt[rl][cl] = (bf16)wv;
       }
     }
-    if (sg.bf_ohwi >= 0) {
+    if (sg.bf_ohwi >= 0 && !pack) {
       __syncthreads();
       for (int q = tid; q < TR * TC; q += 256) {   // along r: the OHWI copy's ci runs
         const int cl = q / TR, rl = q - cl * TR;
@@ -369,8 +384,14 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
       const long l = base + j * 256 + tid;
       if (l < sg.numel) {
         const long e = sg.offset + l;
+        const float g0 = from_gin ? (float)gin[e] : g[e];
+        if constexpr (from_gin) g[e] = g0;
+        if constexpr (pack) {
+          if (gout) gout[e] = (bf16)g0;
+          continue;
+        }
         float wv = w[e];
-        const float gv = g[e] * grad_scale + wd * wv;
+        const float gv = g0 * grad_scale + wd * wv;
         if (use_momentum) {
           const float a = momentum * mom[e] + gv;
           mom[e] = a;
@@ -386,7 +407,7 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
   // before it takes the ticket, so a relaxed ticket orders it -- no fence: an agent-scope
   // release/acquire writes back and invalidates the L2 per workgroup (613 of them: the
   // launch took 54 us with __threadfence + acq_rel); the last one re-arms the ticket
-  if (tid == 0) {
+  if (tid == 0 && !pack) {
     const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {
@@ -399,11 +420,17 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
 void sgd_tiles(float* master, float* grad, float* mom, const LrSchedule& s, long long* gstep,
                float momentum, float wd, float grad_scale, int use_momentum,
                const ParamSeg* segs, const OptWork* work, const int* blk_seg, int nblocks,
-               bf16* bf, float* lr_out, unsigned* ticket, hipStream_t st) {
+               bf16* bf, float* lr_out, unsigned* ticket, const bf16* gin, bf16* gout, int pack,
+               hipStream_t st) {
   if (nblocks <= 0) return;
-  hipLaunchKernelGGL(sgd_tiles_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, master, grad,
-                     mom, s, gstep, momentum, wd, grad_scale, use_momentum, segs, work, blk_seg,
-                     bf, lr_out, ticket);
+#define DTR_SGD_TILES(M)                                                                        \
+  hipLaunchKernelGGL(sgd_tiles_kernel<M>, dim3((unsigned)nblocks), dim3(256), 0, st, master, grad,  \
+                     mom, s, gstep, momentum, wd, grad_scale, use_momentum, segs, work, blk_seg, bf, \
+                     lr_out, ticket, gin, gout)
+  if (pack) DTR_SGD_TILES(1);
+  else if (gin) DTR_SGD_TILES(2);
+  else DTR_SGD_TILES(0);
+#undef DTR_SGD_TILES
   DTR_CHECK_LAUNCH();
 }
 

@@ -79,14 +79,14 @@ def _pow2ceil(x: int) -> int:
     return 1 << max(0, (int(x) - 1).bit_length())
 
 
-def opt_tile(R: int, K: int, splits: int, cslab: int, C: int, taps: int):
+def opt_tile(R: int, K: int, splits: int, cslab: int, C: int, taps: int, nosplit=(64, 64)):
     """Tile (rows tap*C+ci, output channels) of a weight in the one-launch optimizer
     (csrc/optim.hip sgd_tiles_kernel): 64 x 64 without slabs; with `splits` slabs the
     tile shrinks (columns first) until its float4 slab loads fit OPT_TILE_LOADS and,
     past 8 splits (4 thread groups of 64 float4 units), until it has <= 64 units.
     Padded slab rows (cslab != C, the stem) keep all rows in one tile."""
     if splits == 0:
-        return 64, 64
+        return nosplit
     units_max = 64 if splits > 8 else 1 << 30
     TC = min(64, _pow2ceil(K))
     if cslab != C:
@@ -308,7 +308,6 @@ class Engine:
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")
         self.opt_fused = bool(tune.get("opt_fused"))
-        self.opt_fused_layer = bool(tune.get("opt_fused_layer"))
         # why the persistent step is off ("" = on); never on a GPU shared by several ranks
         # (its grids need every CU to themselves), and the same choice on EVERY rank (the
         # two plans issue different collectives)
@@ -1018,13 +1017,16 @@ class Engine:
                 self._mark(plan, *names)
                 self._flushed.add(bi)
 
-    def _emit_allreduce(self, plan, lo: int, hi: int, side_dep: bool, on_main: bool = False):
+    def _emit_allreduce(self, plan, lo: int, hi: int, side_dep: bool, on_main: bool = False,
+                        packed: bool = False):
         """Fork the comm stream off the main stream (and, with ``side_dep``, off the
         side stream, where the bucket's split-K reduces ran) at the bucket's ready
         point and all-reduce grad[lo:hi) there (bf16 exchange: cast kernels on the
         comm stream around a bf16 all-reduce), while the compute streams continue.
         ``on_main``: on the main stream itself, no fork and no join (the persistent
-        step: nothing is left to overlap, and each event costs ~5 us between launches)."""
+        step: nothing is left to overlap, and each event costs ~5 us between launches).
+        ``packed``: grad_bf16[lo:hi) already holds the bf16 input (_emit_pack) and the
+        optimizer reads the result from it: no cast launches."""
         if on_main:
             assert not side_dep
         else:
@@ -1041,9 +1043,11 @@ class Engine:
         g = self.grad.data_ptr() + 4 * lo
         if self.grad_bf16 is not None:
             gb = self.grad_bf16.data_ptr() + 2 * lo
-            plan.cast_f32_bf16(g, gb, n)
+            if not packed:
+                plan.cast_f32_bf16(g, gb, n)
             plan.all_reduce(self.comm, gb, n, self.nat.COMM_BF16)
-            plan.cast_bf16_f32(gb, g, n)
+            if not packed:
+                plan.cast_bf16_f32(gb, g, n)
         else:
             plan.all_reduce(self.comm, g, n, self.nat.COMM_F32)
         self._n_allreduce += 1
@@ -1060,6 +1064,29 @@ class Engine:
         plan.record(ev)
         plan.use_stream(0)
         plan.wait(ev)
+
+    def _packed_gin(self) -> int:
+        """The optimizer's gradient source after a packed all-reduce: grad_bf16 (bf16
+        exchange) or grad itself (0: fp32 exchange, the pack summed the slabs into it)."""
+        return self.grad_bf16.data_ptr() if self.grad_bf16 is not None else 0
+
+    def _emit_pack(self, plan, names, stream: int = 0):
+        """The all-reduce input of `names`' gradients in ONE launch (sgd_tiles pack mode,
+        the optimizer's own slab summation): split-K slab sums and the other gradients as
+        bf16 into grad_bf16 (fp32 exchange: the slab sums into grad).  Replaces a grouped
+        reduce plus a cast launch; the optimizer then reads the all-reduced bf16 (gin)."""
+        names = [n for n in names]
+        slabs = {n: self._pending.pop(n) for n in names if n in self._pending}
+        wt, bt, nblk = self._sgd_tiles_work(slabs, names=set(names))
+        s = self.sched
+        gout = self.grad_bf16.data_ptr() if self.grad_bf16 is not None else 0
+        plan.use_stream(stream)
+        plan.sgd_tiles(self.params.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(),
+                       s.init, s.warm_steps, s.warm_from, s.warm_to, list(s.bounds),
+                       list(s.values), self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
+                       int(self.use_momentum), self.segs.data_ptr(), wt.data_ptr(), bt.data_ptr(),
+                       nblk, self.wbf.data_ptr(), 0, 0, 0, gout, 1)
+        plan.use_stream(0)
 
     def _emit_reduce(self, plan, names, stream: int | None = None):
         descs = [self._pending.pop(n) for n in names if n in self._pending]
@@ -1326,17 +1353,20 @@ class Engine:
         self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
 
-        self._emit_optimizer(plan, fused_slabs={} if self.opt_fused_layer else None)
+        self._emit_optimizer(plan)
 
-    def _sgd_tiles_work(self, slabs):
+    def _sgd_tiles_work(self, slabs, names=None, nosplit=(64, 64)):
         """The work map of the one-launch optimizer (csrc/optim.hip sgd_tiles_kernel): per
         parameter segment its slab (split-K partials still to be summed, or none: the
         gradient is in `grad`) and its first workgroup; weights with bf16 copies or slabs
-        go in tiles of their HWIO master (opt_tile), other tensors in 1024-element chunks."""
+        go in tiles of their HWIO master (opt_tile), other tensors in 1024-element chunks.
+        `names`: only those segments get workgroups (a bucket's pack launch)."""
         work = np.zeros(self.nseg, dtype=OPTW_DTYPE)
         blk = []
         gptr = self.grad.data_ptr()
         for i, (rec, name) in enumerate(zip(self.seg_arr, self.seg_names)):
+            if names is not None and name not in names:
+                continue
             d = slabs.get(name)
             taps, C, K = int(rec["kh"] * rec["kw"]), int(rec["C"]), int(rec["K"])
             tiled = d is not None or rec["bf_ohwi"] >= 0 or rec["bf_hwio"] >= 0
@@ -1348,7 +1378,7 @@ class Engine:
             tr = tc = 0
             if tiled:
                 assert taps * C * K == rec["numel"], name
-                tr, tc = opt_tile(taps * C, K, splits, cslab or C, C, taps)
+                tr, tc = opt_tile(taps * C, K, splits, cslab or C, C, taps, nosplit)
                 n = _ceil(taps * C, tr) * _ceil(K, tc)
             else:
                 n = _ceil(int(rec["numel"]), 1024)
@@ -1356,21 +1386,25 @@ class Engine:
             blk += [i] * n
         assert OPTW_DTYPE.itemsize == self.nat.opt_work_bytes()
         assert not set(slabs) - set(self.seg_names), "slab without a parameter segment"
+        assert names is None or not set(slabs) - set(names), "slab outside the packed segments"
         wt = torch.from_numpy(work.view(np.uint8).copy()).to(self.device)
         bt = torch.tensor(blk, dtype=torch.int32, device=self.device)
         self._keep += [wt, bt]
         return wt, bt, len(blk)
 
-    def _emit_optimizer(self, plan, fused_slabs=None):
+    def _emit_optimizer(self, plan, fused_slabs=None, gin=0):
         """Optimizer segment (fused SGD-momentum + wd + bf16 re-pack, global_step += 1)
         and the `cost` segment (1/2 sum v^2 of the weights).  fused_slabs (a dict, the
-        persistent step): ONE sgd_tiles launch that also sums those weights' slabs."""
+        persistent step): ONE sgd_tiles launch that also sums those weights' slabs.
+        gin: the gradient is read from that bf16 buffer (the all-reduced pack, _emit_pack)."""
         spec = self.spec
         sp = self.scalars.data_ptr()
         b2 = plan.size()
         s = self.sched
         if fused_slabs is not None:
-            wt, bt, nblk = self._sgd_tiles_work(fused_slabs)
+            # (reading the all-reduced bf16, nothing to sum: 32 x 64 tiles, twice the
+            # workgroups of 64 x 64 for a launch that is all load latency)
+            wt, bt, nblk = self._sgd_tiles_work(fused_slabs, nosplit=(32, 64) if gin else (64, 64))
             if not hasattr(self, "opt_ticket"):
                 self.opt_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
             plan.sgd_tiles(self.params.master.data_ptr(), self.grad.data_ptr(),
@@ -1378,7 +1412,7 @@ class Engine:
                            list(s.bounds), list(s.values), self.gstep.data_ptr(), self.momentum,
                            self.wd, 1.0, int(self.use_momentum), self.segs.data_ptr(),
                            wt.data_ptr(), bt.data_ptr(), nblk, self.wbf.data_ptr(), sp + 8,
-                           self.opt_ticket.data_ptr())   # + global_step += 1
+                           self.opt_ticket.data_ptr(), gin, 0, 0)   # + global_step += 1
         else:
             plan.sgd_update_pack(self.params.master.data_ptr(), self.grad.data_ptr(),
                                  self.mom.data_ptr(), self.params.n_train, s.init, s.warm_steps,
@@ -1444,7 +1478,8 @@ class Engine:
         if self.prn.overlap:
             self._emit_persist_overlap(plan, ptrs, ints, floats)
             self.seg["bwd"] = (b1, plan.size())
-            self._emit_optimizer(plan, fused_slabs={} if self.opt_fused else None)
+            self._emit_optimizer(plan, fused_slabs={} if self.opt_fused else None,
+                                 gin=self._packed_gin() if self.opt_fused else 0)
             return
         plan.prn(1, ptrs, ints, floats)
         # the head's batch folds (loss, precision, dense bias and weight gradients): one
@@ -1458,8 +1493,11 @@ class Engine:
         # summed by the optimizer launch itself (sgd_tiles).
         all_names = [n for (_, _, names) in self.buckets for n in names]
         slabs = None
+        packed = self.comm is not None and self.opt_fused
         if self.opt_fused and not self.reduce_buckets:
             slabs = {n: self._pending.pop(n) for n in all_names if n in self._pending}
+        elif packed:   # the all-reduce input in one launch, read back by the optimizer
+            self._emit_pack(plan, all_names)
         else:
             self._emit_reduce(plan, all_names)
         for bi, (lo, hi, names) in enumerate(self.buckets):
@@ -1467,12 +1505,14 @@ class Engine:
             self._flushed.add(bi)
         if self.comm is not None:
             self._emit_allreduce(plan, min(b[0] for b in self.buckets),
-                                 max(b[1] for b in self.buckets), side_dep=False, on_main=True)
+                                 max(b[1] for b in self.buckets), side_dep=False, on_main=True,
+                                 packed=packed)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
         self._join_comm(plan)
         self._t_joined = plan.timing_point("allreduce_joined")
         self.seg["bwd"] = (b1, plan.size())
-        self._emit_optimizer(plan, fused_slabs=(slabs or {}) if self.opt_fused else None)
+        self._emit_optimizer(plan, fused_slabs=(slabs or {}) if self.opt_fused else None,
+                             gin=self._packed_gin() if packed else 0)
         if slabs:
             # not part of the step: the slab sums alone, for callers that want this
             # step's gradient without the update (forward_backward)
@@ -1483,13 +1523,16 @@ class Engine:
 
     def _emit_persist_overlap(self, plan, ptrs, ints, floats):
         """World > 1: the persistent backward launch on the main stream, and on the comm
-        stream (forked before it): the head's batch folds, then per gradient bucket, in
-        the order the backward completes them (persist.bucket_ranges), a one-wave wait
-        for the bucket's line in the launch's barrier region to reach its count, the
-        bucket's grouped slab reduce, and its all-reduce -- all while the backward still
-        runs on the CUs left out of its grid.  The optimizer joins the comm stream.  The
-        stream check takes each bucket wait as ordered after the backward launch
-        (device_deps): the launch publishes the bucket's completion through that line."""
+        stream (forked before it): the head's batch folds, then per gradient bucket but the
+        last, in the order the backward completes them (persist.bucket_ranges), a one-wave
+        wait for the bucket's line in the launch's barrier region to reach its count, the
+        bucket's pack (or grouped slab reduce) and its all-reduce -- all while the backward
+        still runs on the CUs left out of its grid.  The main stream joins the comm stream
+        right after the backward (its buckets are long done by then: the event wait costs
+        no queue round trip) and packs and all-reduces the last bucket itself -- no wait
+        kernel and no join behind it.  The stream check takes each bucket wait as ordered
+        after the backward launch (device_deps): the launch publishes the bucket's
+        completion through that line."""
         from .persist import bucket_ranges
 
         fork = plan.new_event()
@@ -1501,22 +1544,32 @@ class Engine:
         bwd_op = plan.size()
         plan.prn(1, ptrs, ints, floats)        # backward: dgrad chain + weight gradients
         err = self.prn.err.data_ptr()
-        for b, (lo, hi, names) in enumerate(bucket_ranges(self)):
+        ranges = bucket_ranges(self)
+
+        def bucket(lo, hi, names, stream):
+            if self.opt_fused:
+                self._emit_pack(plan, names, stream=stream)
+            else:
+                self._emit_reduce(plan, names, stream=stream)
+            plan.use_stream(stream)
+            self._mark(plan, *names)
+            self._emit_allreduce(plan, lo, hi, side_dep=False, on_main=True, packed=self.opt_fused)
+
+        for b, (lo, hi, names) in enumerate(ranges[:-1]):
             plan.use_stream(2)                 # (_emit_reduce/_emit_allreduce end on main)
             self._device_deps[plan.size()] = bwd_op
             plan.prn_bucket_wait(self.prn_bar, b, self.prn.bucket_target(b), err)
-            self._emit_reduce(plan, names, stream=2)
-            plan.use_stream(2)
-            self._mark(plan, *names)
-            self._emit_allreduce(plan, lo, hi, side_dep=False, on_main=True)
-        for bi in range(len(self.buckets)):
-            self._flushed.add(bi)
+            bucket(lo, hi, names, 2)
         join = plan.new_event()
         plan.use_stream(2)
         plan.record(join)
         plan.use_stream(0)
         plan.wait(join)
-        self._t_bwd_done = self._t_joined = plan.timing_point("allreduce_joined")
+        self._t_bwd_done = plan.timing_point("bwd_compute_done")
+        bucket(*ranges[-1], 0)                 # the last bucket behind the backward, in order
+        for bi in range(len(self.buckets)):
+            self._flushed.add(bi)
+        self._t_joined = plan.timing_point("allreduce_joined")
 
     def forward_backward(self, st=None):
         """Forward + backward of the current batch with `grad` complete and no update

@@ -56,18 +56,14 @@ ENGINE = {
     "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (backward: 4 "
                            "up to 32 images, 2 up to 64, else 1; forward: 4 up to 32, 2 while "
                            "2N <= 3/4 of the CUs, else 1), 1, 2 or 4 for both"),
-    "persist_overlap": (1, "world > 1: the persistent step's gradient buckets (stage 3 + head, "
-                           "stage 2, stage 1 + stem) are slab-reduced and all-reduced on the comm "
-                           "stream while the backward launch still runs (16 CUs left out of its "
-                           "grid), instead of one reduce + one all-reduce after it"),
+    "persist_overlap": (1, "world > 1: the persistent step's first two stage buckets packed and "
+                           "all-reduced on the comm stream while the backward launch runs (16 "
+                           "CUs left out of its grid), the last packed and all-reduced after it "
+                           "on the main stream; 0: one pack + one all-reduce after the backward "
+                           "(profiles/cifar_comm_overlap.md)"),
     "opt_fused": (1, "the persistent step's optimizer as ONE launch (split-K slab sums on "
                      "one GPU, SGD-momentum, both bf16 weight copies: sgd_tiles) instead of "
                      "the grouped slab reduce + sgd_pack + ohwi_pack"),
-    "opt_fused_layer": (0, "the launch-per-layer plan's optimizer as ONE sgd_tiles launch too "
-                           "(SGD-momentum + both bf16 copies; its weight gradients are already "
-                           "summed) instead of sgd_pack + ohwi_pack; off: ImageNet RN50 176 us vs "
-                           "98 + 44 us (scalar 4-byte accesses over 25.5 M weights), steps within "
-                           "noise (10.54-10.59 ms either way), CIFAR per-layer 1.262 vs 1.267 ms"),
     "mat_bn_minc": (256, "... and from this many channels (ImageNet stages 3-4: +1.3 %)"),
 }
 

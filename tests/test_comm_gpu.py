@@ -37,13 +37,14 @@ def _engines(gpu, **kw):
 
 
 def _ar_expect(persist):
-    """(all-reduce ops, their stream) per plan: per-layer -- one per bucket on the comm
+    """(all-reduce ops, their streams) per plan: per-layer -- one per bucket on the comm
     stream, overlapping the backward; persistent step with persist_overlap (default) --
-    three stage buckets on the comm stream, each behind a bucket wait, overlapping the
-    backward launch; persistent step without -- ONE all-reduce on the main stream after it."""
+    the first two stage buckets on the comm stream, each behind a bucket wait, overlapping
+    the backward launch, the last on the main stream after it; persistent step without --
+    ONE all-reduce on the main stream after it."""
     if persist == "0":
-        return None, 2
-    return (3, 2) if "persist_overlap=0" not in persist else (1, 0)
+        return None, None
+    return (3, [2, 2, 0]) if "persist_overlap=0" not in persist else (1, [0])
 
 
 PERSIST_MODES = ["0", "1", "1,persist_overlap=0"]
@@ -64,9 +65,10 @@ def test_native_comm_single_rank_is_identity(gpu, monkeypatch, persist):
     assert "librccl" in info["rccl_library"]
     names = eng.plan.names()
     assert names.count("all_reduce") == info["allreduce_ops"]
-    assert names.count("prn_bucket_wait") == (3 if n_ar == 3 else 0)
+    assert names.count("prn_bucket_wait") == (2 if n_ar == 3 else 0)
     streams = eng.plan.op_streams()
-    assert all(streams[i] == want for i, n in enumerate(names) if n == "all_reduce")
+    got = [streams[i] for i, n in enumerate(names) if n == "all_reduce"]
+    assert got == want if want is not None else set(got) == {2}, got
     for _ in range(3):
         ref.step()
         eng.step()
@@ -149,10 +151,10 @@ def _loopback_engines(gpu, dtype, seed_eng=3):
 @pytest.mark.parametrize("persist", PERSIST_MODES)
 def test_loopback_doubling_standin_orders_every_bucket(gpu, monkeypatch, dtype, persist):
     """grad == 2 x the no-comm engine's grad, bitwise, plain and under jitter (per-layer
-    plan: >= 4 bucket all-reduces; persistent step: three buckets reduced and doubled on
-    the comm stream WHILE the backward launch runs -- a bucket waited for too early, or a
-    slab / BN gradient not yet visible when its bucket's count completed, leaves an element
-    that is not exactly 2x -- or one after it)."""
+    plan: >= 4 bucket all-reduces; persistent step: two buckets reduced and doubled on the
+    comm stream WHILE the backward launch runs -- a bucket waited for too early, or a slab /
+    BN gradient not yet visible when its bucket's count completed, leaves an element that
+    is not exactly 2x -- and the last one after it; or all of them after it)."""
     monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
     n_ar, _ = _ar_expect(persist)
     for trial in range(4):

@@ -102,11 +102,11 @@ def test_engine_step_within_bf16_noise_deep(gpu, spec_fn, N):
     assert cos_e >= cos_32 - 0.05
 
 
-@pytest.mark.parametrize("fused", [0, 1])
-def test_optimizer_step_and_pack(gpu, monkeypatch, fused):
+def test_optimizer_step_and_pack(gpu, monkeypatch):
     """SGD-momentum + weight decay and the bf16 weight copies, by sgd_pack + ohwi_pack
-    or (opt_fused_layer) by the one-launch sgd_tiles."""
-    monkeypatch.setenv("DTR_TUNE", f"persist=0,opt_fused_layer={fused}")
+    (the launch-per-layer plan; the persistent step's one-launch sgd_tiles:
+    test_persist_gpu.py)."""
+    monkeypatch.setenv("DTR_TUNE", "persist=0")
     spec = cifar_spec(8)
     eng, imgs, labels, _ = _make(spec, 16, gpu)
     w0 = eng.params.master.clone()
@@ -130,10 +130,11 @@ def test_optimizer_step_and_pack(gpu, monkeypatch, fused):
     torch.testing.assert_close(ohwi.float(), w.permute(3, 0, 1, 2).to(torch.bfloat16).float())
 
 
-@pytest.mark.parametrize("fused", [0, 1])
-def test_graph_replay_matches_eager(gpu, monkeypatch, fused):
-    """(fused: the optimizer's global_step ticket re-arms across graph replays)"""
-    monkeypatch.setenv("DTR_TUNE", f"persist=0,opt_fused_layer={fused}")
+@pytest.mark.parametrize("persist", [0, 1])
+def test_graph_replay_matches_eager(gpu, monkeypatch, persist):
+    """(persist: the persistent step, whose one-launch optimizer's global_step ticket
+    re-arms across graph replays)"""
+    monkeypatch.setenv("DTR_TUNE", f"persist={persist}")
     spec = cifar_spec(8)
     e1, imgs, labels, _ = _make(spec, 16, gpu)
     e2 = Engine(spec, 16, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=gpu,
