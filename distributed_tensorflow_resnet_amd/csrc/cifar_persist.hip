@@ -260,7 +260,7 @@ __device__ __forceinline__ bool grid_wait(unsigned* base, int off, unsigned k, u
   unsigned* bar = base + off;
   if ((int)threadIdx.x < shards) {
     const unsigned sh = threadIdx.x;
-    const unsigned target = k * ((nsl + shards - 1 - sh) / shards);
+    const unsigned target = k * ((nsl + shards - 1 - sh) >> __builtin_ctz(shards));   // (1 or 8)
     const unsigned* p = bar + sh * PRN_LINE;
     const long long t0 = wall_clock64();
     int ok = 1;
@@ -308,7 +308,16 @@ struct WLoad {
   const bf16* src;
   int rows, K, KP;      // LDS rows x K (padded row KP; columns [K, KP - 8) zero)
   int dgrad, cin, cout; // dgrad: rows = ci of HWIO [tap][ci][co], k = tap * cout + co
+  // unit u -> (row, 16-B column j) without integer division (the shapes are runtime
+  // values -- the next block's -- and a 32-bit division by one is ~20 VALU per unit,
+  // ~40 % of the forward's VALU): row = (u + 1/2) x (8 / K) in fp32 (exact: u < 2^13 and
+  // the quotient's fraction is >= 1/144 away from an integer); cout / 8 is a power of 2
+  float inv_upr;
+  int cu_shift;
 };
+__device__ __forceinline__ int wl_row(const WLoad& L, int u) {
+  return (int)(((float)u + 0.5f) * L.inv_upr);
+}
 
 // (the thread id is taken opaque in both: otherwise each stage loop hoists the per-thread
 // addresses of every weight unit out of its loop and keeps them live across the blocks --
@@ -322,11 +331,11 @@ __device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
   for (int i = 0; i < NR; ++i) {
     const int u = t + i * (PT - 64);
     if (u < units) {
-      const int row = u / upr, j = u - row * upr;
+      const int row = wl_row(L, u), j = u - row * upr;
       long off;
       if (L.dgrad) {
-        const int cu = L.cout / 8, tap = j / cu;
-        off = ((long)tap * L.cin + row) * L.cout + (j - tap * cu) * 8;
+        const int tap = j >> L.cu_shift;
+        off = ((long)tap * L.cin + row) * L.cout + (j - (tap << L.cu_shift)) * 8;
       } else {
         off = (long)row * L.K + j * 8;
       }
@@ -345,14 +354,14 @@ __device__ __forceinline__ void w_store(const WLoad& L, const bf16x8 (&r)[NR], b
     for (int i = 0; i < NR; ++i) {
       const int u = t + i * (PT - 64);
       if (u < units) {
-        const int row = u / upr, j = u - row * upr;
+        const int row = wl_row(L, u), j = u - row * upr;
         *reinterpret_cast<bf16x8*>(wl + row * L.KP + j * 8) = r[i];
       }
     }
   }
-  const int pad = (L.KP - 8 - L.K) / 8;   // zero columns up to the last k-step
+  const int pad = (L.KP - 8 - L.K) / 8;   // zero columns up to the last k-step (0-3)
   for (int q = tid; q < L.rows * pad; q += PT) {
-    const int row = q / pad, j = upr + (q - row * pad);
+    const int row = pad == 1 ? q : pad == 2 ? q >> 1 : q / pad, j = upr + (q - row * pad);
     *reinterpret_cast<bf16x8*>(wl + row * L.KP + j * 8) = bf16x8{};
   }
 }
@@ -365,10 +374,12 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int kpad_of(int K) { return ((K + 31) / 32) * 32 + 8; }
 
 __device__ __forceinline__ WLoad wl_fwd(const bf16* src, int co, int ci, int ks) {
-  return WLoad{src, co, ks * ks * ci, kpad_of(ks * ks * ci), 0, ci, co};
+  const int K = ks * ks * ci;
+  return WLoad{src, co, K, kpad_of(K), 0, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8)};
 }
 __device__ __forceinline__ WLoad wl_dgrad(const bf16* src, int co, int ci, int ks) {
-  return WLoad{src, ci, ks * ks * co, kpad_of(ks * ks * co), 1, ci, co};
+  const int K = ks * ks * co;
+  return WLoad{src, ci, K, kpad_of(K), 1, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8)};
 }
 
 // ---- convolutions on the LDS halo ------------------------------------------------------
