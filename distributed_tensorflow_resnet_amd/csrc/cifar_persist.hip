@@ -313,7 +313,7 @@ struct WLoad {
   // ~40 % of the forward's VALU): row = (u + 1/2) x (8 / K) in fp32 (exact: u < 2^13 and
   // the quotient's fraction is >= 1/144 away from an integer); cout / 8 is a power of 2
   float inv_upr;
-  int cu_shift;
+  int cu_shift, ci_shift;   // log2(cout / 8), log2(cin): the dgrad's HWIO offsets as shifts
 };
 __device__ __forceinline__ int wl_row(const WLoad& L, int u) {
   return (int)(((float)u + 0.5f) * L.inv_upr);
@@ -331,13 +331,13 @@ __device__ __forceinline__ void w_prefetch(const WLoad& L, bf16x8 (&r)[NR]) {
   for (int i = 0; i < NR; ++i) {
     const int u = t + i * (PT - 64);
     if (u < units) {
-      const int row = wl_row(L, u), j = u - row * upr;
-      long off;
-      if (L.dgrad) {
+      int off;   // (< 2^31: weights of <= 64 x 576)
+      if (L.dgrad) {   // HWIO [tap][ci = row][co]: ((tap * cin + row) * cout + co
+        const int row = wl_row(L, u), j = u - __umul24(row, upr);
         const int tap = j >> L.cu_shift;
-        off = ((long)tap * L.cin + row) * L.cout + (j - (tap << L.cu_shift)) * 8;
-      } else {
-        off = (long)row * L.K + j * 8;
+        off = ((((tap << L.ci_shift) + row) << L.cu_shift) + (j - (tap << L.cu_shift))) * 8;
+      } else {         // rows of K contiguous: unit u is at u x 8
+        off = u * 8;
       }
       r[i] = ldg(reinterpret_cast<const bf16x8*>(L.src + off));
     }
@@ -353,9 +353,9 @@ __device__ __forceinline__ void w_store(const WLoad& L, const bf16x8 (&r)[NR], b
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int u = t + i * (PT - 64);
-      if (u < units) {
-        const int row = wl_row(L, u), j = u - row * upr;
-        *reinterpret_cast<bf16x8*>(wl + row * L.KP + j * 8) = r[i];
+      if (u < units) {   // row * KP + j * 8 = u * 8 + row * (KP - K)
+        const int row = wl_row(L, u);
+        *reinterpret_cast<bf16x8*>(wl + u * 8 + __umul24(row, L.KP - L.K)) = r[i];
       }
     }
   }
@@ -375,11 +375,13 @@ __host__ __device__ constexpr int kpad_of(int K) { return ((K + 31) / 32) * 32 +
 
 __device__ __forceinline__ WLoad wl_fwd(const bf16* src, int co, int ci, int ks) {
   const int K = ks * ks * ci;
-  return WLoad{src, co, K, kpad_of(K), 0, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8)};
+  return WLoad{src, co, K, kpad_of(K), 0, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8),
+               __builtin_ctz(ci)};
 }
 __device__ __forceinline__ WLoad wl_dgrad(const bf16* src, int co, int ci, int ks) {
   const int K = ks * ks * co;
-  return WLoad{src, ci, K, kpad_of(K), 1, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8)};
+  return WLoad{src, ci, K, kpad_of(K), 1, ci, co, __frcp_rn((float)(K / 8)), __builtin_ctz(co / 8),
+               __builtin_ctz(ci)};
 }
 
 // ---- convolutions on the LDS halo ------------------------------------------------------
