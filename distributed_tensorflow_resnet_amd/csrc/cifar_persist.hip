@@ -426,7 +426,7 @@ __device__ __forceinline__ void conv_acc(f32x4 (&acc)[8], const bf16* hal, const
   }
   int cb0, pb0;
   tile_of<SO, P>(wave, 0, pb0, cb0);
-#pragma unroll 2
+#pragma unroll
   for (int ks = kh; ks < KS; ks += WPT) {
     const int k = ks * 32 + fq * 8;
     int tap = k / CI;
