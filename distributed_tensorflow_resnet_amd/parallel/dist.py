@@ -155,11 +155,19 @@ def gpu_shared_by_ranks(ctx=None, device_index: int | None = None) -> bool:
     forever.  Decided from the devices' physical identities (device_identity) exchanged
     through the c10d store, not from rank / device counts: launchers that hand every
     rank one GPU by visible-device masks see one device per process."""
-    if ctx is None or not getattr(ctx, "active", False) or torch.cuda.device_count() == 0:
+    if torch.cuda.device_count() == 0:
+        return False
+    if ctx is not None and getattr(ctx, "active", False):
+        rank, world = ctx.rank, ctx.world_size
+    elif dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        # an engine built without a context (a single-process reference beside the
+        # distributed one, as the DP rehearsals build) shares the device all the same
+        rank, world = dist.get_rank(), dist.get_world_size()
+    else:
         return False
     idx = torch.cuda.current_device() if device_index is None else device_index
     store = dist.distributed_c10d._get_default_store()
-    return ranks_on_device(store, ctx.rank, ctx.world_size, device_identity(idx)) > 1
+    return ranks_on_device(store, rank, world, device_identity(idx)) > 1
 
 
 class DistContext:

@@ -1,0 +1,5 @@
+#!/bin/bash
+# In-kernel phase probe of the persistent step at bs128 and bs16 (round 5, final kernels).
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+set -o pipefail
+timeout -k 10 200 python scripts/prn_probe.py 128 > gpurun_out/r5_probe128b.txt 2>&1 && timeout -k 10 200 python scripts/prn_probe.py 16 > gpurun_out/r5_probe16b.txt 2>&1 && echo done
