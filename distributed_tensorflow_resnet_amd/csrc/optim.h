@@ -34,7 +34,8 @@ struct OptWork {
   int tr, tc;              // tile rows / columns (<= 64 each)
 };
 // blk_seg[b] = the segment of workgroup b; ticket: a zero-initialised int the last
-// workgroup resets after its global_step += 1 (every workgroup has read the step).
+// workgroup resets after its global_step += 1 (every workgroup has read the step); null:
+// no global_step increment (a launch updating part of the parameters ahead of the last).
 // gin (no slabs): the gradient read as bf16 from gin (the bf16 all-reduce's result; the
 // fp32 grad is written from it).  pack: no update -- the gradient (slab sums or grad) is
 // only written out, as bf16 to gout (or, gout null, as fp32 to grad): the all-reduce's

@@ -407,7 +407,7 @@ sgd_tiles_kernel(float* __restrict__ w, float* __restrict__ g, float* __restrict
   // before it takes the ticket, so a relaxed ticket orders it -- no fence: an agent-scope
   // release/acquire writes back and invalidates the L2 per workgroup (613 of them: the
   // launch took 54 us with __threadfence + acq_rel); the last one re-arms the ticket
-  if (tid == 0 && !pack) {
+  if (tid == 0 && !pack && ticket != nullptr) {   // (null: an early bucket's update, no step)
     const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {

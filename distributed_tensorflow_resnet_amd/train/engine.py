@@ -1392,16 +1392,37 @@ class Engine:
         self._keep += [wt, bt]
         return wt, bt, len(blk)
 
-    def _emit_optimizer(self, plan, fused_slabs=None, gin=0):
+    def _emit_update(self, plan, names, gin=0, step=True):
+        """ONE sgd_tiles launch updating the segments `names` (no slabs: the gradient is in
+        grad, or the all-reduced bf16 `gin`); step: it also does global_step += 1 (the
+        step's last update launch)."""
+        s = self.sched
+        # (reading the all-reduced bf16, nothing to sum: 32 x 64 tiles, twice the
+        # workgroups of 64 x 64 for a launch that is all load latency)
+        wt, bt, nblk = self._sgd_tiles_work({}, names=names, nosplit=(32, 64) if gin else (64, 64))
+        if not hasattr(self, "opt_ticket"):
+            self.opt_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+        plan.sgd_tiles(self.params.master.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(),
+                       s.init, s.warm_steps, s.warm_from, s.warm_to, list(s.bounds),
+                       list(s.values), self.gstep.data_ptr(), self.momentum, self.wd, 1.0,
+                       int(self.use_momentum), self.segs.data_ptr(), wt.data_ptr(), bt.data_ptr(),
+                       nblk, self.wbf.data_ptr(), self.scalars.data_ptr() + 8,
+                       self.opt_ticket.data_ptr() if step else 0, gin, 0, 0)
+
+    def _emit_optimizer(self, plan, fused_slabs=None, gin=0, names=None):
         """Optimizer segment (fused SGD-momentum + wd + bf16 re-pack, global_step += 1)
         and the `cost` segment (1/2 sum v^2 of the weights).  fused_slabs (a dict, the
         persistent step): ONE sgd_tiles launch that also sums those weights' slabs.
-        gin: the gradient is read from that bf16 buffer (the all-reduced pack, _emit_pack)."""
+        gin: the gradient is read from that bf16 buffer (the all-reduced pack, _emit_pack).
+        names: only those segments (the rest were updated ahead, _emit_update)."""
         spec = self.spec
         sp = self.scalars.data_ptr()
         b2 = plan.size()
         s = self.sched
-        if fused_slabs is not None:
+        if names is not None:
+            assert not fused_slabs
+            self._emit_update(plan, names, gin)
+        elif fused_slabs is not None:
             # (reading the all-reduced bf16, nothing to sum: 32 x 64 tiles, twice the
             # workgroups of 64 x 64 for a launch that is all load latency)
             wt, bt, nblk = self._sgd_tiles_work(fused_slabs, nosplit=(32, 64) if gin else (64, 64))
@@ -1476,10 +1497,13 @@ class Engine:
         self._reduce_main = True   # the slab reduces run on the main stream
         self._produced.add(self.dense_name)
         if self.prn.overlap:
-            self._emit_persist_overlap(plan, ptrs, ints, floats)
+            early = self._emit_persist_overlap(plan, ptrs, ints, floats)
             self.seg["bwd"] = (b1, plan.size())
-            self._emit_optimizer(plan, fused_slabs={} if self.opt_fused else None,
-                                 gin=self._packed_gin() if self.opt_fused else 0)
+            if self.opt_fused:   # the rest: the last bucket's segments
+                self._emit_optimizer(plan, fused_slabs={}, gin=self._packed_gin(),
+                                     names={n for n in self.seg_names if n not in early})
+            else:
+                self._emit_optimizer(plan)
             return
         plan.prn(1, ptrs, ints, floats)
         # the head's batch folds (loss, precision, dense bias and weight gradients): one
@@ -1526,13 +1550,13 @@ class Engine:
         stream (forked before it): the head's batch folds, then per gradient bucket but the
         last, in the order the backward completes them (persist.bucket_ranges), a one-wave
         wait for the bucket's line in the launch's barrier region to reach its count, the
-        bucket's pack (or grouped slab reduce) and its all-reduce -- all while the backward
-        still runs on the CUs left out of its grid.  The main stream joins the comm stream
-        right after the backward (its buckets are long done by then: the event wait costs
-        no queue round trip) and packs and all-reduces the last bucket itself -- no wait
-        kernel and no join behind it.  The stream check takes each bucket wait as ordered
-        after the backward launch (device_deps): the launch publishes the bucket's
-        completion through that line."""
+        bucket's pack (or grouped slab reduce), its all-reduce and (opt_fused) the update of
+        its parameters -- all while the backward still runs on the CUs left out of its
+        grid.  The main stream joins the comm stream right after the backward (its buckets
+        are long done by then) and packs, all-reduces and updates the last bucket itself.
+        The stream check takes each bucket wait as ordered after the backward launch
+        (device_deps): the launch publishes the bucket's completion through that line.
+        Returns the segment names updated on the comm stream."""
         from .persist import bucket_ranges
 
         fork = plan.new_event()
@@ -1555,11 +1579,21 @@ class Engine:
             self._mark(plan, *names)
             self._emit_allreduce(plan, lo, hi, side_dep=False, on_main=True, packed=self.opt_fused)
 
+        early = set()
         for b, (lo, hi, names) in enumerate(ranges[:-1]):
             plan.use_stream(2)                 # (_emit_reduce/_emit_allreduce end on main)
             self._device_deps[plan.size()] = bwd_op
             plan.prn_bucket_wait(self.prn_bar, b, self.prn.bucket_target(b), err)
             bucket(lo, hi, names, 2)
+            if self.opt_fused:
+                # the bucket's parameters updated right behind its all-reduce, still beside
+                # the backward: it has finished with them (their stage's dgrads and BN
+                # backwards precede the count that released this bucket); global_step is
+                # stepped by the last update launch
+                plan.use_stream(2)
+                self._emit_update(plan, set(names), self._packed_gin(), step=False)
+                plan.use_stream(0)
+                early |= set(names)
         join = plan.new_event()
         plan.use_stream(2)
         plan.record(join)
@@ -1570,6 +1604,7 @@ class Engine:
         for bi in range(len(self.buckets)):
             self._flushed.add(bi)
         self._t_joined = plan.timing_point("allreduce_joined")
+        return early
 
     def forward_backward(self, st=None):
         """Forward + backward of the current batch with `grad` complete and no update

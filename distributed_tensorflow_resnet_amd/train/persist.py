@@ -38,8 +38,12 @@ PRN_BLOCK = np.dtype([(k, "<u8") for k in ("x", "h1", "out", "w1f", "w2f", "wpf"
 PRN_ITEM = np.dtype([(k, "<u8") for k in ("dy", "x", "scale", "shift", "part")] +
                     [(k, "<i4") for k in ("kind", "img0", "nimg", "ready", "bucket", "pad_")])
 # overlap mode (world > 1): CUs left out of the backward grid for the comm stream's bucket
-# waits, slab reduces and RCCL all-reduces, which run while the backward does
-OVERLAP_RESERVE_CUS = 16
+# waits, packs, RCCL all-reduces and early updates, which run while the backward does (no
+# comm-stream kernel fits beside a backward workgroup: each holds a CU's LDS and VGPRs).
+# 16 left the stage-3 bucket's pack at 165 us and pushed the chain past the backward's
+# end; 48 keeps it inside (world-1 step within 0-7 us of the exchange-after-backward
+# plan at bs16-64; 64 / 96 no better: profiles/cifar_comm_overlap.md)
+OVERLAP_RESERVE_CUS = 48
 # all-reduce buckets of the overlap mode, in the order the backward completes them:
 # stage 2 (64 channels) + the final BN + dense, stage 1, stage 0 + the stem
 BUCKET_OF_STAGE = (2, 1, 0)
