@@ -56,10 +56,10 @@ ENGINE = {
     "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (backward: 4 "
                            "up to 32 images, 2 up to 64, else 1; forward: 4 up to 32, 2 while "
                            "2N <= 3/4 of the CUs, else 1), 1, 2 or 4 for both"),
-    "persist_overlap": (1, "world > 1: the persistent step's first two stage buckets packed and "
-                           "all-reduced on the comm stream while the backward launch runs (16 "
-                           "CUs left out of its grid), the last packed and all-reduced after it "
-                           "on the main stream; 0: one pack + one all-reduce after the backward "
+    "persist_overlap": (1, "world > 1: the persistent step's first two stage buckets packed, "
+                           "all-reduced and updated on the comm stream while the backward launch "
+                           "runs (48 CUs left out of its grid), the last after it on the main "
+                           "stream; 0: one pack + one all-reduce + one update after the backward "
                            "(profiles/cifar_comm_overlap.md)"),
     "opt_fused": (1, "the persistent step's optimizer as ONE launch (split-K slab sums on "
                      "one GPU, SGD-momentum, both bf16 weight copies: sgd_tiles) instead of "
