@@ -42,8 +42,8 @@
 constexpr long long kSpinTicks = 200000000;   // 2 s at 100 MHz
 constexpr int C = 64;
 
-enum Mode { FLAT = 0, SHARD8 = 1, FLAT4W = 2, SHARD4W = 3, NMODES = 4 };
-static const char* kNames[NMODES] = {"flat", "shard8", "flat4w", "shard4w"};
+enum Mode { FLAT = 0, SHARD8 = 1, FLAT4W = 2, SHARD4W = 3, SHARD8P2 = 4, SHARD8P4 = 5, SHARD8S4 = 6, SHARD8S16 = 7, SHARD16 = 8, NMODES = 9 };
+static const char* kNames[NMODES] = {"flat", "shard8", "flat4w", "shard4w", "shard8 2-in-flight", "shard8 4-in-flight", "shard8 sleep 4", "shard8 sleep 16", "shard16"};
 
 struct Ctl {
   unsigned cnt[16][32];   // 16 counter lines (flat uses line 0; shards lines 0-7)
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(512, 1) bn_barrier_kernel(Ctl* c, int iters, i
   __shared__ double tbl[2 * C];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int G = gridDim.x;
-  const int shard = blockIdx.x % 8;
+  const int shard = blockIdx.x % (MODE == SHARD16 ? 16 : 8);
   // per-shard arrival counts (shard s: blocks b with b % 8 == s)
   float x = (float)tid;
   bool ok = true;
@@ -86,16 +86,48 @@ __global__ void __launch_bounds__(512, 1) bn_barrier_kernel(Ctl* c, int iters, i
     __syncthreads();
     // ---- arrive ----
     if (tid == 0) {
-      unsigned* ctr = (MODE == SHARD8 || MODE == SHARD4W) ? &c->cnt[shard][0] : &c->cnt[0][0];
+      unsigned* ctr = (MODE == FLAT || MODE == FLAT4W) ? &c->cnt[0][0] : &c->cnt[shard][0];
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- wait ----
     const int pollers = (MODE == FLAT4W || MODE == SHARD4W) ? 4 : 1;
-    if (wave < pollers) {
-      const bool sh = MODE == SHARD8 || MODE == SHARD4W;
-      const int lanes = sh ? 8 : 1;
+    if (MODE == SHARD8P2 || MODE == SHARD8P4) {
+      // one wave, lanes 0-7, NP polls in flight: each check waits for the oldest load only
+      constexpr int NP = MODE == SHARD8P2 ? 2 : 4;
+      if (tid < 8) {
+        const unsigned target = (unsigned)it * (unsigned)((G - tid + 7) / 8);
+        const unsigned* ctr = &c->cnt[tid][0];
+        const long long t0 = wall_clock64();
+        unsigned v[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+          v[j] = ld_agent(ctr);
+          if (j + 1 < NP) __builtin_amdgcn_s_sleep(2);
+        }
+        bool fin = false;
+        while (!fin) {
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            const bool done = v[j] >= target;
+            if (__builtin_amdgcn_ballot_w64(!done) == 0) {
+              fin = true;
+              break;
+            }
+            v[j] = ld_agent(ctr);   // re-issue in this slot (the others are still in flight)
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (!fin && wall_clock64() - t0 > kSpinTicks) {
+            if (tid == 0) flag[1] = 1;
+            break;
+          }
+        }
+      }
+    } else if (wave < pollers) {
+      const bool sh = MODE != FLAT && MODE != FLAT4W;
+      const int lanes = MODE == SHARD16 ? 16 : sh ? 8 : 1;
       if (lane < lanes) {
-        const unsigned per = sh ? (unsigned)((G - lane + 7) / 8) : (unsigned)G;
+        const unsigned per = MODE == SHARD16 ? (unsigned)((G - lane + 15) / 16)
+                             : sh ? (unsigned)((G - lane + 7) / 8) : (unsigned)G;
         const unsigned target = per * (unsigned)it;
         const unsigned* ctr = &c->cnt[sh ? lane : 0][0];
         const long long t0 = wall_clock64();
@@ -111,7 +143,9 @@ __global__ void __launch_bounds__(512, 1) bn_barrier_kernel(Ctl* c, int iters, i
           if (pollers > 1 &&
               __hip_atomic_load(&flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
             break;
-          __builtin_amdgcn_s_sleep(1);
+          if (MODE == SHARD8S4) __builtin_amdgcn_s_sleep(4);
+          else if (MODE == SHARD8S16) __builtin_amdgcn_s_sleep(16);
+          else __builtin_amdgcn_s_sleep(1);
           if (wall_clock64() - t0 > kSpinTicks) {
             __hip_atomic_fetch_add(&c->fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) __hip_atomic_store(&flag[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -203,17 +237,16 @@ int main() {
       for (int rep : {4, 8}) {
         bool bad = false;
         float r[NMODES];
-        if (rep == 4) {
-          r[0] = per_barrier<FLAT, 4>(c, G, work, 1, &bad);
-          r[1] = per_barrier<SHARD8, 4>(c, G, work, 1, &bad);
-          r[2] = per_barrier<FLAT4W, 4>(c, G, work, 1, &bad);
-          r[3] = per_barrier<SHARD4W, 4>(c, G, work, 1, &bad);
-        } else {
-          r[0] = per_barrier<FLAT, 8>(c, G, work, 1, &bad);
-          r[1] = per_barrier<SHARD8, 8>(c, G, work, 1, &bad);
-          r[2] = per_barrier<FLAT4W, 8>(c, G, work, 1, &bad);
-          r[3] = per_barrier<SHARD4W, 8>(c, G, work, 1, &bad);
-        }
+        if (rep != 4) continue;
+        r[0] = per_barrier<FLAT, 4>(c, G, work, 1, &bad);
+        r[1] = per_barrier<SHARD8, 4>(c, G, work, 1, &bad);
+        r[2] = per_barrier<FLAT4W, 4>(c, G, work, 1, &bad);
+        r[3] = per_barrier<SHARD4W, 4>(c, G, work, 1, &bad);
+        r[4] = per_barrier<SHARD8P2, 4>(c, G, work, 1, &bad);
+        r[5] = per_barrier<SHARD8P4, 4>(c, G, work, 1, &bad);
+        r[6] = per_barrier<SHARD8S4, 4>(c, G, work, 1, &bad);
+        r[7] = per_barrier<SHARD8S16, 4>(c, G, work, 1, &bad);
+        r[8] = per_barrier<SHARD16, 4>(c, G, work, 1, &bad);
         std::printf("| %d | %d | %d |", G, work, rep);
         for (int m = 0; m < NMODES; ++m) std::printf(" %.2f |", r[m]);
         std::printf("%s\n", bad ? " FAIL (timed-out barrier)" : "");
