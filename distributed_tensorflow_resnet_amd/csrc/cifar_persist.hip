@@ -609,6 +609,18 @@ __device__ __forceinline__ void to_halo(bf16* hal, const bf16x4 (&v)[8], const f
   lane = opaque_v(lane);
   const int fr = lane & 15, fq = lane >> 4;
   if (wave_active<S, P>(wave)) {
+    // (MODE 1) this lane's 4 channels of each of the wave's channel blocks, read once: the
+    // halo stores below may alias the table for the compiler, which re-read it per tile
+    f32x4 scv[G::CBW], shv[G::CBW];
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int j = 0; j < G::CBW; ++j) {
+        int pb, cb;
+        tile_of<S, P>(wave, j, pb, cb);
+        scv[j] = *reinterpret_cast<const f32x4*>(sc + cb * 16 + 4 * fq);
+        shv[j] = *reinterpret_cast<const f32x4*>(sh + cb * 16 + 4 * fq);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < G::TPW; ++t) {
       int pb, cb, h, w;
@@ -618,7 +630,8 @@ __device__ __forceinline__ void to_halo(bf16* hal, const bf16x4 (&v)[8], const f
       bf16x4 o = v[t];
       if constexpr (MODE == 1) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)fmaxf((float)v[t][r] * sc[c0 + r] + sh[c0 + r], 0.f);
+        for (int r = 0; r < 4; ++r)
+          o[r] = (bf16)fmaxf((float)v[t][r] * scv[t % G::CBW][r] + shv[t % G::CBW][r], 0.f);
       }
       const int lr = h - kslice * G::RS + 1;
       *reinterpret_cast<bf16x4*>(hal + haddr<G::U>(lr * G::W2 + w + 1, w + 1, c0)) = o;
@@ -768,7 +781,8 @@ __device__ __forceinline__ void bn_prefetch_bwd(const PrnBn& bn, int C, BnRegs& 
 }
 
 // the forward table (scale, shift, mean, rstd) of a BN the forward launch finalized,
-// into registers before a wait / from registers into LDS [4][64]
+// into registers before a wait / from registers into LDS [4][64] as (scale, shift,
+// -mean*rstd, rstd): the backward's xhat = x*rstd + (-mean*rstd), one fma
 __device__ __forceinline__ void bn_prefetch_tab(const PrnBn& bn, int C, BnRegs& r) {
   const int c = threadIdx.x;
   if (c < C) {
@@ -783,7 +797,7 @@ __device__ __forceinline__ void tab_store(const BnRegs& r, int C, float* tbl) {
   if (c < C) {
     tbl[c] = r.scale;
     tbl[64 + c] = r.shift;
-    tbl[128 + c] = r.mean;
+    tbl[128 + c] = -r.mean * r.rstd;
     tbl[192 + c] = r.rstd;
   }
 }
@@ -824,8 +838,9 @@ __device__ __forceinline__ void bn_fwd_table(const PrnBn& bn, const BnRegs& pr, 
   __syncthreads();
 }
 
-// backward BN: sums (sum g, sum g*xhat) -> coefficient table [a, b, c, mean, rstd, scale,
-// shift] x 64 (dh = a g - b - c xhat, bn_bwd_apply's formula); workgroup 0 writes
+// backward BN: sums (sum g, sum g*xhat) -> coefficient table [a, k0, k1, scale, shift] x 64
+// with dh = a g - b - c xhat (bn_bwd_apply's formula) refactored as a g + k0 + k1 x:
+// k1 = -c rstd, k0 = c mean rstd - b (two fmas per element); workgroup 0 writes
 // dgamma / dbeta.  Ends with a barrier.
 __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, int C, float M,
                                              float* tbl) {
@@ -835,13 +850,12 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, 
     acc_read(bn.bacc, C, c, d1, d2);
     const float sg = (float)d1, sgx = (float)d2;
     const float a = pr.g * pr.rstd;
+    const float b = a * sg / M, cc = a * sgx / M;
     tbl[c] = a;
-    tbl[64 + c] = a * sg / M;
-    tbl[128 + c] = a * sgx / M;
-    tbl[192 + c] = pr.mean;
-    tbl[256 + c] = pr.rstd;
-    tbl[320 + c] = pr.scale;
-    tbl[384 + c] = pr.shift;
+    tbl[64 + c] = cc * pr.mean * pr.rstd - b;
+    tbl[128 + c] = -cc * pr.rstd;
+    tbl[192 + c] = pr.scale;
+    tbl[256 + c] = pr.shift;
     if (blockIdx.x == 0) {   // (write-through: the overlap mode's comm stream reads them
       st_sc1_f32(bn.dbeta + c, sg);   //  while this launch still runs)
       st_sc1_f32(bn.dgamma + c, sgx);
@@ -854,24 +868,27 @@ __device__ __forceinline__ void bn_bwd_table(const PrnBn& bn, const BnRegs& pr, 
 __device__ __forceinline__ void bn_load_table(const PrnBn& bn, int C, float* tbl) {
   const int c = threadIdx.x;
   if (c < C) {
+    const float rs = ldg(bn.rstd + c);
     tbl[c] = ldg(bn.scale + c);
     tbl[64 + c] = ldg(bn.shift + c);
-    tbl[128 + c] = ldg(bn.mean + c);
-    tbl[192 + c] = ldg(bn.rstd + c);
+    tbl[128 + c] = -ldg(bn.mean + c) * rs;   // (tab_store's layout)
+    tbl[192 + c] = rs;
   }
 }
 
-// 8 values of the BN-backward output a g - b - c xhat (+ add), g = da [x*scale+shift > 0]
+// one value of the BN-backward output a g + k0 + k1 x, g = da [x*scale+shift > 0]
+// (bn_bwd_table's coefficients cf)
+__device__ __forceinline__ float bwd1(float da, float xf, const float* cf, int c) {
+  const float gg = fmaf(xf, cf[192 + c], cf[256 + c]) > 0.f ? da : 0.f;
+  return fmaf(cf[128 + c], xf, fmaf(cf[c], gg, cf[64 + c]));
+}
+// 8 values (+ add)
 __device__ __forceinline__ bf16x8 bwd8(bf16x8 da, bf16x8 x, bf16x8 add, bool has_add,
                                        const float* cf, int c0) {
   bf16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    const float xf = (float)x[j];
-    const float gg = (xf * cf[320 + c] + cf[384 + c] > 0.f) ? (float)da[j] : 0.f;
-    const float xh = (xf - cf[192 + c]) * cf[256 + c];
-    float r = cf[c] * gg - cf[64 + c] - cf[128 + c] * xh;
+    float r = bwd1((float)da[j], (float)x[j], cf, c0 + j);
     if (has_add) r += (float)add[j];
     o[j] = (bf16)r;
   }
@@ -1314,7 +1331,7 @@ __device__ __forceinline__ void bwd_sums(Ctx& x, const bf16x4 (&da)[8], const bf
     const float xf = (float)xs[t][r];
     const float gg = (xf * tb[c] + tb[64 + c] > 0.f) ? (float)da[t][r] : 0.f;
     s1 = gg;
-    s2 = gg * (xf - tb[128 + c]) * tb[192 + c];
+    s2 = gg * fmaf(xf, tb[192 + c], tb[128 + c]);   // (tb[128] = -mean * rstd)
   }, x.m.red, ld_const(x.a->bns + (bi)).bacc, wave, lane);
 }
 
@@ -1332,10 +1349,7 @@ __device__ __forceinline__ void bwd_apply(bf16x4 (&out)[8], const bf16x4 (&da)[8
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = cb * 16 + 4 * (lane >> 4) + r;
-      const float xf = (float)xs[t][r];
-      const float gg = (xf * cf[320 + c] + cf[384 + c] > 0.f) ? (float)da[t][r] : 0.f;
-      const float xh = (xf - cf[192 + c]) * cf[256 + c];
-      float o = cf[c] * gg - cf[64 + c] - cf[128 + c] * xh;
+      float o = bwd1((float)da[t][r], (float)xs[t][r], cf, c);
       if (ADD) o += (float)add[t][r];
       out[t][r] = (bf16)o;
     }
