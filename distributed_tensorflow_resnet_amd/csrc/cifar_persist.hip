@@ -109,8 +109,12 @@ __device__ __forceinline__ bool wave_active(int wave) {
 // LDS halo element offset: local pixel `pix` (row-major in the HR x W2 slice halo,
 // column lc), channel c (multiple of 4) of a U-unit (8 channels per 16-B unit) image;
 // units XOR-swizzled by the column so a fragment's 16 pixel lanes spread over banks
+// (Not on the 32x32 map, U = 2: its fragments are parity-class-major, so their 16 lanes
+// share the column parity and the swizzle bit -- it moved no lane to another bank, and
+// without it a halo read is one add on a per-pixel-block base instead of five VALU ops.)
 template <int U>
 __device__ __forceinline__ int haddr(int pix, int lc, int c) {
+  if constexpr (U == 2) return pix * 16 + c;
   return (pix * U + ((c >> 3) ^ (lc & (U - 1)))) * 8 + (c & 7);
 }
 
