@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: no halo swizzle on the 16x16 map either -- pins, then the previous build
+# Round 5: 32-bit-offset buffer loads -- pins, then the previous build
 # (ab_old/) vs this one, same box, alternating runs; then the LDS conflict counter.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail
