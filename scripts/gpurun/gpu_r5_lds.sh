@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: 32-bit-offset buffer loads -- pins, then the previous build
+# Round 5: early weight prefetch, wave-0 drains at P=1 -- pins, then the previous build
 # (ab_old/) vs this one, same box, alternating runs; then the LDS conflict counter.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail

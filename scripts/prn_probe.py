@@ -14,12 +14,13 @@ from distributed_tensorflow_resnet_amd.models.spec import cifar_spec  # noqa: E4
 from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule  # noqa: E402
 
 NAMES = {
-    "fwd": {0: "start", 99: "prev block: tail", 2: "BN1 combine+halo+sync", 3: "conv1", 4: "publish+stats", 5: "arrive",
+    "fwd": {0: "start", 99: "prev block: tail", 1: "BN1 table+halo", 2: "BN1 sync", 3: "conv1", 4: "publish+stats", 5: "arrive",
             6: "wait", 8: "BN2 combine+halo+wstore+sync", 9: "conv2", 10: "publish+stats",
             11: "arrive", 12: "wait+wstore", 200: "blocks done"},
-    "bwd": {0: "start", 1: "loads+publish+sync", 3: "conv2 dgrad", 99: "prev block: BN1 combine+apply+halo", 4: "publish+bwd sums", 5: "arrive", 6: "wait",
+    "bwd": {0: "start", 1: "loads+publish+sync", 3: "conv2 dgrad", 99: "prev block: wstore+tail", 4: "publish+bwd sums", 5: "arrive", 6: "wait",
             8: "BN2 combine+apply+halo+wstore+sync", 9: "conv1 dgrad", 10: "publish+bwd sums",
-            11: "arrive", 12: "wait", 200: "blocks done"},
+            11: "arrive", 12: "wait", 13: "BN1 table (sums read)", 14: "BN1 apply",
+            15: "BN1 halo", 200: "blocks done"},
 }
 
 
