@@ -1051,6 +1051,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   probe(x, 100 + S);
   // BN1 + ReLU of the block input -> halo A (input stage)
   fwd_bn_halo<SI, P>(x, x.m.ha, xr, B.x + img_i, B.bn1, wave, lane);
+  probe(x, 1);
   __syncthreads();
   probe(x, 2);
   bf16x4 pr[8], hr[8];
@@ -1485,16 +1486,19 @@ __device__ __forceinline__ bool block_bwd(Ctx& x, bf16x4 (&dout)[8], bf16x4 (&hs
   NbrBwd q;
   bwd_nbr_issue<SI, P>(nb, B.da1 + img_i, B.x + img_i, PROJ ? nullptr : B.dout + img_o, q);
   bn_bwd_table(ld_const(a.bns + (B.bn1)), x.bnr, GI::C, (float)a.N * GI::R * GI::R, x.m.tbl2);
+  probe(x, 13);
   // a stage's first block is the last one the backward reaches: its BN1 gradient completes
   // the stage's BatchNorm gradients (overlap mode: counted on the stage's bucket line)
   if (PROJ && a.overlap && blockIdx.x == 0 && a.bucket_of_stage[S] >= 0)
     x.mark = a.bar + PRN_BUCKET + a.bucket_of_stage[S] * PRN_LINE;
   if constexpr (PROJ) bwd_apply<SI, P, false>(dout, da, xs, dout, x.m.tbl2, wave, lane);
   else bwd_apply<SI, P, true>(dout, da, xs, dout, x.m.tbl2, wave, lane);
+  probe(x, 14);
   if (has_prev) load_regs<SI, P>(hs, Bn.h1 + img_i, x.kslice, wave, lane);   // previous block's BN2 input
   // the halo of dx for the previous block's conv2 dgrad (its neighbour rows: this block's
   // published da1, the saved block input, and -- identity blocks -- the published dout)
   bwd_halo<SI, P>(x, x.m.hb, dout, nb, q, nullptr, !PROJ, x.m.tbl2, wave, lane);
+  probe(x, 15);
   w_store(next_w2, w2r, x.m.w1);   // visible after the next block's first __syncthreads
   return true;
 }
