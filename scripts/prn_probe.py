@@ -61,8 +61,13 @@ def main():
             eng._run("fwd", st)
             torch.cuda.synchronize()
             eng.nat.prn_set_probe(0)
+        last_item = int(buf[8191].item())
+        buf[8191] = 0
         v = buf.view(-1, 2).cpu().tolist()
         stamps = [(t, c) for t, c in v if c != 0]
+        if seg == "bwd" and last_item:
+            print(f"  (weight-gradient workgroups out of items {(last_item - stamps[-1][1]) / 100.0:+.1f} us "
+                  f"after slice 0's last stamp)")
         acc = defaultdict(list)
         for (t0, c0), (t1, c1) in zip(stamps, stamps[1:]):
             if t1 >= 100 and t1 < 200:
