@@ -1531,23 +1531,47 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
   f32x4 acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int n = it.img0; n < it.img0 + it.nimg; ++n) {
-    __syncthreads();   // the previous image's operands are dead; tb written
-    constexpr int DU = RO * RO * CO / 8;
-    for (int q = tid; q < DU; q += PT)
-      *reinterpret_cast<bf16x8*>(dys + q * 8) = ld_sc1_b128(it.dy, (long)n * RO * RO * CO + q * 8);
-    constexpr int CU = CI / 8;
-    for (int q = tid; q < W2 * W2 * CU; q += PT) {
-      const int pix = q / CU, u = q - pix * CU;
+  // operands of image n + 1 are loaded into registers while image n's MFMAs run
+  constexpr int DU = RO * RO * CO / 8, CU = CI / 8, XU = W2 * W2 * CU;
+  constexpr int ND = (DU + PT - 1) / PT, NX = (XU + PT - 1) / PT;
+  bf16x8 rd[ND], rx[NX];
+  auto fetch = [&](int n) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int q = tid + i * PT;
+      if (q < DU) rd[i] = ld_sc1_b128(it.dy, (long)n * RO * RO * CO + q * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int q = tid + i * PT, pix = q / CU, u = q - pix * CU;
       const int hr = pix / W2, hc = pix - hr * W2;
-      bf16x8 v = {};
-      if (hr >= 1 && hr <= RI && hc >= 1 && hc <= RI) {
-        v = ldg(reinterpret_cast<const bf16x8*>(it.x + (((long)n * RI + hr - 1) * RI + hc - 1) * CI + u * 8));
-        if (it.scale != nullptr) v = affine_relu8(v, tb + u * 8, tb + 64 + u * 8);
+      rx[i] = bf16x8{};
+      if (q < XU && hr >= 1 && hr <= RI && hc >= 1 && hc <= RI)
+        rx[i] = ldg(reinterpret_cast<const bf16x8*>(it.x + (((long)n * RI + hr - 1) * RI + hc - 1) * CI + u * 8));
+    }
+  };
+  const int nend = it.img0 + it.nimg;
+  fetch(it.img0);
+  for (int n = it.img0; n < nend; ++n) {
+    __syncthreads();   // the previous image's operands are dead; tb written
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int q = tid + i * PT;
+      if (q < DU) *reinterpret_cast<bf16x8*>(dys + q * 8) = rd[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int q = tid + i * PT, pix = q / CU, u = q - pix * CU;
+      const int hr = pix / W2, hc = pix - hr * W2;
+      if (q < XU) {
+        bf16x8 v = rx[i];
+        if (it.scale != nullptr && hr >= 1 && hr <= RI && hc >= 1 && hc <= RI)
+          v = affine_relu8(v, tb + u * 8, tb + 64 + u * 8);
+        *reinterpret_cast<bf16x8*>(hal + pix * CI + u * 8) = v;
       }
-      *reinterpret_cast<bf16x8*>(hal + pix * CI + u * 8) = v;
     }
     __syncthreads();
+    if (n + 1 < nend) fetch(n + 1);
 #pragma unroll 1
     for (int kk = 0; kk < KPW; ++kk) {
       const int ks = kq * KPW + kk;
@@ -1581,19 +1605,24 @@ __device__ __forceinline__ void wgrad_item(const PrnItem& it, char* smem, int wa
       }
     }
   }
-  // fixed-order sum of the WKS pixel slices (slice 0 accumulates), then the slab
+  // fixed-order tree sum of the WKS pixel slices (slice kq += slice kq + h, h = WKS/2 .. 1;
+  // each level writes a fresh LDS region, so one barrier per level), then the slab
   float* red = reinterpret_cast<float*>(smem);
-  for (int s = 1; s < WKS; ++s) {
-    __syncthreads();
-    if (kq == s)
+  static_assert((WKS - 1) * TILES * 64 * 16 <= OFF_MISC, "wgrad reduction LDS");
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int h = WKS / 2; h >= 1; h /= 2) {
+    if (kq >= h && kq < 2 * h)
 #pragma unroll
       for (int t = 0; t < TPW; ++t)
-        *reinterpret_cast<f32x4*>(red + ((tg * TPW + t) * 64 + lane) * 4) = acc[t];
+        *reinterpret_cast<f32x4*>(red + (((base + kq - h) * TILES + tg * TPW + t) * 64 + lane) * 4) = acc[t];
     __syncthreads();
-    if (kq == 0)
+    if (kq < h)
 #pragma unroll
       for (int t = 0; t < TPW; ++t)
-        acc[t] += *reinterpret_cast<const f32x4*>(red + ((tg * TPW + t) * 64 + lane) * 4);
+        acc[t] += *reinterpret_cast<const f32x4*>(red + (((base + kq) * TILES + tg * TPW + t) * 64 + lane) * 4);
+    base += h;
   }
   if (kq == 0) {
 #pragma unroll
@@ -1832,7 +1861,12 @@ __global__ void __launch_bounds__(PT, 1) prn_bwd_kernel(PrnArgs a) {
                                           __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const int i = __builtin_amdgcn_readfirstlane(*slot);
-    if (i >= a.nitems) return;
+    if (i >= a.nitems) {
+      if (a.probe != nullptr && tid == 0)   // diagnostics: when the last workgroup ran out of items
+        __hip_atomic_fetch_max(a.probe + 8191, (long long)wall_clock64(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     const PrnItem& it = ld_const(a.items + i);
     if (!count_wait<8>(a.bar, PRN_READY, (unsigned)it.ready, a.err, flag)) return;
     run_item(it, smem, wave, lane, a.overlap != 0);
