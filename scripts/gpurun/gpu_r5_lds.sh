@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: weight-gradient items prefetch the next image's operands (mid), + tree slice sum (new) -- pins, + last-ready weight-gradient items of 1 / 2 images (t1 / t2), then the previous build
+# Round 5: weight-gradient items issue the BN table loads before the first image's (new); + N/32-image items for the last 4 blocks (d4) / all of stage 1 (s0) -- pins, then the previous build
 # (ab_old/) vs this one, same box, alternating runs; then the LDS conflict counter.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail
@@ -8,9 +8,9 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 180 --timeout-method threa
 tail -1 gpurun_out/r5l_tests.log
 for r in 1 2; do
   for b in 128 32 16; do
-    for v in old mid new t1 t2; do
-      case $v in old) cmd="python scripts/ab_run.py ab_old bench.py";; mid) cmd="python scripts/ab_run.py ab_mid bench.py";; *) cmd="python bench.py";; esac
-      case $v in t1) export DTR_PRN_TAIL_IMGS=1;; t2) export DTR_PRN_TAIL_IMGS=2;; *) unset DTR_PRN_TAIL_IMGS;; esac
+    for v in old new d4 s0; do
+      case $v in old) cmd="python scripts/ab_run.py ab_old bench.py";; *) cmd="python bench.py";; esac
+      case $v in d4) export DTR_PRN_TAIL_READY=43;; s0) export DTR_PRN_TAIL_READY=35;; *) unset DTR_PRN_TAIL_READY;; esac
       timeout -k 10 200 $cmd --batch $b --steps 250 --warmup 30 > gpurun_out/r5l_${v}_b$b.json 2> gpurun_out/r5l_err.log || { tail -20 gpurun_out/r5l_err.log; exit 1; }
       echo "round $r bs$b $v $(python -c "import json;d=json.load(open('gpurun_out/r5l_${v}_b$b.json'));print(d['ms_per_step'])")"
     done
