@@ -1,0 +1,8 @@
+#!/bin/bash
+# Kernel tables of the round-5 persistent step at bs16 and bs128 (rocprofv3 kernel trace).
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+set -o pipefail
+for b in 16 128; do
+  timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/prof_r5_$b -o run -- python3 bench.py --batch $b --steps 50 --warmup 10 --phase-steps 0 > gpurun_out/prof_r5_$b.log 2>&1 || { tail -20 gpurun_out/prof_r5_$b.log; exit 1; }
+done
+echo prof done
