@@ -199,6 +199,11 @@ __device__ __forceinline__ void st_sc1_b64(bf16* base, long elem, bf16x4 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 16);
 }
+// the same store without sc1 (write-back L2): tensors only a later launch reads
+__device__ __forceinline__ void st_wb_b64(bf16* base, long elem, bf16x4 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)(elem * 2), 0, 0);
+}
 __device__ __forceinline__ void st_sc1_b128(bf16* base, long elem, bf16x8 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(base), 0, 0x7fffffff, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (int)(elem * 2), 0, 16);
@@ -544,8 +549,9 @@ __device__ __forceinline__ void load_regs(bf16x4 (&v)[8], const bf16* img_base, 
 
 // write-through (sc1) stores: these tensors are read by other workgroups in the launch.
 // ROWS 1: only the slice's first and last rows (what the neighbouring slices read inside
-// the launch), 2: only the rows between them, 0: all.
-template <int S, int P, int ROWS = 0>
+// the launch), 2: only the rows between them, 0: all.  WB: write-back stores instead (the
+// forward's saved tensors past the border rows: only the backward launch reads them).
+template <int S, int P, int ROWS = 0, bool WB = false>
 __device__ __forceinline__ void publish(const bf16x4 (&v)[8], bf16* img_base, int kslice,
                                         int wave, int lane) {
   using G = Stg<S, P>;
@@ -558,8 +564,10 @@ __device__ __forceinline__ void publish(const bf16x4 (&v)[8], bf16* img_base, in
     canon<S, P>(kslice, pb * 16 + (lane & 15), h, w);
     const int lr = h - kslice * G::RS;
     const bool border = lr == 0 || lr == G::RS - 1;
-    if (ROWS == 0 || (ROWS == 1) == border)
-      st_sc1_b64(img_base, (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4), v[t]);
+    if (ROWS == 0 || (ROWS == 1) == border) {
+      if constexpr (WB) st_wb_b64(img_base, (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4), v[t]);
+      else st_sc1_b64(img_base, (h * G::R + w) * G::C + cb * 16 + 4 * (lane >> 4), v[t]);
+    }
   }
 }
 
@@ -1072,7 +1080,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   fwd_sums<S, P>(x, hr, B.bn2, wave, lane);
   probe(x, 4);
   grid_arrive(a.bar + PRN_FWD, a.shards);
-  publish<S, P, P == 1 ? 0 : 2>(hr, B.h1 + img_o, x.kslice, wave, lane);
+  publish<S, P, P == 1 ? 0 : 2, true>(hr, B.h1 + img_o, x.kslice, wave, lane);
   probe(x, 5);
   {
     bf16x8 w2r[nreg(conv_units(G::C, G::C, 3))];
@@ -1096,7 +1104,7 @@ __device__ __forceinline__ bool block_fwd(Ctx& x, bf16x4 (&xr)[8], int bi_next,
   fwd_sums<S, P>(x, xr, bi_next, wave, lane);
   probe(x, 10);
   grid_arrive(a.bar + PRN_FWD, a.shards);
-  publish<S, P, P == 1 ? 0 : 2>(xr, B.out + img_o, x.kslice, wave, lane);
+  publish<S, P, P == 1 ? 0 : 2, true>(xr, B.out + img_o, x.kslice, wave, lane);
   probe(x, 11);
   bf16x8 w1r[nreg_next_fwd<S>()], wpr[1];
   w_prefetch(next_w1, w1r);
@@ -1157,7 +1165,7 @@ __device__ __forceinline__ void prn_forward_body(const PrnArgs& a, char* smem) {
     if constexpr (P > 1) publish<0, P, 1>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     fwd_sums<0, P>(x, xr, B0.bn1, x.wave, x.lane);
     grid_arrive(a.bar + PRN_FWD, a.shards);
-    publish<0, P, P == 1 ? 0 : 2>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
+    publish<0, P, P == 1 ? 0 : 2, true>(xr, B0.x + (long)x.img * 1024 * 16, x.kslice, x.wave, x.lane);
     const WLoad L1 = wl_fwd(B0.w1f, 16, 16, 3);
     WLoad LP{};
     if (B0.wpf) LP = wl_fwd(B0.wpf, 16, 16, 1);

@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round 5: weight-gradient items issue the BN table loads before the first image's (new); + N/32-image items for the last 4 blocks (d4) / all of stage 1 (s0) -- pins, then the previous build
+# Round 5: forward saved tensors (past the border rows) as write-back instead of write-through stores -- pins, then the previous build
 # (ab_old/) vs this one, same box, alternating runs; then the LDS conflict counter.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail
 timeout -k 10 400 python -u -m pytest -x -q --timeout 180 --timeout-method thread \
   tests/test_persist_gpu.py tests/test_golden_gpu.py > gpurun_out/r5l_tests.log 2>&1 || { tail -60 gpurun_out/r5l_tests.log; exit 1; }
 tail -1 gpurun_out/r5l_tests.log
-for r in 1 2; do
+for r in 1 2 3; do
   for b in 128 32 16; do
-    for v in old new d4 s0; do
+    for v in old new; do
       case $v in old) cmd="python scripts/ab_run.py ab_old bench.py";; *) cmd="python bench.py";; esac
       case $v in d4) export DTR_PRN_TAIL_READY=43;; s0) export DTR_PRN_TAIL_READY=35;; *) unset DTR_PRN_TAIL_READY;; esac
       timeout -k 10 200 $cmd --batch $b --steps 250 --warmup 30 > gpurun_out/r5l_${v}_b$b.json 2> gpurun_out/r5l_err.log || { tail -20 gpurun_out/r5l_err.log; exit 1; }
