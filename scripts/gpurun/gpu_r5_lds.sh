@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: backward dout + stem gradient published from the LDS halo at one slice (mid); dout from the halo at every slice count, after the prefetches (new) -- pins, then the previous build
+# Round 5: forward weight prefetches one phase earlier (mid), + backward ones (new) -- pins, then the previous build
 # (ab_old/) vs this one, same box, alternating runs; then the LDS conflict counter.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 set -o pipefail
