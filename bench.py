@@ -203,15 +203,23 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
     import torch
 
     from distributed_tensorflow_resnet_amd.models.spec import build_spec
-    from distributed_tensorflow_resnet_amd.parallel.dist import DistContext, local_device_index
+    from distributed_tensorflow_resnet_amd.parallel.dist import (DistContext, apply_cu_partition,
+                                                                 local_device_index)
     from distributed_tensorflow_resnet_amd.parallel.watchdog import CommWatchdog
     from distributed_tensorflow_resnet_amd.train.engine import (Engine, cifar_lr_schedule,
                                                                 imagenet_lr_schedule)
 
+    # DTR_CU_PARTITION (rehearsals of several ranks on one GPU): this rank's CU mask, in
+    # the environment before the first HIP call
+    cu_mask = apply_cu_partition()
     local_rank = local_device_index()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    ctx = DistContext(device=device)
+    # CIFAR: the persistent step's overlap plan runs RCCL beside its backward grid on the
+    # CUs it reserves -- at most one channel (one all-reduce workgroup) per reserved CU
+    from distributed_tensorflow_resnet_amd.train.persist import OVERLAP_RESERVE_CUS
+    ctx = DistContext(device=device, rccl_max_channels=(OVERLAP_RESERVE_CUS
+                                                        if dataset.startswith("cifar") else None))
     spec = build_spec(dataset, size)
     sched = cifar_lr_schedule() if dataset.startswith("cifar") else imagenet_lr_schedule()
     wd = 2e-4 if dataset.startswith("cifar") else 1e-4
@@ -272,6 +280,8 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
              "step_path": ("persistent (P fwd/bwd = %d/%d)" % (eng.prn.P_fwd, eng.prn.P)
                            if eng.persist else "per-layer plan"),
              "persist_off_reason": eng.persist_reason or None,
+             "persist_overlap": bool(eng.persist_overlap),
+             "cus": int(eng.nat.cu_count()), "cu_mask": cu_mask,
              "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
     return ctx, elapsed, m, extra, phases
 

@@ -1304,6 +1304,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("wg_desc_bytes", []() { return (int)sizeof(WgReduceDesc); });
   m.def("opt_work_bytes", []() { return (int)sizeof(OptWork); });
   m.def("device_count", &hip_device_count);
+  m.def("cu_count", &device_cus,
+        "CUs this process dispatches to on the current device (the set bits of its CU mask, "
+        "ROC_GLOBAL_CU_MASK; the device's CUs without one): persistent-grid sizing");
+  m.def("cu_where", [](uint64_t out, int blocks, long long ticks, uint64_t stream) {
+    cu_where(reinterpret_cast<unsigned*>(out), blocks, ticks, reinterpret_cast<hipStream_t>(stream));
+  }, "diagnostics: per workgroup (HW_ID, XCC_ID) into out[2 * blocks] (CU-mask checks)");
+  m.def("cu_mask", &device_cu_mask,
+        "the process's CU mask on the current device as 32-bit words (bit i = CU i)");
   m.def(
       "crc32c",
       [](py::buffer b, uint32_t crc) {

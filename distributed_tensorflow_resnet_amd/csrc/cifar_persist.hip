@@ -1920,6 +1920,9 @@ __global__ void __launch_bounds__(PT, 1) prn_head_kernel(PrnArgs a) {
 static long long* g_prn_probe = nullptr;
 void prn_set_probe(long long* p) { g_prn_probe = p; }
 
+int device_cus() { return cu_count(); }
+std::vector<uint32_t> device_cu_mask() { return cu_mask_words(); }
+
 size_t prn_lds_bytes() { return LDS_TOTAL; }
 int prn_bar_words() { return PRN_BAR_WORDS; }
 int prn_acc_rep() { return PRN_ACC_REP; }

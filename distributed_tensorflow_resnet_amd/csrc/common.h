@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "tune.h"
 
 namespace dtr {
@@ -147,8 +149,11 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
 inline int wt_store_mode() { return (int)tune(T_WT_STORE); }
 inline bool wt_store_enabled() { return wt_store_mode() == 1; }
 
-// Compute units of the current device, queried once per device (persistent-grid sizing
-// on the launch path without a runtime attribute query per launch).
+// Compute units this process may dispatch to on the current device, queried once per
+// device (persistent-grid sizing on the launch path without a runtime query per launch):
+// the device's CUs, or the set bits of the process-wide CU mask (ROC_GLOBAL_CU_MASK, set
+// by parallel/dist.py apply_cu_partition when several ranks split one GPU's CUs) -- the
+// null stream's mask is that global mask, every stream of the process inherits it.
 inline int cu_count() {
   static int cache[64] = {0};
   int dev = 0;
@@ -157,9 +162,32 @@ inline int cu_count() {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
+    // (the runtime copies its whole global mask, which may hold more words than the
+    // CUs need: a generous buffer)
+    uint32_t mask[256] = {0};
+    const uint32_t words = (uint32_t)((n + 31) / 32);
+    if (words <= 32 && hipExtStreamGetCUMask(nullptr, words, mask) == hipSuccess) {
+      int bits = 0;
+      for (uint32_t w = 0; w < words; ++w) bits += __builtin_popcount(mask[w]);
+      if (bits > 0 && bits < n) n = bits;
+    }
     cache[dev] = n;
   }
   return cache[dev];
+}
+// The process's CU mask on the current device (32-bit words, bit i = CU i).
+inline std::vector<uint32_t> cu_mask_words() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return {};
+  const size_t words = (n + 31) / 32;
+  std::vector<uint32_t> mask(256, 0xA5A5A5A5u);   // generous: see cu_count
+  if (hipExtStreamGetCUMask(nullptr, (uint32_t)words, mask.data()) != hipSuccess) return {};
+  size_t used = mask.size();   // words the runtime wrote (beyond `words`: diagnostics)
+  while (used > words && mask[used - 1] == 0xA5A5A5A5u) --used;
+  mask.resize(used);
+  return mask;
 }
 // Direct convs: write-through once a launch writes >= 2 MB.  A kernel boundary pays
 // ~bytes / 6 TB/s to write back the dirty lines its predecessor left in L2

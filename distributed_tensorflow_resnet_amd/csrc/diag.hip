@@ -7,6 +7,7 @@
 // really does overlap in a different order from run to run.  The clock read is
 // the only memory-side effect: no loads, no stores.
 #include <algorithm>
+#include <stdexcept>
 
 #include "comm.h"
 #include "common.h"
@@ -22,6 +23,27 @@ __global__ void __launch_bounds__(64) plan_delay_kernel(long long ticks) {
 void plan_delay(long long ticks, hipStream_t s) {
   if (ticks <= 0) return;
   hipLaunchKernelGGL(plan_delay_kernel, dim3(1), dim3(64), 0, s, ticks);
+  DTR_CHECK_LAUNCH();
+}
+
+// cu_where: which compute unit each workgroup ran on (CU-mask checks,
+// scripts/cu_mask_probe.py).  One wave per workgroup; lane 0 stores (vector store)
+// the HW_ID register (cu_id bits 11:8, sh_id 12, se_id 15:13) and XCC_ID, then the
+// wave spins `ticks` so the grid's workgroups are resident together and spread out.
+__global__ void __launch_bounds__(64) cu_where_kernel(unsigned* out, long long ticks) {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc;
+  }
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+void cu_where(unsigned* out, int blocks, long long ticks, hipStream_t s) {
+  if (blocks <= 0 || out == nullptr) throw std::invalid_argument("cu_where: blocks > 0, out");
+  hipLaunchKernelGGL(cu_where_kernel, dim3(blocks), dim3(64), 0, s, out, ticks);
   DTR_CHECK_LAUNCH();
 }
 

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "tune.h"
 
@@ -198,6 +199,8 @@ bool conv_direct(const GemmArgs& a, int mode, hipStream_t s);
 bool conv_direct_covers(const GemmArgs& a, int mode);
 void set_direct_probe(long long* p);   // per-workgroup phase stamps of the direct conv (diag)
 void plan_delay(long long ticks, hipStream_t s);   // spin one wave for ticks x 10 ns (diag.hip)
+// per workgroup (HW_ID, XCC_ID) into out[2 * blocks], each spinning ticks x 10 ns (diag.hip)
+void cu_where(unsigned* out, int blocks, long long ticks, hipStream_t s);
 void set_conv_direct(int enabled);
 void set_conv_pipeline(int enabled);   // 2-deep pipelined implicit-GEMM / wgrad loops (tune conv_pipe)
 void set_fin_version(int v);   // BN finalize kernel variant (tune fin_v)
@@ -313,6 +316,9 @@ bool prn_supported(int N, int P, int nblocks, int classes, int kpad);
 // backward at P, the head folds), including co-residency from the occupancy API: "" when
 // the step is supported, else the reason.  The engine calls it once when it builds the plan.
 std::string prn_check(int N, int P, int P_fwd, int nblocks, int classes, int kpad);
+// CUs this process dispatches to on the current device (its CU mask's set bits) and the mask
+int device_cus();
+std::vector<uint32_t> device_cu_mask();
 size_t prn_lds_bytes();
 int prn_bar_words();   // barrier / readiness / queue words of PrnArgs::bar (zeroed every step)
 int prn_acc_rep();   // fp64 accumulator replicas per BatchNorm of the persistent kernels

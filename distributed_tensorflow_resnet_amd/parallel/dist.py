@@ -141,20 +141,89 @@ def ranks_on_device(store, rank: int, world: int, ident: str, tag: str = "dev") 
     of this host: every rank publishes (hostname, identity) through the c10d store and
     reads the others' (blocking until each rank has published -- every rank calls this
     at the same point, the engine build)."""
+    return len(peers_on_device(store, rank, world, ident, tag))
+
+
+def peers_on_device(store, rank: int, world: int, ident: str, tag: str = "dev") -> list:
+    """The ranks (this one included) on the physical device `ident` of this host
+    (ranks_on_device)."""
     mine = f"{socket.gethostname()}|{ident}"
     store.set(f"dtr/{tag}/{rank}", mine)
-    return sum(1 for r in range(world)
-               if (mine if r == rank else bytes(store.get(f"dtr/{tag}/{r}")).decode()) == mine)
+    return [r for r in range(world)
+            if (mine if r == rank else bytes(store.get(f"dtr/{tag}/{r}")).decode()) == mine]
+
+
+def _kfd_cu_count() -> int:
+    """CUs of this host's GPUs from the KFD topology (no HIP call: the CU mask must be in
+    the environment before the runtime starts); 256 (MI355X) when it is not readable."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in sorted(os.listdir(root)):
+            props = {}
+            with open(os.path.join(root, node, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+            simds, per = int(props.get("simd_count", 0)), int(props.get("simd_per_cu", 0))
+            if simds > 0 and per > 0:
+                return simds // per
+    except (OSError, ValueError):
+        pass
+    return 256
+
+
+def cu_partition_mask(index: int, parts: int, total: int) -> int:
+    """CU mask (bit i = CU i) of partition `index` of `parts` contiguous equal ranges."""
+    if not 0 <= index < parts or parts < 1 or total < parts:
+        raise ValueError(f"CU partition {index}/{parts} of {total} CUs")
+    lo, hi = index * total // parts, (index + 1) * total // parts
+    return ((1 << (hi - lo)) - 1) << lo
+
+
+def apply_cu_partition() -> str | None:
+    """Split one GPU's CUs between the ranks that share it (DTR_CU_PARTITION): ``n`` =
+    this process takes partition LOCAL_RANK % n of n contiguous CU ranges, ``i/n`` =
+    partition i.  Sets ROC_GLOBAL_CU_MASK, the HIP runtime's process-wide CU mask that
+    every queue of the process (the null stream, the engine's streams, the transport's
+    copies) inherits, so it must run before the first HIP call (entrypoints call it
+    before touching the GPU).  With disjoint masks two ranks on one GPU can each run
+    the persistent step's co-resident grids (gpu_shared_by_ranks compares the masks;
+    the grids are sized by the masked CU count, _C.cu_count).  Returns the mask (hex)
+    or None when no partition is asked for."""
+    env = os.environ
+    spec = os.environ.get("DTR_CU_PARTITION", "").strip()
+    if not spec or spec == "0":
+        return None
+    if "/" in spec:
+        i, n = (int(v) for v in spec.split("/", 1))
+    else:
+        n = int(spec)
+        i = int(env.get("LOCAL_RANK", env.get("RANK", "0"))) % n
+    mask = hex(cu_partition_mask(i, n, _kfd_cu_count()))
+    env["ROC_GLOBAL_CU_MASK"] = mask
+    return mask
+
+
+def _cu_mask_int() -> int:
+    """This process's CU mask on the current device as an int (0: unknown = all CUs)."""
+    try:
+        from .. import native
+        words = native(required=True).cu_mask()
+    except Exception:   # noqa: BLE001 - no extension: treat as the whole device
+        return 0
+    return sum(int(w) << (32 * i) for i, w in enumerate(words))
 
 
 def gpu_shared_by_ranks(ctx=None, device_index: int | None = None) -> bool:
     """Whether another rank of this job runs on this rank's physical GPU (the one-GPU
-    rehearsals that fold ranks onto one device).  Kernels that need every workgroup
-    co-resident (the persistent CIFAR step) must not run then: two processes' grids
-    interleaved on one device could each hold part of the CUs and wait for the rest
-    forever.  Decided from the devices' physical identities (device_identity) exchanged
-    through the c10d store, not from rank / device counts: launchers that hand every
-    rank one GPU by visible-device masks see one device per process."""
+    rehearsals that fold ranks onto one device) on CUs this rank also uses.  Kernels that
+    need every workgroup co-resident (the persistent CIFAR step) must not run then: two
+    processes' grids interleaved on one device could each hold part of the CUs and wait
+    for the rest forever.  Decided from the devices' physical identities (device_identity)
+    and the processes' CU masks (apply_cu_partition) exchanged through the c10d store,
+    not from rank / device counts: launchers that hand every rank one GPU by
+    visible-device masks see one device per process; ranks whose CU masks are disjoint
+    do not share."""
     if torch.cuda.device_count() == 0:
         return False
     if ctx is not None and getattr(ctx, "active", False):
@@ -167,20 +236,54 @@ def gpu_shared_by_ranks(ctx=None, device_index: int | None = None) -> bool:
         return False
     idx = torch.cuda.current_device() if device_index is None else device_index
     store = dist.distributed_c10d._get_default_store()
-    return ranks_on_device(store, rank, world, device_identity(idx)) > 1
+    peers = [r for r in peers_on_device(store, rank, world, device_identity(idx)) if r != rank]
+    if not peers:
+        return False
+    # several ranks on this GPU: shared unless every other one's CU mask is disjoint
+    mine = _cu_mask_int()
+    store.set(f"dtr/cumask/{rank}", f"{mine:x}")
+    for r in peers:
+        other = int(bytes(store.get(f"dtr/cumask/{r}")).decode(), 16)
+        if mine == 0 or other == 0 or (mine & other):
+            return True
+    return False
+
+
+def rccl_channels_reported(path: str | None) -> int | None:
+    """RCCL's channel count from its INIT debug log (``Channel 00/NN`` lines: the largest
+    NN of this process's communicators), None when there is no log."""
+    if not path or not os.path.exists(path):
+        return None
+    import re
+
+    best = None
+    with open(path, errors="replace") as fh:
+        for line in fh:
+            for m in re.finditer(r"Channel \d+/(\d+)", line):
+                best = max(best or 0, int(m.group(1)))
+    return best
 
 
 class DistContext:
-    """Thin, explicit wrapper so the engine never touches global state."""
+    """Thin, explicit wrapper so the engine never touches global state.
+
+    ``rccl_max_channels``: cap RCCL's channels (NCCL_MAX_NCHANNELS, set before the first
+    communicator of the process unless the user set it): each channel is one workgroup of
+    an all-reduce kernel, and the persistent CIFAR step's overlap plan runs the all-reduces
+    beside its backward grid on the OVERLAP_RESERVE_CUS it leaves free -- at one channel
+    per reserved CU they fit (train/persist.py).  RCCL's own INIT log (NCCL_DEBUG=INFO,
+    NCCL_DEBUG_SUBSYS=INIT into a per-process file, unless the user set NCCL_DEBUG) is kept
+    so comm_info can report the channel count RCCL actually built."""
 
     def __init__(self, backend: str | None = None, device: torch.device | None = None,
-                 timeout_s: float = 600.0):
+                 timeout_s: float = 600.0, rccl_max_channels: int | None = None):
         self.rank, self.world_size, self.local_rank = env_world()
         self.backend = backend
         self.device = device
         self.timeout_s = float(timeout_s)
         self.comm_fallback_reason = None
         self.initialized_here = False
+        self.rccl_log = None
         if device is not None and device.type == "cuda":
             engine_streams(device)   # before RCCL's streams: distinct hardware queues
         if self.world_size > 1 and not dist.is_initialized():
@@ -190,6 +293,16 @@ class DistContext:
                 backend = os.environ.get("DTR_DIST_BACKEND") or (
                     "nccl" if torch.cuda.is_available() else "gloo")
             self.backend = backend
+            if backend == "nccl":
+                if rccl_max_channels and "NCCL_MAX_NCHANNELS" not in os.environ:
+                    os.environ["NCCL_MAX_NCHANNELS"] = str(int(rccl_max_channels))
+                if "NCCL_DEBUG" not in os.environ:
+                    import tempfile
+
+                    self.rccl_log = os.path.join(tempfile.gettempdir(),
+                                                 f"dtr-rccl-init-{os.getpid()}.log")
+                    os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT",
+                                      NCCL_DEBUG_FILE=self.rccl_log)
             kw = {}
             if backend == "nccl" and device is not None:
                 kw["device_id"] = device
@@ -291,6 +404,11 @@ class DistContext:
             self.comm_fallback_reason = err or f"{kind} canary failed on another rank"
             return None
         return comm
+
+    def rccl_channel_info(self) -> dict:
+        """The channel cap in force and the count RCCL reported (bench JSON, comm_info)."""
+        return {"rccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS"),
+                "rccl_channels": rccl_channels_reported(self.rccl_log)}
 
     @property
     def is_chief(self) -> bool:

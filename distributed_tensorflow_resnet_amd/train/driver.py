@@ -21,7 +21,7 @@ import time
 import torch
 
 from ..models.spec import build_spec
-from ..parallel.dist import DistContext, local_device_index
+from ..parallel.dist import DistContext, apply_cu_partition, local_device_index
 from ..utils.checkpoint import Saver
 from ..utils.flags import build_parser, warn_unsupported
 from ..utils.records import EventWriter
@@ -111,8 +111,39 @@ def run_eval(flags, spec, device: str):
     return ev.run()
 
 
+def persist_fault_policy(flags) -> str:
+    """The persist_fault marker's lifecycle at start-up: '' when this attempt may select
+    the persistent CIFAR step, else why not (the marker left by an attempt whose grid
+    barrier timed out: DTR_TUNE gets persist=0 for this process and its children, and
+    the reason is logged and written into metrics.jsonl through the engine's
+    persist_reason).  --reset_persist_fault deletes the marker first."""
+    if not flags.train_dir:
+        return ""
+    path = os.path.join(flags.train_dir, PERSIST_FAULT_MARKER)
+    if flags.reset_persist_fault and os.path.exists(path):
+        try:
+            os.remove(path)
+        except FileNotFoundError:   # another rank removed it first
+            pass
+        H.log(f"--reset_persist_fault: removed {path}; the persistent step may be selected again")
+    if not os.path.exists(path):
+        return ""
+    try:
+        with open(path) as fh:
+            why = fh.read().strip().splitlines()[0]
+    except (OSError, IndexError):
+        why = "(unreadable)"
+    os.environ["DTR_TUNE"] = ",".join(filter(None, [os.environ.get("DTR_TUNE", ""), "persist=0"]))
+    reason = f"{PERSIST_FAULT_MARKER} in {flags.train_dir}: {why}"
+    H.log(f"persistent step disabled: {reason} (a previous attempt's grid barrier timed out; "
+          "--reset_persist_fault to retry it)")
+    return reason
+
+
 def main(argv=None, kind: str = "cifar") -> int:
     flags = build_parser(kind).parse_args(argv)
+    # DTR_CU_PARTITION (several ranks on one GPU): the CU mask before the first HIP call
+    apply_cu_partition()
     warn_unsupported(flags, H.log)
     if flags.job_name == "ps":
         return 0
@@ -128,16 +159,17 @@ def main(argv=None, kind: str = "cifar") -> int:
     # a previous attempt's persistent CIFAR step failed (a grid barrier timed out): this
     # attempt runs the launch-per-layer plan (every rank reads the same marker, and the
     # engine agrees the choice over c10d anyway)
-    if flags.train_dir and os.path.exists(os.path.join(flags.train_dir, PERSIST_FAULT_MARKER)):
-        os.environ["DTR_TUNE"] = ",".join(filter(None, [os.environ.get("DTR_TUNE", ""), "persist=0"]))
-        H.log(f"persistent step disabled: {PERSIST_FAULT_MARKER} in {flags.train_dir} "
-              "(a previous attempt's grid barrier timed out)")
+    fault_reason = persist_fault_policy(flags)
     dev = None
     if device == "gpu":
         local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-    ctx = DistContext(device=dev, timeout_s=flags.comm_timeout_secs)
+    from .persist import OVERLAP_RESERVE_CUS
+    # CIFAR: RCCL's channels capped at the persistent overlap plan's CU reserve (DistContext)
+    ctx = DistContext(device=dev, timeout_s=flags.comm_timeout_secs,
+                      rccl_max_channels=(OVERLAP_RESERVE_CUS if spec.dataset.startswith("cifar")
+                                         else None))
     dp_ctx = None if flags.variable_update == "independent" else ctx
     rank, world = ctx.rank, ctx.world_size
     sched = cifar_lr_schedule() if spec.dataset.startswith("cifar") else imagenet_lr_schedule()
@@ -149,6 +181,9 @@ def main(argv=None, kind: str = "cifar") -> int:
                            dist_ctx=dp_ctx, bucket_mb=flags.bucket_mb, use_graph=flags.use_graph,
                            data_seed=1234 + rank, allreduce_dtype=flags.allreduce_dtype,
                            input_mode="imagenet_u8" if u8 else "auto")
+    eng = getattr(backend, "engine", None)
+    if fault_reason and eng is not None and not eng.persist:
+        eng.persist_reason = fault_reason
     it = _train_batches(flags, spec, rank, world, u8=u8)
     feeder = None
     if it is None:
@@ -182,6 +217,9 @@ def main(argv=None, kind: str = "cifar") -> int:
         saver = Saver(flags.train_dir, flags.max_to_keep)
         chief_hooks.append(H.CheckpointSaverHook(saver, flags.save_checkpoint_steps,
                                                  flags.save_checkpoint_secs))
+    if eng is not None and eng.persist and world > 1 and dp_ctx is not None:
+        # every rank agrees the persistent launches' health before saves (and at the end)
+        hooks.append(H.PersistHealthHook(ctx, flags.save_checkpoint_steps or flags.log_every))
     if flags.check_numerics:
         hooks.append(H.NanGuardHook())
     ks = int(os.environ.get("DTR_FAULT_KILL_STEP", flags.fault_kill_step))
@@ -206,9 +244,12 @@ def main(argv=None, kind: str = "cifar") -> int:
         # skips the hooks' end() on an exception); the launcher (--max_restarts) restarts
         # from the last good checkpoint and the marker puts the restart on the per-layer plan
         H.log(f"FATAL: {e}; exiting with code {H.StepWatchdogHook.EXIT_CODE} for a restart")
-        if flags.train_dir and is_chief:
-            with open(os.path.join(flags.train_dir, PERSIST_FAULT_MARKER), "w") as fh:
-                fh.write(f"{e}\n")
+        if flags.train_dir:   # whichever rank faulted (every rank, once agreed)
+            os.makedirs(flags.train_dir, exist_ok=True)
+            tmp = os.path.join(flags.train_dir, f".{PERSIST_FAULT_MARKER}.{rank}")
+            with open(tmp, "w") as fh:
+                fh.write(f"rank {rank} at step {sess.global_step}: {e}\n")
+            os.replace(tmp, os.path.join(flags.train_dir, PERSIST_FAULT_MARKER))
         return H.StepWatchdogHook.EXIT_CODE
     dt = time.time() - t0
     if is_chief:

@@ -307,6 +307,7 @@ class Engine:
         from ..parallel.dist import gpu_shared_by_ranks
         pm = tune.get("persist")
         self.persist_slices = tune.get("persist_slices")
+        self.persist_overlap_tune = bool(tune.get("persist_overlap"))
         self.opt_fused = bool(tune.get("opt_fused"))
         # why the persistent step is off ("" = on); never on a GPU shared by several ranks
         # (its grids need every CU to themselves), and the same choice on EVERY rank (the
@@ -326,7 +327,7 @@ class Engine:
         # world > 1 (or a forced communicator): the gradient buckets' reduces and
         # all-reduces overlap the persistent backward launch (tune persist_overlap)
         self.persist_overlap = (self.persist and self.comm is not None
-                                and bool(tune.get("persist_overlap")))
+                                and self.persist_overlap_tune)
         self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
@@ -1774,6 +1775,13 @@ class Engine:
                 "rccl_library": self.comm.library_path if nat else None,
                 "rccl_version": (self.nat.Comm.rccl_version()
                                  if nat and transport == "rccl" else None),
+                # the persistent overlap plan's CU budget: CUs left out of the backward
+                # grid for the comm stream, and RCCL's channel cap / reported channels
+                "overlap_reserve_cus": (self.prn.cus - self.N * self.prn.P - self.prn.wgrad_wgs
+                                        if self.persist_overlap else 0),
+                **(self.dist.rccl_channel_info() if self.dist is not None else
+                   {"rccl_max_nchannels": os.environ.get("NCCL_MAX_NCHANNELS"),
+                    "rccl_channels": None}),
                 # the communication environment of this run (RCCL / HSA knobs)
                 "env": {k: v for k, v in sorted(os.environ.items())
                         if k.startswith(("NCCL_", "RCCL_", "HSA_"))}}

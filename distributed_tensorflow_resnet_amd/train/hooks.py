@@ -140,6 +140,10 @@ class JsonlMetricsHook(Hook):
         if self.n > 0 and step % self.n == 0 and session.is_chief:
             m = dict(session.metrics())
             m["time"] = time.time()
+            eng = getattr(session.backend, "engine", None)
+            if eng is not None:   # which step ran, and why the persistent one did not
+                m["step_path"] = "persistent" if getattr(eng, "persist", False) else "per-layer"
+                m["persist_disabled_reason"] = getattr(eng, "persist_reason", "") or None
             os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
             with open(self.path, "a") as fh:
                 fh.write(json.dumps(m) + "\n")
@@ -181,12 +185,48 @@ class CheckpointSaverHook(Hook):
     def after_run(self, session, step):
         due = (self.steps > 0 and step % self.steps == 0) or \
               (self.secs > 0 and time.time() - self.last_t >= self.secs)
-        if due and step != self.last_step:
+        # with a PersistHealthHook (multi-rank persistent step) only steps whose health
+        # every rank has agreed are saved: a due time-based save waits for the next one
+        if due and step != self.last_step and getattr(session, "health_step", step) == step:
             self._save(session, step)
 
     def end(self, session):
         if session.global_step != self.last_step:
             self._save(session, session.global_step)
+
+
+class PersistHealthHook(Hook):
+    """Every rank, multi-rank jobs on the persistent CIFAR step: every `every` steps and at
+    the end, agree over the process group whether ANY rank's persistent launch failed a
+    grid barrier (its error flag).  A failing rank's gradients still reach the all-reduce,
+    so every replica holds garbage after it, while the checkpoint is written by the chief,
+    whose own flag is clean: the agreement raises PersistentStepError on every rank (each
+    writes the persist_fault marker, driver.py), and the checkpoint hook saves only agreed
+    steps (session.health_step).  A collective, so every rank runs it at the same steps."""
+
+    def __init__(self, ctx, every: int):
+        self.ctx, self.every = ctx, max(1, int(every))
+
+    def begin(self, session):
+        session.health_step = -1
+
+    def _agree(self, session, step):
+        from .engine import PersistentStepError
+
+        eng = session.backend.engine
+        bad = eng.persist_error()
+        if not self.ctx._agree(not bad):
+            raise PersistentStepError(
+                f"a persistent-step grid barrier timed out on {'this' if bad else 'another'} "
+                f"rank by step {step}; every replica's state is invalid")
+        session.health_step = step
+
+    def after_run(self, session, step):
+        if step % self.every == 0:
+            self._agree(session, step)
+
+    def end(self, session):
+        self._agree(session, session.global_step)
 
 
 class NanGuardHook(Hook):

@@ -11,13 +11,22 @@ publishes anyway), grid barriers only where BatchNorm needs batch statistics (ex
 atomic sums), and the CUs beyond the slices compute the weight gradients (fp32 slabs per
 image group) while the backward's dgrad chain continues.  The step is then:
 
-    [augment] -> prn forward -> prn backward -> prn head folds (loss, precision, dense
-              gradients: one workgroup) -> one GPU: sgd_tiles (the weight-gradient slab
-              sums + SGD-momentum + both bf16 weight copies, ONE launch)
-                                         | world > 1: grouped slab reduce -> all-reduce
-                                           of the whole gradient -> optimizer
+    one GPU (5 launches, all on the main stream):
+      [augment] -> prn forward -> prn backward -> prn head folds (loss, precision, dense
+      gradients: one workgroup) -> sgd_tiles (the weight-gradient slab sums +
+      SGD-momentum + both bf16 weight copies, ONE launch)
 
-all on the main stream (5 launches on one GPU).
+    world > 1, a native communicator (tune persist_overlap=1, the default): three stage
+    buckets (bucket_ranges: stage 3 + final BN + dense, stage 2, stage 1 + stem)
+      main:  [augment] -> prn forward -> prn backward (N x P slice workgroups + the
+             weight-gradient workgroups; OVERLAP_RESERVE_CUS left out of its grid) ->
+             join -> pack(bucket 2) -> all-reduce(bucket 2) -> update(bucket 2, +step)
+      comm:  (forked after the forward) head folds -> for buckets 0, 1: a one-wave wait
+             for the bucket's count in the backward's barrier region (its weight-gradient
+             items + its BatchNorm mark, bucket_target) -> pack (slab sums, bf16 for a
+             bf16 exchange: one sgd_tiles launch) -> all-reduce -> update of the bucket's
+             parameters, all while the backward still runs on the other CUs
+    (persist_overlap=0: pack + ONE all-reduce + ONE update after the backward, main stream.)
 
 Selected by the engine (tune ``persist``: -1 auto = per-rank batch <= AUTO_MAX_BATCH on a supported
 CIFAR spec, 0 off, 1 on when supported).
@@ -48,9 +57,9 @@ OVERLAP_RESERVE_CUS = 48
 # stage 2 (64 channels) + the final BN + dense, stage 1, stage 0 + the stem
 BUCKET_OF_STAGE = (2, 1, 0)
 
-# every supported per-rank batch (MI355X, CIFAR RN50 step vs the per-layer engine: bs16
-# 0.660 vs 0.915 ms, bs32 0.722 vs 0.962, bs64 0.837 vs 1.085, bs96 1.034 vs 1.272, bs128
-# (1 slice) 1.101 vs 1.261)
+# every supported per-rank batch (MI355X, CIFAR RN50 one-GPU step, round-5 build vs the
+# per-layer engine: bs16 0.558 vs 0.926 ms, bs32 0.576 vs 0.964, bs64 0.647 vs 1.084,
+# bs128 (1 slice) 0.731-0.740 vs 1.261; profiles/final_check_r05.md)
 AUTO_MAX_BATCH = 240
 
 
@@ -107,13 +116,22 @@ def check(eng) -> str:
         first = i % n == 0
         if (b.proj is not None) != first or b.stride != (2 if first and stage else 1):
             return "projection / stride layout is not the CIFAR v2 one"
-    cus = torch.cuda.get_device_properties(eng.device).multi_processor_count
+    cus = nat.cu_count()   # this process's CUs (its CU mask, apply_cu_partition)
     P = slices_for(eng.N, cus, eng.persist_slices)
-    # (at least 16 CUs left for the weight-gradient workgroups)
-    if eng.N * P + 16 > cus:
-        return f"{eng.N} x {P} slices leave fewer than 16 CUs for the weight gradients"
+    # (at least 16 CUs left for the weight-gradient workgroups, beside the overlap
+    # plan's reserve for the comm stream)
+    reserve = OVERLAP_RESERVE_CUS if overlap_planned(eng) else 0
+    if eng.N * P + 16 + reserve > cus:
+        return (f"{eng.N} x {P} slices + {reserve} reserved CUs leave fewer than 16 of "
+                f"{cus} CUs for the weight gradients")
     return str(nat.prn_check(eng.N, P, fwd_slices_for(eng.N, cus, eng.persist_slices), nb,
                              spec.num_classes, eng.kpad))
+
+
+def overlap_planned(eng) -> bool:
+    """Whether the engine asks for the overlap plan (a communicator and tune
+    persist_overlap): its backward grid leaves OVERLAP_RESERVE_CUS to the comm stream."""
+    return eng.comm is not None and bool(getattr(eng, "persist_overlap_tune", False))
 
 
 def supported(eng) -> bool:
@@ -143,6 +161,17 @@ def bucket_ranges(eng):
     return [tuple(r) for r in out]
 
 
+def fault_injection_bar(rank: int) -> int:
+    """Tests only: the forward grid barrier at which workgroup 0 abandons its launch
+    (DTR_PRN_FAULT_BAR = ``bar`` on every rank or ``bar@rank`` on one rank of the job: a
+    lost workgroup), -1 off.  Honoured only with DTR_TEST_FAULTS=1."""
+    spec = os.environ.get("DTR_PRN_FAULT_BAR", "-1")
+    bar, _, only = spec.partition("@")
+    if int(bar) < 0 or os.environ.get("DTR_TEST_FAULTS", "0") != "1":
+        return -1
+    return int(bar) if only == "" or int(only) == rank else -1
+
+
 def _stage(b) -> int:
     return int(math.log2(b.cout // 16))
 
@@ -169,7 +198,7 @@ class PersistStep:
             r["dgamma"], r["dbeta"] = e.dgamma, e.dbeta
             r["acc"], r["bacc"] = e.acc.data_ptr(), e.bacc.data_ptr()
         self.bn_dev = self._dev(bn_rows)
-        self.cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.cus = nat.cu_count()   # this process's CUs (its CU mask)
         self.P = slices_for(N, self.cus, eng.persist_slices)          # backward
         self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
         self.overlap = bool(getattr(eng, "persist_overlap", False))
@@ -177,7 +206,7 @@ class PersistStep:
         # logged metrics (Engine.metrics) sees it at no extra cost; never cleared by the
         # kernels (Engine.clear_persist_error)
         self.err = eng.scalars[4:5].view(torch.int32)
-        self.fault_bar = int(os.environ.get("DTR_PRN_FAULT_BAR", "-1"))
+        self.fault_bar = fault_injection_bar(eng.dist.rank if eng.dist is not None else 0)
         self.dpool = torch.zeros((N, 64), device=dev)
         self.dx0 = torch.empty_like(eng.X[0])
         # per-block backward gradients published to the weight-gradient workgroups

@@ -151,6 +151,10 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_argument("--fault_kill_step", type=int, default=-1,
                    help="Fault injection: rank --fault_kill_rank exits at this step.")
     p.add_argument("--fault_kill_rank", type=int, default=0)
+    p.add_bool("reset_persist_fault", False,
+               "Delete the persist_fault marker in --train_dir (left by an attempt whose "
+               "persistent CIFAR step failed a grid barrier) so this attempt selects the "
+               "persistent step again.")
     p.add_argument("--step_watchdog_secs", type=float, default=0.0,
                    help="If > 0, abort (exit 3, for the launcher to restart from the latest "
                         "checkpoint) when no step completes for this many seconds.  Multi-rank "

@@ -24,6 +24,7 @@ import torch  # noqa: E402
 
 from distributed_tensorflow_resnet_amd.models.spec import build_spec  # noqa: E402
 from distributed_tensorflow_resnet_amd.parallel.dist import (DistContext,  # noqa: E402
+                                                             apply_cu_partition,
                                                              local_device_index)
 from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule  # noqa: E402
 
@@ -32,6 +33,7 @@ def main() -> int:
     size = int(os.environ.get("DP_CHECK_SIZE", "14"))
     per_rank = int(os.environ.get("DP_CHECK_BATCH", "8"))
     bucket_mb = float(os.environ.get("DP_CHECK_BUCKET_MB", "0.25"))
+    cu_mask = apply_cu_partition()   # DTR_CU_PARTITION: before the first HIP call
     torch.cuda.set_device(local_device_index())
     dev = torch.device("cuda", local_device_index())
     ctx = DistContext(device=dev)
@@ -46,9 +48,16 @@ def main() -> int:
     eng.broadcast_parameters(0)
     for e in (eng, ref):
         e.fill_synthetic(seed=rank)
+    if eng.persist != ref.persist:
+        raise SystemExit(f"dp_check: persistent step on the DP engine {eng.persist} "
+                         f"({eng.persist_reason}) but {ref.persist} on the local one ({ref.persist_reason})")
     eng.step()
-    ref.step()
+    # the local gradient without an update (the one-GPU persistent step leaves its
+    # weight-gradient slabs to the optimizer launch; forward_backward sums them into grad)
+    ref.forward_backward()
     torch.cuda.synchronize()
+    if eng.persist_error() or ref.persist_error():
+        raise SystemExit("dp_check: a persistent-step grid barrier timed out")
     info = eng.comm_info()
     if ctx.backend == "gloo":
         local = ref.grad.cpu()
@@ -74,7 +83,7 @@ def main() -> int:
             want = want + p
         grad_ok = torch.equal(want, got)
     maxdiff = float((want - got).abs().max())
-    for _ in range(3):
+    for _ in range(int(os.environ.get("DP_CHECK_STEPS", "3"))):
         eng.step()
     torch.cuda.synchronize()
     state = torch.cat([eng.params.master, eng.mom])
@@ -83,14 +92,20 @@ def main() -> int:
     sync_ok = torch.equal(r0, state)
     flags = torch.tensor([0 if grad_ok else 1, 0 if sync_ok else 1], device=dev)
     ctx.all_reduce_sum(flags)
+    err = torch.tensor([int(eng.persist_error())], device=dev)
+    ctx.all_reduce_sum(err)
     m = eng.metrics()
     if ctx.is_chief:
+        path = (f"persistent(P={eng.prn.P_fwd}/{eng.prn.P},overlap={int(eng.persist_overlap)},"
+                f"wgrad_wgs={eng.prn.wgrad_wgs})" if eng.persist else "per-layer")
         print(f"dp_check world={world} transport={info['transport']} "
               f"native={info['native']} allreduce_ops={info['allreduce_ops']} "
-              f"fallback={info['fallback_reason']} grad_equal_ranks_failing="
+              f"fallback={info['fallback_reason']} step_path={path} cus={eng.nat.cu_count()} "
+              f"cu_mask={cu_mask} grad_equal_ranks_failing="
               f"{int(flags[0])} (max|diff|={maxdiff:.3g}) replicas_diverged={int(flags[1])} "
+              f"persist_errors={int(err)} "
               f"loss={m['cross_entropy']:.4f} step={m['global_step']}", flush=True)
-        ok = int(flags.sum()) == 0
+        ok = int(flags.sum()) == 0 and int(err) == 0
         print("DP_CHECK_OK" if ok else "DP_CHECK_FAIL", flush=True)
     ctx.shutdown()
     return 0

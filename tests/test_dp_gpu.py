@@ -157,3 +157,77 @@ def test_launcher_restarts_native_job_from_checkpoint(gpu, tmp_path):
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     assert "restarting job" in r.stdout and "Restoring parameters from" in r.stdout, r.stdout[-3000:]
     assert tb.latest_checkpoint(td).endswith("model.ckpt-6")
+
+
+# Two ranks on ONE GPU with disjoint halves of its CUs (DTR_CU_PARTITION=2 ->
+# ROC_GLOBAL_CU_MASK per process): each rank may then run the persistent step's
+# co-resident grids, sized by its masked CU count (128), so the world > 1 headline path
+# -- the persistent backward with the overlap plan's 48-CU reserve, the comm stream's
+# bucket waits, packs, all-reduces and early parameter updates beside it -- runs with a
+# real second rank and a real cross-process exchange (the shm transport: RCCL refuses
+# two ranks on one device).  bs16 per rank = the 8-GPU share of the global batch 128.
+CUP = dict(SHM, DTR_CU_PARTITION="2")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,port", [("fp32", 29751), ("bf16", 29752)])
+def test_persistent_overlap_two_ranks_cu_partition(gpu, dtype, port):
+    r = _torchrun(["scripts/dp_check.py"], port, timeout=600,
+                  extra_env=dict(CUP, DP_CHECK_SIZE="50", DP_CHECK_BATCH="16",
+                                 DP_CHECK_STEPS="20", DP_CHECK_ALLREDUCE=dtype))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "DP_CHECK_OK" in r.stdout, r.stdout[-3000:]
+    assert "step_path=persistent(P=4/4,overlap=1" in r.stdout, r.stdout[-2000:]
+    assert "transport=shm native=True" in r.stdout and "cus=128" in r.stdout, r.stdout[-2000:]
+    assert "persist_errors=0" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_persistent_cu_partition(gpu):
+    """`bench.py --gpus 2` on the persistent step at world 2 (CU halves, shm transport)."""
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **CUP)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5",
+                        "--batch", "32"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    cfg = out["config"]
+    assert out["pg_world_size"] == 2 and cfg["per_gpu_batch"] == 16, out
+    assert cfg["step_path"].startswith("persistent") and cfg["persist_overlap"], cfg
+    assert cfg["cus"] == 128 and cfg["comm"]["transport"] == "shm", cfg
+
+
+@pytest.mark.gpu
+def test_fault_on_one_rank_fails_job_and_restarts_per_layer(gpu, tmp_path):
+    """a grid-barrier timeout on a NON-chief rank (DTR_PRN_FAULT_BAR=3@1) must
+    fail the whole job before the chief checkpoints the poisoned state: the faulting rank
+    raises at its next health read and writes the marker; the restart resumes from the
+    last agreed checkpoint on the per-layer plan and finishes."""
+    import distributed_tensorflow_resnet_amd.utils.tensor_bundle as tb
+
+    td = str(tmp_path / "train")
+    common = ["resnet_cifar_main.py", "--device", "gpu", "--resnet_size", "8", "--batch_size", "16",
+              "--synthetic", "--train_dir", td, "--save_checkpoint_steps", "1",
+              "--variable_update", "horovod", "--log_every", "1", "--comm_timeout_secs", "120"]
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **CUP)
+    launch = [sys.executable, "-m", "distributed_tensorflow_resnet_amd.parallel.launch", "--nproc", "2"]
+    r = subprocess.run(launch + ["--master_port", "29761"] + common + ["--train_steps", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-2")
+    env.update(DTR_PRN_FAULT_BAR="3@1", DTR_TEST_FAULTS="1")
+    r = subprocess.run(launch + ["--master_port", "29771", "--max_restarts", "1"] + common +
+                       ["--train_steps", "4"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=500)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "grid barrier timed out" in out and "[launch] a rank failed" in out, out[-4000:]
+    assert "persistent step disabled" in out, out[-4000:]
+    assert os.path.exists(os.path.join(td, "persist_fault"))
+    # written by the faulting rank 1 and by rank 0 once the agreement failed (last wins)
+    marker = open(os.path.join(td, "persist_fault")).read()
+    assert "rank 1 at step 3" in marker or "rank 0 at step 3" in marker and "another rank" in marker
+    # the broken step never reached a checkpoint: both attempts resumed from step 2
+    assert out.count("(global_step=2)") == 4, out[-4000:]   # 2 ranks x 2 attempts
+    assert tb.latest_checkpoint(td).endswith("model.ckpt-4")

@@ -72,7 +72,7 @@ def test_persistent_fault_fails_job_and_restart_falls_back(gpu, tmp_path):
     assert tb.latest_checkpoint(td).endswith("model.ckpt-2")
     r = run(["-m", "distributed_tensorflow_resnet_amd.parallel.launch", "--nproc", "1",
              "--max_restarts", "1", "--master_port", "29634", "resnet_cifar_main.py",
-             "--train_steps", "4"] + common, env={"DTR_PRN_FAULT_BAR": "3"})
+             "--train_steps", "4"] + common, env={"DTR_PRN_FAULT_BAR": "3", "DTR_TEST_FAULTS": "1"})
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "grid barrier timed out" in out and "exiting with code 3" in out, out[-4000:]
