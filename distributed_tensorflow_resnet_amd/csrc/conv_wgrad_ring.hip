@@ -34,13 +34,45 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 constexpr int kWrOOB = 0x7fff0000;   // buffer offset past every operand (reads zeros)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor (base, 0 stride, num_records bytes, the same dword3 as
+// __builtin_amdgcn_make_buffer_rsrc's 0x00020000) for the inline-asm DMA below.
+__device__ __forceinline__ i32x4 buf_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32) & 0xffff);
+  r.z = __builtin_amdgcn_readfirstlane(bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// buffer_load_dwordx4 ... lds (16 B per lane, lane-linear at M0 = the wave's LDS base) as
+// inline asm.  Through the builtin, hipcc treats the DMA as a pending LDS write that may
+// alias every ds_read: it waited vmcnt(0) right after each K tile's issue, before the
+// ds_reads of the tile being computed -- no DMA ever overlapped this wave's MFMAs (only
+// the second workgroup on the CU's).  Invisible to the compiler's counters, the DMAs are
+// waited for only by this kernel's own counted vmcnt at the top of the K loop (no other
+// vector-memory load is in flight in the loop).
+__device__ __forceinline__ void dma16(const i32x4& rsrc, unsigned lds_base, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(lds_base), "v"(voff), "s"(rsrc) : "m0");
+}
 
 }  // namespace
 
+// Two LDS stages (each K tile's A and B images, 32 KiB): one tile in flight beside the
+// MFMAs, two workgroups per CU.  Tiles past the slice's end are issued all out-of-range
+// (zeros, never read), so every wait is the same vmcnt and the loop body has no branch.
+// (3 / 4 stages at one workgroup per CU for the grids of <= one workgroup per CU measured
+// slower standalone and 1-2 % slower in-step: a 128 KiB workgroup keeps every other
+// kernel off its CU; profiles/imagenet_wgrad_r6.md.)
 template <bool PRE>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_wgrad_ring_kernel(WgradArgs args) {
+  constexpr int NST = 2;
   constexpr int BM = 128, BN = 128, BK = 64, WN = 2;
   constexpr int WTM = 64, WTN = 64, MR = 4, NR = 4;
   constexpr int OP_B = BK * BM * 2;          // 16 KiB per operand tile
@@ -64,10 +96,9 @@ conv_wgrad_ring_kernel(WgradArgs args) {
 
   const long x_elems = (long)g.N * g.H * g.W * Cin;
   const long dy_elems = (long)P * Cout;
-  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.x), 0,
-                                                      (int)(x_elems * 2), 0x00020000);
-  const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(args.dy), 0,
-                                                       (int)(dy_elems * 2), 0x00020000);
+  const i32x4 rs_x = buf_rsrc(args.x, (int)(x_elems * 2));
+  const i32x4 rs_dy = buf_rsrc(args.dy, (int)(dy_elems * 2));
+  const unsigned lds0 = (unsigned)(unsigned long long)(lds_void*)smem;   // LDS byte address
 
   // ---- per-lane DMA state: rows r_i = (wave * 4 + i) * 4 + lr, slot sl ----
   const int sl = lane & 15, lr = lane >> 4;
@@ -102,55 +133,81 @@ conv_wgrad_ring_kernel(WgradArgs args) {
       pb1[j] = b_ok[j] ? *reinterpret_cast<const f32x4*>(args.pre_shift + b_ci[j] + 4) : z;
     }
   }
-  // pixel of each of the lane's 4 rows, stepped by BK per issued tile
+  // Each of the lane's 4 rows is one pixel, stepped by BK per issued tile.  Its source
+  // offsets are kept incrementally in bytes -- A: p * Cout * 2; B: the 3x3 window origin
+  // ((img * H + hs) * W + ws) * Cin * 2 with hs = ho * stride - pad, ws = wo * stride - pad
+  // -- so a tile's 8 DMA addresses cost adds and selects, no multiply: with one workgroup
+  // per CU (the slab-capped deep-K grids) the per-tile address chain (quarter-rate 32-bit
+  // multiplies and 64-bit mads, one dependent on the next) ran ~0.65 us per K tile,
+  // longer than the tile's MFMAs and DMAs together.
+  const int S = g.stride;
   const int HoWo = g.Ho * g.Wo;
   const int d_ho = BK / g.Wo, d_wo = BK - d_ho * g.Wo;
-  int px_img[4], px_ho[4], px_wo[4];
+  const int Cb = Cin * 2;   // bytes per input pixel
+  int prow[4], pa[4], hs[4], ws[4], xb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int p = p_begin + (wave * 4 + i) * 4 + lr;
-    px_img[i] = p / HoWo;
-    const int rem = p - px_img[i] * HoWo;
-    px_ho[i] = rem / g.Wo;
-    px_wo[i] = rem - px_ho[i] * g.Wo;
+    const int img = p / HoWo;
+    const int rem = p - img * HoWo;
+    const int ho = rem / g.Wo, wo = rem - (rem / g.Wo) * g.Wo;
+    prow[i] = p;
+    pa[i] = p * Cout * 2;
+    hs[i] = ho * S - g.pad;
+    ws[i] = wo * S - g.pad;
+    xb[i] = ((img * g.H + hs[i]) * g.W + ws[i]) * Cb;
   }
-  unsigned pend = 0u;   // PRE: which of this lane's 4 B chunks of the pending tile are real
-  int it_pbase = p_begin;
+  // per column parity j: A channel bytes, B tap offset bytes from the window origin
+  int ta[2], tb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ta[j] = a_col[j] * 2;
+    tb[j] = (b_r[j] * g.W + b_c[j]) * Cb + b_ci[j] * 2;
+  }
+  // stepping constants (uniform): +BK pixels, the row wrap, the image wrap
+  const int st_pa = BK * Cout * 2;
+  const int st_ws = d_wo * S, st_hs = d_ho * S, st_xb = (d_ho * S * g.W + d_wo * S) * Cb;
+  const int w_lim = g.Wo * S - g.pad, w_ws = g.Wo * S, w_xb = (S * g.W - g.Wo * S) * Cb;
+  const int h_lim = g.Ho * S - g.pad, h_hs = g.Ho * S, h_xb = (g.H * g.W - g.Ho * S * g.W) * Cb;
+  // PRE: which of this lane's 4 B chunks of each issued, unconsumed tile are real, 4 bits
+  // per tile in issue order (the oldest in bits 3:0)
+  unsigned pend = 0u;
 
-  auto issue = [&](int stage) {   // K tile at it_pbase -> stage (4 A + 4 B DMAs per wave)
-    char* st = smem + stage * 2 * OP_B;
+  auto issue = [&](int stage) {   // the rows' next K tile -> stage (4 A + 4 B DMAs per wave)
+    const unsigned st = lds0 + stage * 2 * OP_B;
     unsigned msk = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 4 + lr;
-      const int p = it_pbase + row;
       const int j = i & 1;
-      const bool pok = p < p_end;
-      const int aoff = (pok && a_col[j] >= 0) ? (p * Cout + a_col[j]) * 2 : kWrOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_dy, (lds_void*)(st + (wave * 4 + i) * 1024), 16, aoff, 0, 0, 0);
-      const int hi = px_ho[i] * g.stride - g.pad + b_r[j];
-      const int wi = px_wo[i] * g.stride - g.pad + b_c[j];
-      const bool ok = pok && b_ok[j] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      const int boff = ok ? (((px_img[i] * g.H + hi) * g.W + wi) * Cin + b_ci[j]) * 2 : kWrOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_x, (lds_void*)(st + OP_B + (wave * 4 + i) * 1024), 16, boff, 0, 0, 0);
-      msk |= ok ? (1u << i) : 0u;
-      // advance this row's pixel by BK for the next tile (host: BK / Wo + 1 <= 3 Ho)
-      px_wo[i] += d_wo;
-      px_ho[i] += d_ho;
-      const bool wrap = px_wo[i] >= g.Wo;
-      px_wo[i] -= wrap ? g.Wo : 0;
-      px_ho[i] += wrap ? 1 : 0;
+      // (masks, not ?: on the offsets: hipcc sank those selects into exec-masked
+      // branches, one DMA per side)
+      const int pok = prow[i] < p_end;
+      const int aok = pok & (a_col[j] >= 0);
+      const int aoff = kWrOOB + ((pa[i] + ta[j] - kWrOOB) & -aok);
+      dma16(rs_dy, st + (wave * 4 + i) * 1024, aoff);
+      const int ok = pok & (int)b_ok[j] & ((unsigned)(hs[i] + b_r[j]) < (unsigned)g.H) &
+                     ((unsigned)(ws[i] + b_c[j]) < (unsigned)g.W);
+      const int boff = kWrOOB + ((xb[i] + tb[j] - kWrOOB) & -ok);
+      dma16(rs_x, st + OP_B + (wave * 4 + i) * 1024, boff);
+      msk |= (unsigned)ok << i;
+      // advance this row's pixel by BK (host: BK / Wo + 1 <= 3 Ho)
+      prow[i] += BK;
+      pa[i] += st_pa;
+      ws[i] += st_ws;
+      hs[i] += st_hs;
+      xb[i] += st_xb;
+      const bool wrap = ws[i] >= w_lim;
+      ws[i] -= wrap ? w_ws : 0;
+      hs[i] += wrap ? S : 0;
+      xb[i] += wrap ? w_xb : 0;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const bool nxt = px_ho[i] >= g.Ho;
-        px_ho[i] -= nxt ? g.Ho : 0;
-        px_img[i] += nxt ? 1 : 0;
+        const bool nxt = hs[i] >= h_lim;
+        hs[i] -= nxt ? h_hs : 0;
+        xb[i] += nxt ? h_xb : 0;
       }
     }
-    pend = msk;
-    it_pbase += BK;
+    pend |= msk << (4 * (NST - 2));
   };
 
   f32x4 acc[MR][NR];
@@ -192,16 +249,27 @@ conv_wgrad_ring_kernel(WgradArgs args) {
     }
   };
 
-  if (KT > 0) issue(0);
+  // prologue: tiles 0 .. NST-2 in flight
+  if (KT > 0) {
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) {
+      pend >>= 4;   // (each issue lands at the FIFO's tail, NST - 2)
+      issue(i);
+    }
+  }
+  constexpr int kAfter = (NST - 2) * 8;   // this thread's DMAs issued after tile t's
   int rd = 0;
   for (int t = 0; t < KT; ++t) {
-    __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));   // vmcnt(0): own DMAs landed
+    // own DMAs of tile t landed (the NST - 2 newer tiles' may still be in flight)
+    __builtin_amdgcn_s_waitcnt((kAfter & 15) | ((kAfter >> 4) << 14) | (7 << 4) | (15 << 8));
     asm volatile("" ::: "memory");
+    const unsigned cur = pend & 15u;
+    pend >>= 4;
     if constexpr (PRE) {   // BN+ReLU on this thread's own B chunks (the ones it fetched)
       bf16* Bst = reinterpret_cast<bf16*>(smem + rd * 2 * OP_B + OP_B);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if ((pend >> i) & 1u) {
+        if ((cur >> i) & 1u) {
           bf16x8* q = reinterpret_cast<bf16x8*>(Bst + ((wave * 4 + i) * 1024 + lane * 16) / 2);
           const int j = i & 1;
           *q = affine_relu8_reg(*q, ps0[j], ps1[j], pb0[j], pb1[j]);
@@ -211,10 +279,15 @@ conv_wgrad_ring_kernel(WgradArgs args) {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < KT) issue(rd ^ 1);
+    // into the stage consumed at t - 1 (every wave passed this barrier after its
+    // MFMAs); past the slice's end all out of range, so the issue needs no branch and
+    // its address adds can interleave with the MFMAs
+    issue(rd == 0 ? NST - 1 : rd - 1);
     mma_stage(rd);
-    rd ^= 1;
+    rd = rd == NST - 1 ? 0 : rd + 1;
   }
+  // the out-of-range tail DMAs land before the LDS is released
+  __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));
 
   float* out = args.part + (long)split * Cout * NT;
 #pragma unroll

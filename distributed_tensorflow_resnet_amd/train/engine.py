@@ -1611,6 +1611,11 @@ class Engine:
         """Forward + backward of the current batch with `grad` complete and no update
         (the persistent step on one GPU otherwise leaves its weight-gradient slabs to
         the optimizer launch)."""
+        if self.persist_overlap:
+            # the overlap plan updates the early buckets' parameters on the comm stream
+            # inside the backward segment (ADVICE r5): no update-free backward exists
+            raise RuntimeError("forward_backward: the persistent overlap plan (world > 1, "
+                               "tune persist_overlap=1) updates parameters during the backward")
         st = torch.cuda.current_stream().cuda_stream if st is None else st
         self._run("fwd", st)
         self._run_bwd(st)
