@@ -214,3 +214,28 @@ def test_comm_transports_and_host_errors(gpu):
     assert sh.async_error() == 6
     with pytest.raises(RuntimeError):
         sh.all_reduce(y.data_ptr(), y.numel(), nat.COMM_F32, s2.cuda_stream)
+
+
+@pytest.mark.gpu
+def test_rccl_init_log_goes_to_its_file_and_reports_channels(gpu, tmp_path):
+    """DistContext's RCCL INIT log (NCCL_DEBUG=INFO, SUBSYS=INIT, NCCL_DEBUG_FILE) must land
+    in the per-process file -- never on stdout, where rank 0 prints bench.py's one JSON
+    line -- and carry the channel count comm_info reports; with NCCL_MAX_NCHANNELS set
+    (the persistent overlap plan's cap) RCCL builds no more channels than that."""
+    log = tmp_path / "rccl.log"
+    code = (
+        "import torch\n"
+        "from distributed_tensorflow_resnet_amd.parallel.dist import DistContext, rccl_channels_reported\n"
+        "torch.cuda.set_device(0)\n"
+        "comm = DistContext().native_comm(0, force=True)\n"
+        "assert comm is not None\n"
+        f"print('CHANNELS', rccl_channels_reported({str(log)!r}))\n")
+    env = dict(os.environ, NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT", NCCL_DEBUG_FILE=str(log),
+               NCCL_MAX_NCHANNELS="4")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "NCCL INFO" not in r.stdout, r.stdout[-2000:]
+    assert log.exists() and "NCCL INFO" in log.read_text(), r.stdout[-2000:]
+    got = [ln for ln in r.stdout.splitlines() if ln.startswith("CHANNELS")][0].split()[1]
+    assert got == "None" or int(got) <= 4, got
