@@ -332,7 +332,10 @@ class Engine:
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan
         self.ready_index: dict[str, int] = {}
-        self._device_deps: dict[int, int] = {}   # stream check: device-side waits (op -> producer op)
+        # stream check: device-side waits (op -> producer op, or (producer op, buffers the
+        # wait covers)) and the buffers the ops running beside a partial wait touch
+        self._device_deps: dict = {}
+        self._op_buffers: dict[int, set] = {}
         self.reduce_buckets = self.world > 1 or self.comm is not None
         if self.reduce_buckets:
             if not bucket_mb:
@@ -369,7 +372,7 @@ class Engine:
         else:
             self.bucket_sched = []
         errs = check_plan(self.plan, self.seg, barriers=[i for i, _, _ in self.bucket_sched],
-                          device_deps=self._device_deps)
+                          device_deps=self._device_deps, op_buffers=self._op_buffers)
         if errs:   # fork/join structure of the three streams (race check)
             raise RuntimeError("plan stream-ordering violations:\n  " + "\n  ".join(errs[:8]))
         self.graph = None
@@ -1555,8 +1558,11 @@ class Engine:
         its parameters -- all while the backward still runs on the CUs left out of its
         grid.  The main stream joins the comm stream right after the backward (its buckets
         are long done by then) and packs, all-reduces and updates the last bucket itself.
-        The stream check takes each bucket wait as ordered after the backward launch
-        (device_deps): the launch publishes the bucket's completion through that line.
+        The stream check takes each bucket wait as a PARTIAL dependency on the backward
+        launch (device_deps with the buffers it covers: the bucket's gradients / slabs and
+        parameters, which the launch publishes complete and no longer reads once the count
+        is reached, plus the lr slot and global step the launch never touches), and holds
+        every comm-stream op before the join to the buffers it declares (op_buffers, R5).
         Returns the segment names updated on the comm stream."""
         from .persist import bucket_ranges
 
@@ -1571,7 +1577,12 @@ class Engine:
         err = self.prn.err.data_ptr()
         ranges = bucket_ranges(self)
 
-        def bucket(lo, hi, names, stream):
+        def declare(a0, bset):
+            for i in range(a0, plan.size()):
+                self._op_buffers[i] = set(bset)
+
+        def bucket(b, lo, hi, names, stream):
+            a0 = plan.size()
             if self.opt_fused:
                 self._emit_pack(plan, names, stream=stream)
             else:
@@ -1579,20 +1590,23 @@ class Engine:
             plan.use_stream(stream)
             self._mark(plan, *names)
             self._emit_allreduce(plan, lo, hi, side_dep=False, on_main=True, packed=self.opt_fused)
+            declare(a0, {f"grad:{b}"})
 
         early = set()
         for b, (lo, hi, names) in enumerate(ranges[:-1]):
             plan.use_stream(2)                 # (_emit_reduce/_emit_allreduce end on main)
-            self._device_deps[plan.size()] = bwd_op
+            self._device_deps[plan.size()] = (bwd_op, {f"grad:{b}", f"param:{b}", "lr", "gstep"})
             plan.prn_bucket_wait(self.prn_bar, b, self.prn.bucket_target(b), err)
-            bucket(lo, hi, names, 2)
+            bucket(b, lo, hi, names, 2)
             if self.opt_fused:
                 # the bucket's parameters updated right behind its all-reduce, still beside
                 # the backward: it has finished with them (their stage's dgrads and BN
                 # backwards precede the count that released this bucket); global_step is
                 # stepped by the last update launch
                 plan.use_stream(2)
+                a0 = plan.size()
                 self._emit_update(plan, set(names), self._packed_gin(), step=False)
+                declare(a0, {f"grad:{b}", f"param:{b}", "lr", "gstep"})
                 plan.use_stream(0)
                 early |= set(names)
         join = plan.new_event()
@@ -1601,7 +1615,7 @@ class Engine:
         plan.use_stream(0)
         plan.wait(join)
         self._t_bwd_done = plan.timing_point("bwd_compute_done")
-        bucket(*ranges[-1], 0)                 # the last bucket behind the backward, in order
+        bucket(len(ranges) - 1, *ranges[-1], 0)   # the last bucket behind the backward, in order
         for bi in range(len(self.buckets)):
             self._flushed.add(bi)
         self._t_joined = plan.timing_point("allreduce_joined")

@@ -36,13 +36,21 @@ R4  collectives: an all-reduce (or a host split point, `barriers`: an index
     `Plan.run` calls) is ordered after EVERY launch queued before it in the
     plan, on every stream -- the bucket it reads is complete, whichever stream
     produced its gradients.
+R5  partial device dependencies: see below.
 
-Device-side dependencies (`device_deps` {op: producer op}): a launch that waits on the
-device for a producer launch on another stream to publish its part (the persistent
-backward's bucket counters: engine.py `_emit_persist_overlap`, the one-wave
-`prn_bucket_wait` kernel) orders everything after it on its stream after the producer,
-as far as this structural check is concerned -- the producer's kernel publishes that
-bucket complete (write-through stores drained before the count) while it still runs.
+Device-side dependencies (`device_deps` {op: producer op} or {op: (producer op,
+covered buffers)}): a launch that waits on the device for a producer launch on another
+stream to publish its part (the persistent backward's bucket counters: engine.py
+`_emit_persist_overlap`, the one-wave `prn_bucket_wait` kernel).  A bare producer index
+orders everything after the wait on its stream after the WHOLE producer.  With a set of
+covered buffer names the ordering is partial -- the producer still runs and still uses
+other buffers: until that stream is ordered after the producer by an event, every launch
+after the wait must declare the buffers it reads or writes (`op_buffers` {op: names}) and
+touch only buffers some earlier wait on its stream covered (R5); a collective among them
+satisfies R4 against the producer only through that coverage.  What a count covers (the
+bucket's gradients, slabs and parameters, which the producer publishes complete and no
+longer reads after the count) is the engine's claim; this check holds the comm stream's
+ops to it (a misassigned bucket or a weight the backward still reads is caught).
 
 Op encoding (`Plan.op_kinds` / `op_streams` / `op_events`): kind 0 launch,
 1 record, 2 wait, 3 timing probe (ignored); stream 0 main, 1 side, 2 comm.
@@ -60,7 +68,8 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
                      segments: Iterable[Tuple[str, int, int]],
                      names: Sequence[str] | None = None,
                      barriers: Sequence[int] = (),
-                     device_deps: Dict[int, int] | None = None) -> List[str]:
+                     device_deps: Dict[int, object] | None = None,
+                     op_buffers: Dict[int, Iterable[str]] | None = None) -> List[str]:
     """Return a list of human-readable violations (empty = ordering is sound).
 
     ``barriers``: plan indices where the host runs a collective on the main
@@ -87,10 +96,22 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
         forked = [True, False, False]
         launched = [-1] * NSTREAMS
         reported_fork = [False] * NSTREAMS
+        # partial[s]: (producer op, buffers covered so far) of the device waits on stream s
+        # whose producer stream s is not yet ordered after
+        partial: Dict[int, Tuple[int, set]] = {}
+
+        def bufs(i: int):
+            got = (op_buffers or {}).get(i)
+            return None if got is None else set(got)
 
         def r4(i: int, s: int, what: str):
             for t in range(NSTREAMS):
                 if t != s and launched[t] > clock[s][t]:
+                    p = partial.get(s)
+                    b = bufs(i)
+                    if (p is not None and launched[t] == p[0] and b is not None
+                            and b <= p[1]):
+                        continue   # ordered after the producer's covered part (R5)
                     errs.append(f"{seg}: {what} at {op(i)} is not ordered after {op(launched[t])} "
                                 f"on stream {t} (R4)")
 
@@ -117,13 +138,35 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
                 forked[s] = forked[s] or src[2]
             elif k == LAUNCH:
                 dep = (device_deps or {}).get(i)
+                covered = None
+                if isinstance(dep, tuple):
+                    dep, covered = dep[0], set(dep[1])
+                p = partial.get(s)
+                if p is not None and clock[s][streams[p[0]]] >= p[0]:
+                    partial.pop(s)   # an event has since ordered s after the whole producer
+                    p = None
                 if dep is not None:
                     if not (a <= dep < i) or kinds[dep] != LAUNCH or streams[dep] == s:
                         errs.append(f"{seg}: device dependency of {op(i)} on {op(dep)} is not "
                                     f"an earlier launch of this segment on another stream")
-                    else:
+                    elif covered is None:
                         t = streams[dep]
                         clock[s][t] = max(clock[s][t], dep)
+                    elif p is not None and p[0] != dep:
+                        errs.append(f"{seg}: {op(i)} adds a partial device dependency on "
+                                    f"{op(dep)} beside one on {op(p[0])} (R5)")
+                    else:
+                        partial[s] = (dep, (p[1] if p is not None else set()) | covered)
+                        p = partial[s]
+                elif p is not None:
+                    b = bufs(i)
+                    if b is None:
+                        errs.append(f"{seg}: {op(i)} runs beside {op(p[0])} (a partial device "
+                                    f"dependency) without declaring its buffers (R5)")
+                    elif not b <= p[1]:
+                        errs.append(f"{seg}: {op(i)} touches {sorted(b - p[1])} while "
+                                    f"{op(p[0])} may still use them: only {sorted(p[1])} are "
+                                    f"covered by the device waits before it (R5)")
                 if s != 0 and not forked[s] and not reported_fork[s]:
                     errs.append(f"{seg}: stream-{s} {op(i)} before any fork from the main "
                                 f"stream (R2)")
@@ -142,8 +185,9 @@ def check_plan_order(kinds: Sequence[int], streams: Sequence[int], events: Seque
 
 
 def check_plan(plan, segments: Dict[str, Tuple[int, int]], barriers: Sequence[int] = (),
-               device_deps: Dict[int, int] | None = None) -> List[str]:
+               device_deps: Dict[int, object] | None = None,
+               op_buffers: Dict[int, Iterable[str]] | None = None) -> List[str]:
     """`check_plan_order` over a native `_C.Plan` and the engine's {name: (a, b)}."""
     return check_plan_order(plan.op_kinds(), plan.op_streams(), plan.op_events(),
                             [(k, a, b) for k, (a, b) in segments.items()], plan.names(),
-                            barriers=barriers, device_deps=device_deps)
+                            barriers=barriers, device_deps=device_deps, op_buffers=op_buffers)

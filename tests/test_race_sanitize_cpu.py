@@ -186,6 +186,40 @@ def test_streamcheck_device_dependency_orders_bucket_wait():
         assert any("device dependency" in x for x in errs), (dep, errs)
 
 
+def test_streamcheck_partial_device_dependency_holds_ops_to_covered_buffers():
+    """a bucket wait orders the comm stream after the backward launch's COVERED
+    buffers only (the bucket's gradients and parameters): the ops after it must declare
+    their buffers and stay inside the coverage until an event orders the stream after
+    the whole launch (R5); the all-reduce satisfies R4 only through that coverage."""
+    # main: fwd, record e0 | comm: wait e0, head | main: bwd (4) | comm: bucket wait (5),
+    # pack (6), all_reduce (7), update (8), record e1 | main: wait e1, optimizer
+    ops = [(LAUNCH, 0, -1), (RECORD, 0, 0), (WAIT, 2, 0), (LAUNCH, 2, -1), (LAUNCH, 0, -1),
+           (LAUNCH, 2, -1), (LAUNCH, 2, -1), (LAUNCH, 2, -1), (LAUNCH, 2, -1), (RECORD, 2, 1),
+           (WAIT, 0, 1), (LAUNCH, 0, -1)]
+    k, s, e = _plan(ops)
+    seg = [("bwd", 0, len(k))]
+    names = _names(len(k), [7])
+    dep = {5: (4, {"grad:0", "param:0", "lr"})}
+    good = {6: {"grad:0"}, 7: {"grad:0"}, 8: {"grad:0", "param:0", "lr"}}
+    assert check_plan_order(k, s, e, seg, names=names, device_deps=dep, op_buffers=good) == []
+    # an update of a parameter the backward may still read (a misassigned bucket): R5
+    bad = {**good, 8: {"grad:0", "param:1"}}
+    errs = check_plan_order(k, s, e, seg, names=names, device_deps=dep, op_buffers=bad)
+    assert any("(R5)" in x and "param:1" in x for x in errs), errs
+    # an op with no declared buffers beside the running producer: R5
+    errs = check_plan_order(k, s, e, seg, names=names, device_deps=dep,
+                            op_buffers={7: {"grad:0"}, 8: {"grad:0"}})
+    assert any("(R5)" in x and "without declaring" in x for x in errs), errs
+    # the all-reduce of a range the waits do not cover races the backward: R4
+    errs = check_plan_order(k, s, e, seg, names=names, device_deps=dep,
+                            op_buffers={**good, 7: {"grad:1"}})
+    assert any("(R4)" in x and "all_reduce" in x for x in errs), errs
+    # a second bucket wait widens the coverage
+    dep2 = {5: (4, {"grad:0"}), 6: (4, {"grad:1", "param:1"})}
+    ok2 = {7: {"grad:1"}, 8: {"grad:0", "param:1"}}
+    assert check_plan_order(k, s, e, seg, names=names, device_deps=dep2, op_buffers=ok2) == []
+
+
 def test_streamcheck_host_split_needs_join():
     """gloo rehearsal: the host all-reduces between Plan.run calls at a split index;
     a side-stream launch queued before the split but joined only later is a race
