@@ -17,7 +17,7 @@ from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_sche
 
 def build(N, comm, overlap):
     os.environ["DTR_TUNE"] = f"persist_overlap={overlap}"
-    kw = dict(native_comm=True, allreduce_dtype="bf16") if comm else {}
+    kw = dict(native_comm=True, allreduce_dtype=os.environ.get("COMM_DTYPE", "bf16")) if comm else {}
     eng = Engine(cifar_spec(50), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
                  device=torch.device("cuda", 0), use_graph=False, **kw)
     del os.environ["DTR_TUNE"]
