@@ -227,13 +227,13 @@ __device__ __forceinline__ int opaque_s(int v) {
 }
 
 // ---- grid barrier ---------------------------------------------------------------------
-// Arrival counters sharded over PRN_SHARDS cache lines: workgroup b adds to line b % 8 (one
-// XCD per line under round-robin placement), and the waiters poll all 8 lines with ONE
-// 8-lane load.  One shared counter serialises its arrivals at the memory side (~12 ns
+// Arrival counters sharded over up to PRN_SHARDS cache lines: workgroup b adds to line
+// b % shards (8 or 64, prn_shards; with 8, one XCD per line under round-robin placement),
+// and the waiters poll all lines with ONE load, one lane per line.  One shared counter serialises its arrivals at the memory side (~12 ns
 // each) and its pollers contend with them: microbench/bn_barrier.hip, profiles/bn_barrier.md
 // -- a BN barrier (sums, drain, arrive, wait, sums read) at 128 workgroups 3.94 -> 2.72 us,
 // at 256 8.85 -> 4.86 us, at 64 2.31 -> 2.07 us.
-constexpr int PRN_SHARDS = 8, PRN_LINE = 32;   // 32 words = one 128-B line per shard
+constexpr int PRN_SHARDS = 64, PRN_LINE = 32;   // (max shards) 32 words = one 128-B line per shard
 // bar layout (words): forward shards at PRN_FWD + 32 s, backward shards at PRN_BWD + 32 s,
 // the backward readiness count at PRN_READY, the weight-gradient item queue at PRN_QUEUE
 // (each on its own line; PRN_BAR_WORDS in all, zeroed every step)
@@ -1945,7 +1945,17 @@ static_assert(wg_lds(16, 16, 1, 32) <= LDS_TOTAL && wg_lds(32, 16, 2, 16) <= LDS
                   wg_lds(16, 8, 1, 32) <= LDS_TOTAL,
               "weight-gradient LDS");
 
-static int prn_shards() { return tune(T_PRN_SHARDS) == 1 ? 1 : PRN_SHARDS; }
+// Arrival shards of a launch whose barriers N x P slices arrive at.  Auto (tune -1): 64
+// (about two arrivals per line) when 128 or more slices of at most half an image each
+// arrive together, else 8 -- more lines cost every poll (one load per line) and pay only
+// where the arrivals cluster.  Same-process A/B, step ms, 8 / 32 / 64 shards (scripts/
+// tune_ab.py): bs16 0.5573 / 0.5592 / 0.5598, bs32 0.5764 / 0.5710 / 0.5676, bs64 0.6439
+// / 0.6434 / 0.6409, bs128 (one slice per image) 0.7332 / 0.7323 / 0.7351.
+static int prn_shards(int N, int P) {
+  const long t = tune(T_PRN_SHARDS);
+  if (t == 1 || t == 8 || t == 16 || t == 32 || t == 64) return (int)t;
+  return N * P >= 128 && P >= 2 ? 64 : 8;
+}
 
 static size_t prn_head_lds(int N, int kpad) {
   return 1024 + 32 + (size_t)N * ((64 + kpad) * sizeof(bf16) + (kpad + 2) * sizeof(float)) +
@@ -1985,7 +1995,7 @@ void prn_forward(const PrnArgs& a, hipStream_t s) {
     throw std::invalid_argument("prn_forward: unsupported shape (N x P <= CUs, 3n blocks, <= 64 classes)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  b.shards = prn_shards();
+  b.shards = prn_shards(a.N, a.P);
   if (a.P == 1) hipLaunchKernelGGL(prn_fwd_kernel<1>, dim3(a.N), dim3(PT), LDS_TOTAL, s, b);
   else if (a.P == 2) hipLaunchKernelGGL(prn_fwd_kernel<2>, dim3(a.N * 2), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_fwd_kernel<4>, dim3(a.N * 4), dim3(PT), LDS_TOTAL, s, b);
@@ -2017,7 +2027,7 @@ void prn_backward(const PrnArgs& a, int wgrad_wgs, hipStream_t s) {
     throw std::invalid_argument("prn_backward: the grid must be co-resident (<= one per CU)");
   PrnArgs b = a;
   b.probe = g_prn_probe;
-  b.shards = prn_shards();
+  b.shards = prn_shards(a.N, a.P);
   if (a.P == 1) hipLaunchKernelGGL(prn_bwd_kernel<1>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   else if (a.P == 2) hipLaunchKernelGGL(prn_bwd_kernel<2>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);
   else hipLaunchKernelGGL(prn_bwd_kernel<4>, dim3(grid), dim3(PT), LDS_TOTAL, s, b);

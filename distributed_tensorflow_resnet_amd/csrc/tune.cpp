@@ -76,9 +76,10 @@ const TuneEntry kTable[T_COUNT] = {
     {"ring_kt_dgrad", 4,
      "ring dgrads from this many 64-deep K tiles (the 4-tile 14x14 1024->256 dgrad: 75.8 -> "
      "68.8 us on the ring)"},
-    {"prn_shards", 8,
+    {"prn_shards", -1,
      "arrival-counter shards (one 128-B line each, workgroup b on b % shards) of the persistent "
-     "CIFAR step's grid barriers: 8 or 1 (profiles/bn_barrier.md)"},
+     "CIFAR step's grid barriers: -1 auto (64 when >= 128 slices of <= half an image arrive, "
+     "else 8), or 1, 8, 16, 32, 64 (profiles/bn_barrier.md)"},
 };
 
 std::atomic<long> g_val[T_COUNT];
