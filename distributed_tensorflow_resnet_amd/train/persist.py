@@ -64,15 +64,16 @@ AUTO_MAX_BATCH = 240
 
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
-    """Row slices (workgroups) per image of the backward: 4 up to 32 images, 2 up to 64,
-    else 1 (MI355X, CIFAR RN50 step ms: bs24 0.637 at 4 / 0.712 at 2; bs32 0.670 at 4 /
-    0.712 at 2; bs48 0.757 at 4 / 0.733 at 2; bs64 0.836 at 2 / 0.893 at 1; bs96 1.025
-    at 2 / 0.998 at 1 -- more slices shorten each layer, more arrivals lengthen each
-    barrier and leave fewer CUs for the weight gradients).  The engine's tune
-    persist_slices overrides."""
+    """Row slices (workgroups) per image of the backward: 4 while 4N slices leave 32 CUs
+    for the weight gradients (56 images on 256 CUs), 2 up to 64, else 1.  More slices
+    shorten each layer, more arrivals lengthen each barrier; with the 64-shard arrival
+    counters of round 6 the 4-slice backward wins wherever it fits (MI355X, CIFAR RN50
+    step ms, forward slicing fixed at 2: bs40 0.594-0.600 at 4 / 0.626-0.632 at 2; bs48
+    0.607-0.608 / 0.634; bs56 0.626-0.628 / 0.636-0.638; older: bs64 0.836 at 2 / 0.893
+    at 1, bs96 1.025 at 2 / 0.998 at 1).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
-    if N <= 32 and 4 * N + 32 <= cus:
+    if 4 * N + 32 <= cus:
         return 4
     return 2 if N <= 64 and 2 * N + 32 <= cus else 1
 
@@ -80,14 +81,15 @@ def slices_for(N: int, cus: int, override: int = -1) -> int:
 def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:
     """Row slices per image of the forward launch.  The forward has no weight-gradient
     workgroups to leave CUs for, and its slicing is independent of the backward's (both
-    launches exchange only whole NHWC tensors and global BN sums): 4 up to 32 images,
-    2 while 2N slices fill at most 3/4 of the CUs, else 1 (MI355X, CIFAR RN50 forward:
-    bs32 0.294 ms at 4 / 0.302 at 2, bs48 0.343 / 0.315; step bs96 0.961 -> 0.918 ms with
-    a 2-slice forward; bs128's 256-workgroup forward ran 0.58 ms against 0.43 at 1
-    slice).  The engine's tune persist_slices overrides."""
+    launches exchange only whole NHWC tensors and global BN sums): 4 while 4N slices fill
+    less than 3/4 of the CUs (47 images on 256), 2 while 2N do, else 1 (MI355X, CIFAR RN50
+    step ms with a 4-slice backward: bs40 0.584-0.587 at 4 / 0.594-0.600 at 2; bs48
+    0.609-0.610 / 0.607-0.608; bs56 0.643-0.644 / 0.626-0.628; older: step bs96 0.961 ->
+    0.918 ms with a 2-slice forward; bs128's 256-workgroup forward ran 0.58 ms against
+    0.43 at 1 slice).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
-    if N <= 32 and 4 * N <= cus:
+    if 16 * N < 3 * cus:
         return 4
     return 2 if 8 * N <= 3 * cus else 1
 
@@ -117,10 +119,10 @@ def check(eng) -> str:
         if (b.proj is not None) != first or b.stride != (2 if first and stage else 1):
             return "projection / stride layout is not the CIFAR v2 one"
     cus = nat.cu_count()   # this process's CUs (its CU mask, apply_cu_partition)
-    P = slices_for(eng.N, cus, eng.persist_slices)
     # (at least 16 CUs left for the weight-gradient workgroups, beside the overlap
-    # plan's reserve for the comm stream)
+    # plan's reserve for the comm stream; the backward slices by what is left)
     reserve = OVERLAP_RESERVE_CUS if overlap_planned(eng) else 0
+    P = slices_for(eng.N, cus - reserve, eng.persist_slices)
     if eng.N * P + 16 + reserve > cus:
         return (f"{eng.N} x {P} slices + {reserve} reserved CUs leave fewer than 16 of "
                 f"{cus} CUs for the weight gradients")
@@ -199,9 +201,11 @@ class PersistStep:
             r["acc"], r["bacc"] = e.acc.data_ptr(), e.bacc.data_ptr()
         self.bn_dev = self._dev(bn_rows)
         self.cus = nat.cu_count()   # this process's CUs (its CU mask)
-        self.P = slices_for(N, self.cus, eng.persist_slices)          # backward
-        self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
         self.overlap = bool(getattr(eng, "persist_overlap", False))
+        # the backward grid leaves the overlap plan's reserve to the comm stream
+        self.P = slices_for(N, self.cus - (OVERLAP_RESERVE_CUS if self.overlap else 0),
+                            eng.persist_slices)                       # backward
+        self.P_fwd = fwd_slices_for(N, self.cus, eng.persist_slices)  # forward
         # barrier-timeout flag: slot 4 of the engine's scalars, so the host read of the
         # logged metrics (Engine.metrics) sees it at no extra cost; never cleared by the
         # kernels (Engine.clear_persist_error)

@@ -43,7 +43,7 @@ def _pair(monkeypatch, spec, N, gpu, slices=-1):
 
 
 @pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (20, 32, 2), (50, 16, 4), (20, 16, 1),
-                                           (8, 64, 2)])
+                                           (8, 64, 2), (8, 40, 4)])
 def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N, slices):
     """Saved activations, batch statistics and head outputs of the one-launch forward
     vs the per-layer forward (same weights, same batch): bf16-rounding agreement, for
@@ -71,7 +71,8 @@ def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N, slices)
     assert _rel(ep.params.stats, er.params.stats) < 1e-3   # moving averages
 
 
-@pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (8, 32, 2), (8, 16, 1), (8, 48, 2)])
+@pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (8, 32, 2), (8, 16, 1), (8, 48, 2),
+                                           (8, 56, 4)])
 def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N, slices):
     """Whole training step (forward + backward + slab reduces): per-tensor gradients
     vs the bf16-emulating fp32 oracle, like test_engine_step_matches_autograd_shallow."""
@@ -134,7 +135,8 @@ def test_persistent_step_within_bf16_noise_deep(gpu, monkeypatch, size, N):
     assert torch.isfinite(ep.grad).all()
 
 
-@pytest.mark.parametrize("size,N,slices", [(20, 16, 4), (20, 32, 2), (50, 128, 1)])
+@pytest.mark.parametrize("size,N,slices", [(20, 16, 4), (20, 32, 2), (50, 128, 1),
+                                           (8, 56, 4)])
 def test_persistent_step_bitwise_under_concurrent_load(gpu, monkeypatch, size, N, slices):
     """Race stress for the hand-off protocol (write-through publishes, drained arrives,
     sc1 reads, the weight-gradient readiness line): while the persistent launches run,
