@@ -65,33 +65,35 @@ AUTO_MAX_BATCH = 240
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
     """Row slices (workgroups) per image of the backward: 4 while 4N slices leave 32 CUs
-    for the weight gradients (56 images on 256 CUs), 2 up to 64, else 1.  More slices
-    shorten each layer, more arrivals lengthen each barrier; with the 64-shard arrival
-    counters of round 6 the 4-slice backward wins wherever it fits (MI355X, CIFAR RN50
-    step ms, forward slicing fixed at 2: bs40 0.594-0.600 at 4 / 0.626-0.632 at 2; bs48
-    0.607-0.608 / 0.634; bs56 0.626-0.628 / 0.636-0.638; older: bs64 0.836 at 2 / 0.893
-    at 1, bs96 1.025 at 2 / 0.998 at 1).  The engine's tune persist_slices overrides."""
+    for the weight gradients (56 images on 256 CUs), 2 while 2N leave 64 (96 images),
+    else 1.  More slices shorten each layer, more arrivals lengthen each barrier; with
+    the 64-shard arrival counters of round 6 (MI355X, CIFAR RN50 step ms, two runs each;
+    forward slicing fixed: bs40 0.594-0.600 at 4 / 0.626-0.632 at 2; bs48 0.607-0.608 /
+    0.634; bs56 0.626-0.628 / 0.636-0.638; bs64 0.639-0.641 at 2 / 0.673-0.675 at 1;
+    bs80 0.654 / 0.680-0.687; bs96 0.675-0.676 / 0.695-0.701; bs112 0.735-0.737 /
+    0.717-0.724).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
     if 4 * N + 32 <= cus:
         return 4
-    return 2 if N <= 64 and 2 * N + 32 <= cus else 1
+    return 2 if 2 * N + 64 <= cus else 1
 
 
 def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:
     """Row slices per image of the forward launch.  The forward has no weight-gradient
     workgroups to leave CUs for, and its slicing is independent of the backward's (both
     launches exchange only whole NHWC tensors and global BN sums): 4 while 4N slices fill
-    less than 3/4 of the CUs (47 images on 256), 2 while 2N do, else 1 (MI355X, CIFAR RN50
-    step ms with a 4-slice backward: bs40 0.584-0.587 at 4 / 0.594-0.600 at 2; bs48
-    0.609-0.610 / 0.607-0.608; bs56 0.643-0.644 / 0.626-0.628; older: step bs96 0.961 ->
-    0.918 ms with a 2-slice forward; bs128's 256-workgroup forward ran 0.58 ms against
-    0.43 at 1 slice).  The engine's tune persist_slices overrides."""
+    less than 3/4 of the CUs (47 images on 256), 2 while 2N leave 16 (120 images), else 1
+    (MI355X, CIFAR RN50 step ms, two runs each, backward slicing fixed: bs40 0.584-0.587
+    at 4 / 0.594-0.600 at 2; bs48 0.609-0.610 / 0.607-0.608; bs56 0.643-0.644 /
+    0.626-0.628; bs64 0.639-0.641 at 2 / 0.689-0.690 at 1; bs96 0.675-0.676 /
+    0.703; bs112 0.719-0.723 / 0.729; bs120 0.730-0.731 / 0.733-0.734; bs128 0.746-0.749
+    / 0.740-0.742).  The engine's tune persist_slices overrides."""
     if override in (1, 2, 4):
         return override
     if 16 * N < 3 * cus:
         return 4
-    return 2 if 8 * N <= 3 * cus else 1
+    return 2 if 2 * N + 16 <= cus else 1
 
 
 def check(eng) -> str:

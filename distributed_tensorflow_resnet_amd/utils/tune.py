@@ -54,8 +54,9 @@ ENGINE = {
                     "one workgroup per image row slice; train/persist.py): -1 auto = per-rank "
                     "batch <= 240, 0 off, 1 whenever the network is supported"),
     "persist_slices": (-1, "row slices per image of the persistent step: -1 auto (backward: 4 "
-                           "while 4N + 32 <= CUs, 2 up to 64 images, else 1; forward: 4 while "
-                           "4N < 3/4 of the CUs, 2 while 2N <= 3/4, else 1), 1, 2 or 4 for both"),
+                           "while 4N + 32 <= CUs, 2 while 2N + 64 <= CUs, else 1; forward: 4 "
+                           "while 4N < 3/4 of the CUs, 2 while 2N + 16 <= CUs, else 1), 1, 2 "
+                           "or 4 for both"),
     "persist_overlap": (1, "world > 1: the persistent step's first two stage buckets packed, "
                            "all-reduced and updated on the comm stream while the backward launch "
                            "runs (48 CUs left out of its grid), the last after it on the main "

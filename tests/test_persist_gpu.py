@@ -43,7 +43,7 @@ def _pair(monkeypatch, spec, N, gpu, slices=-1):
 
 
 @pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (20, 32, 2), (50, 16, 4), (20, 16, 1),
-                                           (8, 64, 2), (8, 40, 4)])
+                                           (8, 64, 2), (8, 40, 4), (8, 112, 2)])
 def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N, slices):
     """Saved activations, batch statistics and head outputs of the one-launch forward
     vs the per-layer forward (same weights, same batch): bf16-rounding agreement, for
@@ -72,7 +72,7 @@ def test_persistent_forward_matches_per_layer(gpu, monkeypatch, size, N, slices)
 
 
 @pytest.mark.parametrize("size,N,slices", [(8, 16, 4), (8, 32, 2), (8, 16, 1), (8, 48, 2),
-                                           (8, 56, 4)])
+                                           (8, 56, 4), (8, 96, 2)])
 def test_persistent_step_matches_autograd(gpu, monkeypatch, size, N, slices):
     """Whole training step (forward + backward + slab reduces): per-tensor gradients
     vs the bf16-emulating fp32 oracle, like test_engine_step_matches_autograd_shallow."""
