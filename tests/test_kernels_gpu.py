@@ -212,17 +212,21 @@ def test_head_pool_xent(gpu):
                                rtol=1e-2, atol=1e-3)
 
 
-def test_maxpool(gpu):
+@pytest.mark.parametrize("H,k,stride", [(112, 3, 2), (113, 3, 2), (15, 3, 2), (56, 3, 1), (28, 2, 2)])
+def test_maxpool(gpu, H, k, stride):
+    """TF SAME max pool vs the padded PyTorch pool: the stem's 3x3 / 2, odd sizes (a top /
+    left pad of 1), stride 1 and a 2x2 window."""
     torch.manual_seed(8)
-    x = torch.randn(2, 112, 112, 64, device=gpu).to(BF)
-    y, am = fn.maxpool_fwd(x)
+    x = torch.randn(2, H, H, 64, device=gpu).to(BF)
+    y, am = fn.maxpool_fwd(x, k, stride)
     xf = x.float().requires_grad_(True)
-    r = ref.max_pool_same(xf)
-    assert y.shape == r.shape == (2, 56, 56, 64)
+    r = ref.max_pool_same(xf, k, stride)
+    Ho = -(-H // stride)
+    assert y.shape == r.shape == (2, Ho, Ho, 64)
     torch.testing.assert_close(y.float(), r.detach())
     dy = torch.randn_like(r).to(BF)
     r.backward(dy.float())
-    dx = fn.maxpool_bwd(am, dy, tuple(x.shape))
+    dx = fn.maxpool_bwd(am, dy, tuple(x.shape), k, stride)
     assert _rel(dx, xf.grad) < 1e-2
 
 
