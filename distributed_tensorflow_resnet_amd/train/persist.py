@@ -64,9 +64,10 @@ AUTO_MAX_BATCH = 240
 
 
 def slices_for(N: int, cus: int, override: int = -1) -> int:
-    """Row slices (workgroups) per image of the backward: 4 while 4N slices leave 32 CUs
-    for the weight gradients (56 images on 256 CUs), 2 while 2N leave 64 (96 images),
-    else 1.  More slices shorten each layer, more arrivals lengthen each barrier; with
+    """Row slices (workgroups) per image of the backward, of the ``cus`` the backward grid
+    may fill (the overlap plan's reserve already taken out): 4 while 4N slices leave 32
+    CUs for the weight gradients (56 images on 256 CUs), 2 while 2N leave 64 (96
+    images), else -- small budgets -- the most slices that leave 16, else 1.  More slices shorten each layer, more arrivals lengthen each barrier; with
     the 64-shard arrival counters of round 6 (MI355X, CIFAR RN50 step ms, two runs each;
     forward slicing fixed: bs40 0.594-0.600 at 4 / 0.626-0.632 at 2; bs48 0.607-0.608 /
     0.634; bs56 0.626-0.628 / 0.636-0.638; bs64 0.639-0.641 at 2 / 0.673-0.675 at 1;
@@ -76,7 +77,14 @@ def slices_for(N: int, cus: int, override: int = -1) -> int:
         return override
     if 4 * N + 32 <= cus:
         return 4
-    return 2 if 2 * N + 64 <= cus else 1
+    if 2 * N + 64 <= cus:
+        return 2
+    # small CU budgets (a rank on a CU partition, after the overlap reserve): slices
+    # before weight-gradient CUs, down to the 16 the check requires (two ranks on CU
+    # halves, 16 images per rank: P = 4 with 16 weight-gradient CUs, 1.16 ms/step)
+    if N <= 32 and 4 * N + 16 <= cus:
+        return 4
+    return 2 if N <= 64 and 2 * N + 16 <= cus else 1
 
 
 def fwd_slices_for(N: int, cus: int, override: int = -1) -> int:

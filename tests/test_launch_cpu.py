@@ -107,7 +107,9 @@ def test_persistent_slice_selection():
     from distributed_tensorflow_resnet_amd.train.persist import fwd_slices_for, slices_for
 
     assert [slices_for(n, 256) for n in (8, 16, 32, 48, 56, 64, 96, 112, 128, 224)] == [4, 4, 4, 4, 4, 2, 2, 1, 1, 1]
-    assert [slices_for(n, 128) for n in (16, 24, 32, 48, 96)] == [4, 4, 2, 1, 1]
+    assert [slices_for(n, 128) for n in (16, 24, 32, 48, 96)] == [4, 4, 2, 2, 1]
+    # a rank on a CU half after the overlap reserve (128 - 48)
+    assert [slices_for(n, 80) for n in (8, 16, 24, 32, 64)] == [4, 4, 2, 2, 1]
     assert [fwd_slices_for(n, 256) for n in (8, 16, 32, 40, 47, 48, 64, 96, 120, 128, 200)] == [4, 4, 4, 4, 4, 2, 2, 2, 2, 1, 1]
     assert slices_for(128, 256, 2) == 2 and fwd_slices_for(16, 256, 1) == 1
     for n in range(1, 241):
