@@ -107,14 +107,13 @@ def main():
             "dgrad": (lambda: fn.conv2d_dgrad(dy, whwio, tuple(x.shape), s, out=dx, bnb=bnb,
                                               bfin=[bacc]),
                       yb + wb + 2 * xb),
-            "wgrad": (lambda: fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, pre_scale=sc,
-                                              pre_shift=sh),
+            "wgrad": (lambda: fn.conv2d_wgrad(dy, x, k, k, s, grad_hwio=gw, **pre),
                       yb + xb + 2 * slab + K * k * k * C * 4),
         }
         for p, (f, byts) in passes.items():
             if p == "dgrad" and C < 64:
                 continue
-            name = f"{H}x{H} {C}->{K} {k}x{k}/{s}" + (" PRE" if p == "fwd" and pre else "")
+            name = f"{H}x{H} {C}->{K} {k}x{k}/{s}" + (" PRE" if p != "dgrad" and pre else "")
             if manifest:
                 manifest.write(f"{name}|{p}|{reps + 1}|{byts}|{flop}\n")
                 manifest.flush()
@@ -159,8 +158,8 @@ def main():
     print(f"# ImageNet ResNet-50 v2 conv roofline, N = {N}, 1x MI355X\n")
     print("Floor = max(FLOP / 2.3 PF/s, unique bytes / 5 TB/s); unique bytes count each operand "
           "once (dgrad: dy, W, dx and the BN input x its epilogue reads; wgrad: dy, x, the fp32 "
-          "split-K slabs written and read back, dW).  Forward convs take the BN+ReLU prologue "
-          "(PRE) where the engine does.  `scripts/roofline.py`, HIP-event medians.\n")
+          "split-K slabs written and read back, dW).  Forward and weight-gradient convs take "
+          "the BN+ReLU prologue on their input (PRE) where the engine does.  `scripts/roofline.py`, HIP-event medians.\n")
     print("| layer | pass | x/step | GFLOP | MB | floor us | achieved us | x floor | TF/s | TB/s |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for name, p, cnt, flop, byts, floor, us in rows:
