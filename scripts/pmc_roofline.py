@@ -14,7 +14,7 @@ import csv
 import re
 import sys
 
-OURS = re.compile(r"conv_gemm_kernel|conv3x3_direct_kernel|conv_wgrad|wgrad_reduce")
+OURS = re.compile(r"conv_gemm_kernel|conv_ring_kernel|conv3x3_direct_kernel|conv_wgrad|wgrad_reduce")
 
 
 def load(path):
