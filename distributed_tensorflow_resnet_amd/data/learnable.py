@@ -51,14 +51,21 @@ def make_images(rng, templates, labels, noise=45.0, shift=3):
 
 
 def make_learnable_cifar(out_dir: str, n_train: int = 10000, n_test: int = 2000, seed: int = 0,
-                         num_classes: int = 10) -> dict:
+                         num_classes: int = 10, noise: float = 45.0, shift: int = 3,
+                         separation: float = 1.0) -> dict:
+    """``separation`` < 1 blends every class template with one field common to all
+    classes (template = (1 - s) * common + s * own), which with more ``noise`` / ``shift``
+    makes the classes confusable: a task a deep network does not solve perfectly."""
     rng = np.random.default_rng(seed)
     templates = _smooth_fields(rng, num_classes)
+    if separation != 1.0:
+        common = _smooth_fields(rng, 1)
+        templates = (1.0 - separation) * common + separation * templates
     os.makedirs(out_dir, exist_ok=True)
     ytr = rng.integers(0, num_classes, n_train)
     yte = rng.integers(0, num_classes, n_test)
-    xtr = make_images(rng, templates, ytr)
-    xte = make_images(rng, templates, yte)
+    xtr = make_images(rng, templates, ytr, noise, shift)
+    xte = make_images(rng, templates, yte, noise, shift)
     parts = np.array_split(np.arange(n_train), 5)
     for i, idx in enumerate(parts, start=1):
         write_records(os.path.join(out_dir, f"data_batch_{i}.bin"), xtr[idx], ytr[idx])
@@ -73,8 +80,13 @@ def main(argv=None):
     ap.add_argument("--train", type=int, default=10000)
     ap.add_argument("--test", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--noise", type=float, default=45.0, help="per-pixel noise sigma")
+    ap.add_argument("--shift", type=int, default=3, help="max template shift (pixels)")
+    ap.add_argument("--separation", type=float, default=1.0,
+                    help="class-template weight against a common field (1: none common)")
     a = ap.parse_args(argv)
-    print(make_learnable_cifar(a.out_dir, a.train, a.test, a.seed))
+    print(make_learnable_cifar(a.out_dir, a.train, a.test, a.seed, noise=a.noise, shift=a.shift,
+                               separation=a.separation))
 
 
 if __name__ == "__main__":
