@@ -228,35 +228,57 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
     # (pad/crop/flip/standardize), ImageNet flips / mean-subtracts / packs random
     # uint8 224x224 crops into the stem's bf16 layout (imagenet_u8_pack)
     input_mode = "cifar_u8" if dataset.startswith("cifar") else "imagenet_u8"
-    eng = Engine(spec, per_rank, weight_decay=wd, lr_schedule=sched, device=device,
-                 dist_ctx=ctx, global_batch=global_batch, bucket_mb=args.bucket_mb,
-                 seed=0, data_seed=1234 + ctx.rank, use_graph=use_graph,
-                 allreduce_dtype=args.allreduce_dtype, input_mode=input_mode)
-    dog = CommWatchdog(eng.comm, args.step_timeout, 3 * args.step_timeout).start()
-    eng.broadcast_parameters(0)
-    eng.fill_synthetic(seed=ctx.rank)
+    # A persistent-step grid barrier that times out (workgroups not co-resident beside
+    # the job's other kernels) flags the step instead of hanging, and its numbers are
+    # garbage.  World > 1 then measures again, all ranks together, on the next plan down
+    # -- the persistent step without the comm-stream overlap, then the per-layer plan --
+    # and records why (`fallback`); one GPU reports the failure.
+    base_tune = os.environ.get("DTR_TUNE")
+    plans = [""] + (["persist_overlap=0", "persist=0"] if world > 1 else [])
+    fallback = []
+    for plan_i, plan_tune in enumerate(plans):
+        os.environ["DTR_TUNE"] = ",".join(filter(None, [base_tune or "", plan_tune]))
+        eng = Engine(spec, per_rank, weight_decay=wd, lr_schedule=sched, device=device,
+                     dist_ctx=ctx, global_batch=global_batch, bucket_mb=args.bucket_mb,
+                     seed=0, data_seed=1234 + ctx.rank, use_graph=use_graph,
+                     allreduce_dtype=args.allreduce_dtype, input_mode=input_mode)
+        dog = CommWatchdog(eng.comm, args.step_timeout, 3 * args.step_timeout).start()
+        eng.broadcast_parameters(0)
+        eng.fill_synthetic(seed=ctx.rank)
 
-    done = 0
-    if use_graph:
-        done = eng.capture(warmup=min(2, max(args.warmup, 1)))
-    for _ in range(max(args.warmup - done, 0)):
-        eng.step()
+        done = 0
+        if use_graph:
+            done = eng.capture(warmup=min(2, max(args.warmup, 1)))
+        for _ in range(max(args.warmup - done, 0)):
+            eng.step()
+            dog.beat()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.step()
+            dog.beat()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
         dog.beat()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
-        dog.beat()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    dog.beat()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    ctx.all_reduce_max(t)
-    elapsed = float(t.item())
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        ctx.all_reduce_max(t)
+        elapsed = float(t.item())
+        if ctx._agree(not eng.persist_error()) or plan_i == len(plans) - 1:
+            break
+        dog.stop()
+        fallback.append(f"{plans[plan_i] or 'default plan'}: persistent barrier timeout "
+                        f"on some rank")
+        print(f"bench.py: rank {ctx.rank}: {fallback[-1]}; measuring again with "
+              f"DTR_TUNE={plans[plan_i + 1]}", file=sys.stderr, flush=True)
+        del eng
+    if base_tune is None:
+        os.environ.pop("DTR_TUNE", None)
+    else:
+        os.environ["DTR_TUNE"] = base_tune
     m = eng.metrics()
     # per-phase timing, outside the timed region (not part of `value`)
     phases = None
@@ -281,6 +303,7 @@ def run_gpu(args, dataset, size, per_rank, global_batch, world):
                            if eng.persist else "per-layer plan"),
              "persist_off_reason": eng.persist_reason or None,
              "persist_overlap": bool(eng.persist_overlap),
+             "fallback": fallback or None,
              "cus": int(eng.nat.cu_count()), "cu_mask": cu_mask,
              "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2)}
     return ctx, elapsed, m, extra, phases

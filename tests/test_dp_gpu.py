@@ -199,6 +199,28 @@ def test_bench_two_ranks_persistent_cu_partition(gpu):
 
 
 @pytest.mark.gpu
+def test_bench_two_ranks_falls_back_after_a_persistent_fault(gpu):
+    """bench.py at world > 1: a persistent-step barrier timeout on ONE rank (rank 1's lost
+    workgroup, DTR_PRN_FAULT_BAR=3@1) is agreed over the process group and the job
+    measures again on the next plan down -- persistent without the overlap (which faults
+    again: the injection stays on), then the per-layer plan -- and reports that number
+    with the fallback chain instead of no number."""
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               DTR_TEST_FAULTS="1", DTR_PRN_FAULT_BAR="3@1", **CUP)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "10", "--warmup", "3",
+                        "--batch", "32"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    cfg = out["config"]
+    assert cfg["step_path"] == "per-layer plan", cfg
+    assert cfg["fallback"] and len(cfg["fallback"]) == 2, cfg
+    assert "persist_overlap=0" in cfg["fallback"][1], cfg
+    assert out["value"] > 0 and out["pg_world_size"] == 2, out
+
+
+@pytest.mark.gpu
 def test_fault_on_one_rank_fails_job_and_restarts_per_layer(gpu, tmp_path):
     """a grid-barrier timeout on a NON-chief rank (DTR_PRN_FAULT_BAR=3@1) must
     fail the whole job before the chief checkpoints the poisoned state: the faulting rank
