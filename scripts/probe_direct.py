@@ -22,6 +22,8 @@ from distributed_tensorflow_resnet_amd.ops import functional as fn  # noqa: E402
 
 BF = torch.bfloat16
 SHAPES = [(32, 16), (16, 32), (8, 64)]
+if os.environ.get("PROBE_SHAPES"):   # e.g. "56x64" (with DTR_TUNE=direct_wide=1)
+    SHAPES = [tuple(int(v) for v in t.split("x")) for t in os.environ["PROBE_SHAPES"].split(",")]
 NL = 6   # launches per chain
 
 
