@@ -73,6 +73,72 @@ def make_learnable_cifar(out_dir: str, n_train: int = 10000, n_test: int = 2000,
     return {"train": n_train, "test": n_test, "classes": num_classes, "dir": out_dir}
 
 
+def _imagenet_shard(args):
+    """One TFRecord shard of the learnable ImageNet-format task (worker of
+    make_learnable_imagenet): JPEG-encoded class templates under random shift,
+    brightness / contrast, a low-frequency distractor and per-pixel noise."""
+    import io
+
+    from PIL import Image
+
+    from ..utils import records
+
+    path, labels, templates, distract, seed, size, noise, shift = args
+    rng = np.random.default_rng(seed)
+    w = records.RecordWriter(path)
+    for lab in labels:
+        t = np.roll(templates[lab], tuple(rng.integers(-shift, shift + 1, 2)), axis=(1, 2))
+        d = distract[rng.integers(0, len(distract))]
+        img = (rng.uniform(100, 156) + rng.uniform(40, 80) * t + rng.uniform(0, 30) * d
+               + noise * rng.standard_normal(t.shape, dtype=np.float32))
+        arr = np.clip(np.rint(img), 0, 255).astype(np.uint8).transpose(1, 2, 0)
+        buf = io.BytesIO()
+        Image.fromarray(arr).save(buf, format="JPEG", quality=90)
+        w.write(records.make_example({"image/encoded": buf.getvalue(), "image/format": b"JPEG",
+                                      "image/class/label": int(lab) + 1}))
+    w.close()
+    return len(labels)
+
+
+def make_learnable_imagenet(out_dir: str, n_train: int = 25600, n_test: int = 5000,
+                            classes: int = 100, seed: int = 0, size: int = 256,
+                            noise: float = 30.0, shift: int = 32, separation: float = 0.5,
+                            shards: int = 16, workers: int = 8) -> dict:
+    """The ImageNet input format (train-%05d-of-01024 / validation-%05d-of-00128
+    TFRecord shards of tf.train.Example with JPEG `image/encoded` and a 1-based
+    `image/class/label`, data/imagenet.py) holding a learnable task: `classes` smooth
+    colour templates (6x6 noise upsampled to `size`), each (1 - separation) a field
+    common to all classes, under random shift, brightness / contrast, a distractor and
+    per-pixel noise.  The reference's VGG preprocessing then adds scale (shorter side
+    256-512) and crop jitter."""
+    import multiprocessing as mp
+
+    import torch
+
+    rng = np.random.default_rng(seed)
+    f = torch.from_numpy(rng.standard_normal((classes + 1, 3, 6, 6)).astype(np.float32))
+    up = torch.nn.functional.interpolate(f, size=(size, size), mode="bilinear",
+                                         align_corners=False)
+    up = (up / up.abs().amax(dim=(1, 2, 3), keepdim=True).clamp_min(1e-6)).numpy()
+    templates = ((1.0 - separation) * up[classes:] + separation * up[:classes]).astype(np.float32)
+    d = torch.nn.functional.interpolate(torch.from_numpy(rng.standard_normal((64, 3, 3, 3))
+                                                         .astype(np.float32)),
+                                        size=(size, size), mode="bilinear", align_corners=False)
+    distract = d.numpy()   # a bank of low-frequency distractors, one drawn per image
+    os.makedirs(out_dir, exist_ok=True)
+    jobs = []
+    for split, n, nsh, fmt in (("train", n_train, shards, "train-%05d-of-01024"),
+                               ("validation", n_test, max(1, shards // 4),
+                                "validation-%05d-of-00128")):
+        labels = rng.integers(0, classes, n)
+        for k, part in enumerate(np.array_split(labels, nsh)):
+            jobs.append((os.path.join(out_dir, fmt % k), part, templates, distract,
+                         seed * 100003 + len(jobs), size, noise, shift))
+    with mp.get_context("spawn").Pool(max(1, workers)) as pool:
+        done = sum(pool.map(_imagenet_shard, jobs))
+    return {"images": done, "classes": classes, "dir": out_dir}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -84,7 +150,19 @@ def main(argv=None):
     ap.add_argument("--shift", type=int, default=3, help="max template shift (pixels)")
     ap.add_argument("--separation", type=float, default=1.0,
                     help="class-template weight against a common field (1: none common)")
+    ap.add_argument("--imagenet", action="store_true",
+                    help="the ImageNet TFRecord/JPEG format (make_learnable_imagenet; --classes, "
+                         "--workers; noise / shift / separation default 30 / 32 / 0.5)")
+    ap.add_argument("--classes", type=int, default=100)
+    ap.add_argument("--workers", type=int, default=8)
     a = ap.parse_args(argv)
+    if a.imagenet:
+        kw = {k: v for k, v in (("noise", a.noise), ("shift", a.shift),
+                                ("separation", a.separation))
+              if v != ap.get_default(k)}
+        print(make_learnable_imagenet(a.out_dir, a.train, a.test, a.classes, a.seed,
+                                      workers=a.workers, **kw))
+        return
     print(make_learnable_cifar(a.out_dir, a.train, a.test, a.seed, noise=a.noise, shift=a.shift,
                                separation=a.separation))
 

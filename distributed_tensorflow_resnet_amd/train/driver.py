@@ -27,7 +27,8 @@ from ..utils.flags import build_parser, warn_unsupported
 from ..utils.records import EventWriter
 from . import hooks as H
 from .backends import make_backend
-from .engine import PersistentStepError, cifar_lr_schedule, imagenet_lr_schedule, scaled
+from .engine import (PersistentStepError, cifar_lr_schedule, imagenet_lr_schedule,
+                     lr_values_scaled, scaled)
 from .evaluator import SidecarEvaluator, make_inference
 from .session import TrainingSession, run_training
 
@@ -173,7 +174,7 @@ def main(argv=None, kind: str = "cifar") -> int:
     dp_ctx = None if flags.variable_update == "independent" else ctx
     rank, world = ctx.rank, ctx.world_size
     sched = cifar_lr_schedule() if spec.dataset.startswith("cifar") else imagenet_lr_schedule()
-    sched = scaled(sched, flags.lr_schedule_scale)
+    sched = lr_values_scaled(scaled(sched, flags.lr_schedule_scale), flags.lr_value_scale)
     # real ImageNet on the GPU: uint8 crops from the workers, flip/mean/bf16 pack on device
     u8 = device == "gpu" and spec.dataset == "imagenet" and not flags.synthetic
     backend = make_backend(spec, flags.batch_size, device=device, weight_decay=flags.weight_decay,

@@ -151,6 +151,14 @@ def scaled(s: LRSchedule, factor: float) -> LRSchedule:
                       int(round(s.warm_steps * factor)), s.warm_from, s.warm_to)
 
 
+def lr_values_scaled(s: LRSchedule, factor: float) -> LRSchedule:
+    """The same schedule with every LR value (and the warm-up's ends) x factor."""
+    if factor == 1.0:
+        return s
+    return LRSchedule(s.init * factor, list(s.bounds), [v * factor for v in s.values],
+                      s.warm_steps, s.warm_from * factor, s.warm_to * factor)
+
+
 def constant_lr(lr: float) -> LRSchedule:
     return LRSchedule(lr, [], [lr])
 

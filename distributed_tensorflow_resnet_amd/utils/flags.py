@@ -167,6 +167,10 @@ def build_parser(kind: str = "cifar", description: str | None = None) -> FlagPar
     p.add_argument("--lr_schedule_scale", type=float, default=1.0,
                    help="Multiply the LR schedule's step boundaries (and warm-up) by this "
                         "factor: compressed schedules for short runs (convergence tests).")
+    p.add_argument("--lr_value_scale", type=float, default=1.0,
+                   help="Multiply every LR value of the schedule (and its warm-up) by this "
+                        "factor: the linear scaling rule when the global batch differs from "
+                        "the reference's (ImageNet: 0.4 for 8 x 128 images).")
     p.add_argument("--allreduce_dtype", default="fp32", choices=("fp32", "bf16"),
                    help="Gradient all-reduce precision: bf16 halves the bytes on xGMI (fp32 "
                         "master weights and optimizer are unchanged).")

@@ -342,3 +342,27 @@ def test_step_watchdog_fires_on_hang_only():
     _t.sleep(0.6)                  # a hung step
     assert h.fired and exits == [StepWatchdogHook.EXIT_CODE]
     h.end(None)
+
+
+def test_learnable_imagenet_records_and_lr_value_scale(tmp_path):
+    """data/learnable.py --imagenet writes the reference's ImageNet input format (JPEG
+    TFRecord shards, 1-based labels) that data/imagenet.input_fn reads back; the CLI's
+    --lr_value_scale scales every value of the schedule, warm-up included."""
+    from distributed_tensorflow_resnet_amd.data import imagenet
+    from distributed_tensorflow_resnet_amd.data.learnable import make_learnable_imagenet
+    from distributed_tensorflow_resnet_amd.train.engine import (imagenet_lr_schedule,
+                                                                lr_values_scaled)
+
+    d = str(tmp_path / "in")
+    info = make_learnable_imagenet(d, 96, 32, classes=5, shards=2, workers=2, size=96)
+    assert info["images"] == 128
+    xs, ys = [], []
+    for x, y in imagenet.input_fn(True, d, 16, workers=0, u8=True, image_size=64):
+        xs.append(x)
+        ys.append(y)
+    assert sum(len(y) for y in ys) == 96 and xs[0].shape == (16, 64, 64, 3)
+    assert int(min(y.min() for y in ys)) >= 0 and int(max(y.max() for y in ys)) < 5
+    s = imagenet_lr_schedule()
+    h = lr_values_scaled(s, 0.125)
+    for step in (0, 100, 6240, 50000, 120000):
+        assert abs(h.at(step) - 0.125 * s.at(step)) < 1e-9, step
