@@ -38,6 +38,22 @@ class GPUInference:
 
     def run(self, images, labels):
         raw = images.dtype == torch.uint8
+        n, full = images.shape[0], self.engine.N
+        if n < full:
+            # a short last batch (an eval pipeline's remainder, e.g. several loader
+            # workers over 390-image ImageNet validation shards): the static plan runs
+            # the full batch with the first image repeated, and the loss / correct count
+            # are taken from the valid rows' probabilities
+            pad = full - n
+            images = torch.cat([images, images[:1].expand(pad, *images.shape[1:])])
+            labels_p = torch.cat([labels, labels[:1].expand(pad)])
+            _, _, probs = self.plan.run(images.to(self.engine.device),
+                                        labels_p.to(self.engine.device), raw_u8=raw)
+            p = probs[:n].float()
+            y = labels.to(p.device).long()
+            loss = float(-torch.log(p.gather(1, y[:, None]).clamp_min(1e-30)).sum())
+            correct = float((p.argmax(1) == y).sum())
+            return loss, correct, probs[:n]
         loss, correct, probs = self.plan.run(images.to(self.engine.device),
                                              labels.to(self.engine.device), raw_u8=raw)
         return loss, correct, probs

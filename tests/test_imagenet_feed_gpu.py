@@ -66,3 +66,22 @@ def test_engine_trains_from_u8_crops(gpu):
     assert int(eng.gstep.item()) == 12
     assert all(torch.isfinite(torch.tensor(losses)))
     assert min(losses[-3:]) < losses[0]     # memorises the fixed batch
+
+
+def test_eval_short_last_batch(gpu):
+    """The evaluator's static plan scores a short last batch (an eval loader's remainder:
+    several workers over 390-image ImageNet validation shards) from the valid rows only:
+    loss and correct count equal those rows' share of a full batch."""
+    from distributed_tensorflow_resnet_amd.models.spec import cifar_spec
+    from distributed_tensorflow_resnet_amd.train.evaluator import GPUInference
+
+    torch.manual_seed(3)
+    inf = GPUInference(cifar_spec(8), 8, device=gpu)
+    x = torch.randn(8, 32, 32, 3) * 60 + 120
+    y = torch.randint(0, 10, (8,))
+    _, _, probs = inf.run(x, y)
+    p = probs[:5].float().cpu()
+    loss5, corr5, _ = inf.run(x[:5], y[:5])
+    ref_loss = float(-torch.log(p.gather(1, y[:5, None]).clamp_min(1e-30)).sum())
+    assert abs(loss5 - ref_loss) < 1e-3 * max(1.0, abs(ref_loss))
+    assert corr5 == float((p.argmax(1) == y[:5]).sum())
