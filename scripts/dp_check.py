@@ -38,7 +38,9 @@ def main() -> int:
     dev = torch.device("cuda", local_device_index())
     ctx = DistContext(device=dev)
     world, rank = ctx.world_size, ctx.rank
-    spec = build_spec("cifar10", size)
+    # DP_CHECK_DATASET=imagenet: the ImageNet per-layer plan (side stream + comm-stream
+    # buckets), e.g. ResNet-50 at 16 images per rank with DP_CHECK_BUCKET_MB=25
+    spec = build_spec(os.environ.get("DP_CHECK_DATASET", "cifar10"), size)
     ar_dtype = os.environ.get("DP_CHECK_ALLREDUCE", "fp32")
     kw = dict(weight_decay=2e-4, lr_schedule=cifar_lr_schedule(), device=dev,
               global_batch=per_rank * world, seed=0, data_seed=1234 + rank)

@@ -183,6 +183,21 @@ def test_persistent_overlap_two_ranks_cu_partition(gpu, dtype, port):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype,port", [("fp32", 29753), ("bf16", 29754)])
+def test_imagenet_plan_two_ranks_cu_partition(gpu, dtype, port):
+    """The ImageNet per-layer plan at world 2 (ResNet-50, 16 images per rank, CU halves,
+    shm transport): main + side streams and four 25 MB comm-stream buckets; the all-reduced
+    gradient is the exact rank-order sum and the replicas stay identical."""
+    r = _torchrun(["scripts/dp_check.py"], port, timeout=600,
+                  extra_env=dict(CUP, DP_CHECK_DATASET="imagenet", DP_CHECK_SIZE="50",
+                                 DP_CHECK_BATCH="16", DP_CHECK_BUCKET_MB="25",
+                                 DP_CHECK_STEPS="10", DP_CHECK_ALLREDUCE=dtype))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "DP_CHECK_OK" in r.stdout, r.stdout[-3000:]
+    assert "allreduce_ops=4" in r.stdout and "step_path=per-layer" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_persistent_cu_partition(gpu):
     """`bench.py --gpus 2` on the persistent step at world 2 (CU halves, shm transport)."""
     env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **CUP)
