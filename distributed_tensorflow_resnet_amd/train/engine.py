@@ -334,8 +334,10 @@ class Engine:
         self.persist = reason == ""
         # world > 1 (or a forced communicator): the gradient buckets' reduces and
         # all-reduces overlap the persistent backward launch (tune persist_overlap)
-        self.persist_overlap = (self.persist and self.comm is not None
-                                and self.persist_overlap_tune)
+        self.persist_overlap = self.persist and _persist.overlap_planned(self)
+        if self.persist and self.dist is not None and self.dist.active:
+            # one plan shape on every rank (3 bucket all-reduces or 1)
+            self.persist_overlap = self.dist._agree(self.persist_overlap)
         self.prn = _persist.PersistStep(self) if self.persist else None
         self.plan = self.nat.Plan()
         self._keep = []   # tensors referenced by the plan

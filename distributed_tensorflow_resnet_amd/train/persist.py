@@ -141,9 +141,18 @@ def check(eng) -> str:
 
 
 def overlap_planned(eng) -> bool:
-    """Whether the engine asks for the overlap plan (a communicator and tune
-    persist_overlap): its backward grid leaves OVERLAP_RESERVE_CUS to the comm stream."""
-    return eng.comm is not None and bool(getattr(eng, "persist_overlap_tune", False))
+    """Whether the engine takes the overlap plan: a communicator, tune persist_overlap,
+    and a backward slicing the OVERLAP_RESERVE_CUS left to the comm stream does not
+    reduce.  Where the reserve would cost slices (48 / 56 images on 256 CUs: 4 -> 2; 97 to
+    112: 2 -> 1) the buckets go after the backward instead: the world-1 RCCL rehearsal
+    over no communicator (`scripts/comm_step_time.py`, round 6) measured overlap / after
+    +5.2 / +6.1 us at bs16, +5.3 / +6.3 bs32, +4.4 / +6.5 bs40, +10.1 / +11.4 bs64, but
+    +38.9 / +11.0 at bs48 and +18.2 / +7.2 at bs96."""
+    if eng.comm is None or not bool(getattr(eng, "persist_overlap_tune", False)):
+        return False
+    cus = eng.nat.cu_count()
+    return (slices_for(eng.N, cus - OVERLAP_RESERVE_CUS, eng.persist_slices)
+            == slices_for(eng.N, cus, eng.persist_slices))
 
 
 def supported(eng) -> bool:

@@ -81,6 +81,24 @@ def test_native_comm_single_rank_is_identity(gpu, monkeypatch, persist):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,overlap", [(16, True), (48, False), (64, True), (96, False)])
+def test_overlap_plan_only_where_the_reserve_costs_no_slices(gpu, monkeypatch, N, overlap):
+    """The persistent overlap plan leaves 48 CUs to the comm stream; where that would cut
+    the backward's slices (48 images: 4 -> 2, 96: 2 -> 1) the buckets go after the
+    backward instead (train/persist.py overlap_planned)."""
+    from distributed_tensorflow_resnet_amd.models.spec import build_spec
+    from distributed_tensorflow_resnet_amd.train.engine import Engine, cifar_lr_schedule
+
+    monkeypatch.setenv("DTR_TUNE", "persist=1")
+    eng = Engine(build_spec("cifar10", 8), N, weight_decay=2e-4, lr_schedule=cifar_lr_schedule(),
+                 device=gpu, native_comm=True)
+    assert eng.persist and eng.persist_overlap == overlap
+    assert eng.comm_info()["allreduce_ops"] == (3 if overlap else 1)
+    if eng.nat.cu_count() == 256:
+        assert eng.prn.P == {16: 4, 48: 4, 64: 2, 96: 2}[N]
+
+
+@pytest.mark.gpu
 def test_native_comm_bf16_exchange(gpu):
     ref, eng = _engines(gpu, allreduce_dtype="bf16")
     assert eng.comm_info()["allreduce_bytes"] == 2 * eng.params.n_train
