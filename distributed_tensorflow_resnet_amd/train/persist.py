@@ -151,8 +151,11 @@ def overlap_planned(eng) -> bool:
     if eng.comm is None or not bool(getattr(eng, "persist_overlap_tune", False)):
         return False
     cus = eng.nat.cu_count()
-    return (slices_for(eng.N, cus - OVERLAP_RESERVE_CUS, eng.persist_slices)
-            == slices_for(eng.N, cus, eng.persist_slices))
+    p = slices_for(eng.N, cus - OVERLAP_RESERVE_CUS, eng.persist_slices)
+    # (and the reserved grid still leaves its 16 weight-gradient CUs: a rank on a quarter
+    # of the CUs takes the persistent step with the buckets after the backward instead)
+    return (p == slices_for(eng.N, cus, eng.persist_slices)
+            and eng.N * p + 16 + OVERLAP_RESERVE_CUS <= cus)
 
 
 def supported(eng) -> bool:

@@ -214,6 +214,24 @@ def test_bench_two_ranks_persistent_cu_partition(gpu):
 
 
 @pytest.mark.gpu
+def test_bench_four_ranks_persistent_cu_quarters(gpu):
+    """`bench.py --gpus 4` with four ranks on CU quarters (64 CUs each, 32 images per rank):
+    the overlap plan's 48-CU reserve does not fit beside the grid, so each rank takes the
+    persistent step with the buckets after the backward (train/persist.py overlap_planned)
+    rather than the per-layer plan."""
+    env = dict(os.environ, DTR_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               **dict(SHM, DTR_CU_PARTITION="4"))
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "20", "--warmup", "5"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    cfg = out["config"]
+    assert out["pg_world_size"] == 4 and cfg["per_gpu_batch"] == 32 and cfg["cus"] == 64, out
+    assert cfg["step_path"].startswith("persistent") and not cfg["persist_overlap"], cfg
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_falls_back_after_a_persistent_fault(gpu):
     """bench.py at world > 1: a persistent-step barrier timeout on ONE rank (rank 1's lost
     workgroup, DTR_PRN_FAULT_BAR=3@1) is agreed over the process group and the job
