@@ -145,9 +145,12 @@ __device__ __forceinline__ bf16x8 affine_relu8_sel(bf16x8 v, const f32x4& s0, co
 
 // Host: conv epilogue / dh stores write-through (sc1).  tune wt_store = 1 forces it on
 // for every conv, 0 off; -1 (default): the direct 3x3 convs decide by output size
-// (wt_store_direct), the implicit-GEMM convs store normally.
+// (wt_store_direct), the implicit-GEMM / ring convs write through (round 6, RN50 bs128
+// step, four interleaved rounds: 10.316-10.325 -> 10.260-10.286 ms -- their outputs are
+// read next by kernels on other CUs / XCDs while the side stream's weight gradients
+// fill the L2s; CIFAR per-layer bs128 / bs256 and RN101 bs256 unchanged within noise).
 inline int wt_store_mode() { return (int)tune(T_WT_STORE); }
-inline bool wt_store_enabled() { return wt_store_mode() == 1; }
+inline bool wt_store_enabled() { return wt_store_mode() != 0; }
 
 // Compute units this process may dispatch to on the current device, queried once per
 // device (persistent-grid sizing on the launch path without a runtime query per launch):
