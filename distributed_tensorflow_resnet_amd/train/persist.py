@@ -57,9 +57,9 @@ OVERLAP_RESERVE_CUS = 48
 # stage 2 (64 channels) + the final BN + dense, stage 1, stage 0 + the stem
 BUCKET_OF_STAGE = (2, 1, 0)
 
-# every supported per-rank batch (MI355X, CIFAR RN50 one-GPU step, round-5 build vs the
-# per-layer engine: bs16 0.558 vs 0.926 ms, bs32 0.576 vs 0.964, bs64 0.647 vs 1.084,
-# bs128 (1 slice) 0.731-0.740 vs 1.261; profiles/final_check_r05.md)
+# every supported per-rank batch (MI355X, CIFAR RN50 one-GPU step, round-6 build vs the
+# per-layer engine: bs16 0.554-0.556 vs 0.926 ms, bs32 0.565-0.570 vs 0.964, bs64
+# 0.638-0.641 vs 1.084, bs128 (1 slice) 0.733-0.743 vs 1.299; profiles/final_check_r06.md)
 AUTO_MAX_BATCH = 240
 
 
@@ -67,8 +67,9 @@ def slices_for(N: int, cus: int, override: int = -1) -> int:
     """Row slices (workgroups) per image of the backward, of the ``cus`` the backward grid
     may fill (the overlap plan's reserve already taken out): 4 while 4N slices leave 32
     CUs for the weight gradients (56 images on 256 CUs), 2 while 2N leave 64 (96
-    images), else -- small budgets -- the most slices that leave 16, else 1.  More slices shorten each layer, more arrivals lengthen each barrier; with
-    the 64-shard arrival counters of round 6 (MI355X, CIFAR RN50 step ms, two runs each;
+    images), else -- small budgets -- the most slices that leave 16, else 1.  More
+    slices shorten each layer, more arrivals lengthen each barrier; with the 64-shard
+    arrival counters of round 6 (MI355X, CIFAR RN50 step ms, two runs each;
     forward slicing fixed: bs40 0.594-0.600 at 4 / 0.626-0.632 at 2; bs48 0.607-0.608 /
     0.634; bs56 0.626-0.628 / 0.636-0.638; bs64 0.639-0.641 at 2 / 0.673-0.675 at 1;
     bs80 0.654 / 0.680-0.687; bs96 0.675-0.676 / 0.695-0.701; bs112 0.735-0.737 /
